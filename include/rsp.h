@@ -1,0 +1,216 @@
+/*
+ * rsp.h -- C-ABI of the MI355X radar signal-processing library (librsp.so).
+ *
+ * Drop-in boundary for the per-frame chain of the MATLAB reference
+ * (XuZerui2023/Radar-Signal-Simulation-and-Target-Detection, Simulation/):
+ *
+ *   final_targets = fun_process_single_frame(targets, config, cfar_params,
+ *                       cluster_params, precomputed_data, frame_idx)
+ *                                              (fun_process_single_frame.m:13)
+ *   [MTD_results, PC_results] = process_stage2_mtd(iq_data, angle, config)
+ *                                              (process_stage2_mtd.m:1)
+ *
+ * The reference has no FFI; these entry points are what a MEX gateway or a
+ * MATLAB `loadlibrary`/`calllib` binding of that path binds.
+ * Plain C types only: pointers, sizes, int32 status codes.
+ *
+ * Conventions (mirroring MATLAB so a MEX gateway passes mxArray data as is):
+ *   - complex arrays are interleaved (re, im) doubles (mxGetComplexDoubles,
+ *     R2018a API) or interleaved floats (RSP_C64);
+ *   - matrices are column-major; the echo cube is [P x N x C] (pulse fastest),
+ *     range-Doppler maps [P x G x B], CFAR maps [P x G x (B-1)];
+ *   - indices reported to the caller are 1-based (fun_process_single_frame.m:220);
+ *   - segment starts in rsp_precomputed are 1-based (v8:116-117,130).
+ * Errors: every function returns RSP_OK (0) or a negative rsp_status; the
+ * message of the last failure on the calling thread is rsp_last_error().
+ * Threading: a plan is not thread-safe; use one plan per host thread (MATLAB
+ * parfor workers are processes, each with its own plan).
+ */
+#ifndef RSP_H
+#define RSP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSP_ABI_VERSION 1
+
+typedef enum rsp_status {
+    RSP_OK = 0,
+    RSP_ERR_INVALID = -1,      /* bad argument / inconsistent config            */
+    RSP_ERR_UNSUPPORTED = -2,  /* config outside what the kernels implement      */
+    RSP_ERR_DEVICE = -3,       /* HIP runtime failure                            */
+    RSP_ERR_NOMEM = -4,        /* device or host allocation failed               */
+    RSP_ERR_OVERFLOW = -5      /* detection list longer than the plan's capacity */
+} rsp_status;
+
+typedef enum rsp_dtype {
+    RSP_C64 = 1,   /* interleaved complex float  */
+    RSP_C128 = 2   /* interleaved complex double (MATLAB) */
+} rsp_dtype;
+
+typedef enum rsp_layout {
+    RSP_LAYOUT_PNC = 0   /* MATLAB column-major [P x N x C]: index m + P*(n + N*c) */
+} rsp_layout;
+
+/* config.Sig_Config + config.Array (main_simulate_echoes_with_array_v8.m:54-69). */
+typedef struct rsp_sig_config {
+    double c;                 /* Sig_Config.c                       */
+    double fs;                /* Sig_Config.fs                      */
+    double fc;                /* Sig_Config.fc                      */
+    double prt;               /* Sig_Config.prt (s)                 */
+    double wavelength;        /* Sig_Config.wavelength              */
+    double element_spacing;   /* Array.element_spacing (m)          */
+    int32_t prtNum;           /* P: pulses per frame                */
+    int32_t point_PRT;        /* N: fast-time samples per pulse     */
+    int32_t channel_num;      /* C                                  */
+    int32_t beam_num;         /* B                                  */
+} rsp_sig_config;
+
+/* cfar_params (v8:45-47). Only 'GOCA' exists in the reference. */
+typedef struct rsp_cfar_params {
+    int32_t refCells_V, guardCells_V, refCells_R, guardCells_R;
+    double T_CFAR;
+} rsp_cfar_params;
+
+/* cluster_params (v8:49-51). */
+typedef struct rsp_cluster_params {
+    double max_range_sep, max_vel_sep, max_angle_sep;
+} rsp_cluster_params;
+
+/* precomputed_data (v8:79-155).  Arrays are borrowed for rsp_plan_create only. */
+typedef struct rsp_precomputed {
+    const double* tx_pulse;            /* complex, point_PRT entries (synthesis; may be NULL) */
+    double P_signal_unscaled;
+    const double* DBF_coeffs_data_C;   /* complex, B x C column-major                        */
+    const double* MF_narrow;           /* real FIR taps                                      */
+    int32_t n_MF_narrow;
+    int32_t fir_delay;
+    const double* MF_medium_fft;       /* complex, N_fft_med entries                          */
+    int32_t N_fft_med;
+    const double* MF_long_fft;         /* complex, N_fft_long entries                         */
+    int32_t N_fft_long;
+    int32_t N_gate_narrow, N_gate_medium, N_gate_long, N_total_gate;
+    int32_t seg_start_narrow, seg_start_medium, seg_start_long;   /* 1-based */
+    const double* MTD_win;             /* prtNum                                              */
+    const double* range_axis;          /* N_total_gate                                        */
+    const double* velocity_axis;       /* prtNum                                              */
+    double deltaR, deltaV;
+    const double* beam_angles_deg;     /* beam_num                                            */
+    const double* k_slopes_LUT;        /* beam_num - 1                                        */
+} rsp_precomputed;
+
+/* targets(k) of the driver (v8:29-37). */
+typedef struct rsp_target_in {
+    double Range, Velocity, ElevationAngle, SNR_dB;
+} rsp_target_in;
+
+/* One entry of final_targets / intra_beam_targets (fun_process_single_frame.m:393-406). */
+typedef struct rsp_target {
+    double Range, Velocity, Angle, Power;
+} rsp_target;
+
+/* One row of all_raw_detections (fsf:220, 1-based v/r/pair, the CFAR map value)
+ * together with its S9 estimate (fsf:293-297). */
+typedef struct rsp_detection {
+    int32_t v_idx, r_idx, pair_idx, reserved;
+    double amp;
+    double Range, Velocity, Angle;
+} rsp_detection;
+
+/* Caller-owned outputs of one frame.  Any pointer may be NULL (not produced).
+ * Sizes from rsp_query_sizes. */
+typedef struct rsp_frame_out {
+    double* rdm;              /* complex, [P x G x B] column-major (rdm_13beam, fsf:135)        */
+    double* cfar_maps;        /* real, [P x G x (B-1)] (rdm_for_cfar_all, fsf:187)             */
+    rsp_detection* dets;      /* parameterized detections in reference order                   */
+    int32_t dets_cap;
+    int32_t n_dets;           /* out                                                           */
+    rsp_target* targets;      /* final_targets                                                 */
+    int32_t targets_cap;
+    int32_t n_targets;        /* out                                                           */
+} rsp_frame_out;
+
+typedef struct rsp_sizes {
+    int64_t cube_elems;       /* P*N*C complex samples                      */
+    int64_t rdm_elems;        /* P*G*B                                      */
+    int64_t cfar_map_elems;   /* P*G*(B-1)                                  */
+    int32_t P, N, C, B, G;
+    int32_t used_samples;     /* fast-time samples the chain actually reads */
+    int32_t max_detections;   /* per frame device capacity                  */
+    int32_t n_stages;         /* device stages (for rsp_profile_stages)     */
+} rsp_sizes;
+
+typedef struct rsp_plan rsp_plan;
+
+int32_t rsp_abi_version(void);
+const char* rsp_last_error(void);
+
+/* Build a plan on HIP device `device`: uploads DBF weights, FIR taps, matched-filter
+ * spectra (re-blocked for overlap-save), MTD window, axes, angles, K-LUT.
+ * `frames_per_launch` (1..8) frames are batched into each kernel launch by the
+ * queue interface; rsp_process_* always run one frame. */
+int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar,
+                        const rsp_cluster_params* cluster, const rsp_precomputed* pre,
+                        int32_t device, int32_t frames_per_launch, rsp_plan** out);
+int32_t rsp_plan_destroy(rsp_plan* plan);
+int32_t rsp_query_sizes(const rsp_plan* plan, rsp_sizes* out);
+
+/* Cube-in path: S5..S11 of fun_process_single_frame on one host cube
+ * (layout RSP_LAYOUT_PNC, dtype RSP_C64 or RSP_C128).  Synchronous. */
+int32_t rsp_process_cube(rsp_plan* plan, const void* cube, int32_t dtype, int32_t layout,
+                         int32_t frame_idx, rsp_frame_out* out);
+
+/* Reference-signature path (fsf:13): S4 echo synthesis + S4.1 Philox noise
+ * (seed, frame_idx) on the device, then S5..S11.  Needs tx_pulse in the plan. */
+int32_t rsp_process_targets(rsp_plan* plan, const rsp_target_in* targets, int32_t n_targets,
+                            int32_t frame_idx, uint64_t seed, double p_noise, rsp_frame_out* out);
+
+/* Synthesise (S4 + S4.1) one cube on the device into `d_cube` (complex64, PNC layout,
+ * device pointer with cube_elems entries).  Enqueued on the plan's stream 0. */
+int32_t rsp_synthesize_device(rsp_plan* plan, const rsp_target_in* targets, int32_t n_targets,
+                              int32_t frame_idx, uint64_t seed, double p_noise, void* d_cube);
+
+/* ---- device-resident queue (throughput path) ----
+ * rsp_enqueue_device: process a complex64 PNC cube already resident in device
+ * memory.  Frames are batched frames_per_launch at a time and alternate over the
+ * plan's lanes (streams); detections come back asynchronously and are clustered
+ * on the host.  rsp_drain waits for everything queued.  Results are kept in
+ * enqueue order until rsp_results_clear. */
+int32_t rsp_enqueue_device(rsp_plan* plan, const void* d_cube, int32_t frame_idx);
+int32_t rsp_drain(rsp_plan* plan);
+int32_t rsp_results_count(const rsp_plan* plan, int32_t* n_frames, int64_t* n_targets);
+int32_t rsp_results_get(const rsp_plan* plan, int32_t i, int32_t* frame_idx, rsp_target* targets,
+                        int32_t cap, int32_t* n_targets, int32_t* n_dets);
+int32_t rsp_results_clear(rsp_plan* plan);
+
+/* Stage-2 path (process_stage2_mtd.m:1): already-beamformed fast-time data
+ * iq_data [P x N x B] (PNC layout with B beams) -> PC_results and MTD_results,
+ * both complex [P x G x B] column-major (either may be NULL).  The reference's
+ * fun_MTD_produce is un-vendored; this backs it with fsf S6 + S7. */
+int32_t rsp_process_stage2(rsp_plan* plan, const void* iq_beams, int32_t dtype,
+                           double* mtd_out, double* pc_out);
+
+/* ---- measurement ----
+ * Time each device stage `iters` times on the plan's stream with HIP events over a
+ * device-resident complex64 cube; ms_out[i] = average ms per launch of stage i
+ * (one frame per launch).  bytes_out[i] = algorithmic HBM bytes per launch.
+ * Stage names via rsp_stage_name. */
+int32_t rsp_profile_stages(rsp_plan* plan, const void* d_cube, int32_t iters, float* ms_out,
+                           int64_t* bytes_out, int32_t cap);
+const char* rsp_stage_name(int32_t stage);
+
+/* Device memory helpers (so hosts without a GPU runtime binding can stage cubes). */
+int32_t rsp_device_alloc(rsp_plan* plan, int64_t bytes, void** d_ptr);
+int32_t rsp_device_free(rsp_plan* plan, void* d_ptr);
+int32_t rsp_device_upload(rsp_plan* plan, void* d_dst, const void* h_src, int64_t bytes);
+int32_t rsp_device_download(rsp_plan* plan, void* h_dst, const void* d_src, int64_t bytes);
+int32_t rsp_device_sync(rsp_plan* plan);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSP_H */

@@ -1,0 +1,91 @@
+// rsp_internal.h -- shared host/device descriptors of librsp (not part of the C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define RSP_MAX_F 8          // frames batched per launch
+#define RSP_K2_POINTS 4096   // complex points per pulse-compression workgroup
+#define RSP_THREADS 256
+
+// Device record of one CFAR detection + its S9 estimate; layout == rsp_detection.
+struct DevDet {
+    int32_t v_idx, r_idx, pair_idx, reserved;   // 1-based like fsf:220
+    double amp, range, velocity, angle;
+};
+
+// Pulse-compression segment (fsf:105-126).  Output gates [ga, gb) of the stitched
+// row come from this segment.  x~(n) = x(n) for lo_eff <= n <= hi, else 0, where
+// [lo, hi] is the window of samples that reach a kept gate (plan-time analysis).
+struct SegDesc {
+    int type;        // 0 = direct FIR (narrow, fsf:111-112), 1 = FFT overlap-save (fsf:115-120)
+    int ga, gb;      // stitched gate range
+    int seg_lo;      // 0-based first sample of the segment (seg_start - 1)
+    int lo, hi;      // needed sample window (0-based, inclusive), lo >= seg_lo
+    int off;         // compacted sample index of `lo`
+    // direct FIR: y[g] = sum_j h[j] x~(seg_lo + k - j), k = (g + delay) mod Ls
+    int ntaps, delay, Ls, taps_off;
+    // FFT overlap-save: y[g] = sum_{j<Lh} h[j] x~(seg_lo + g - j), block size M, V = M-Lh+1 valid
+    int Lh, M, logM, V, nblocks, H_off, tw_off;
+    int nrad, rad[8];
+    int rows_per_wg;
+};
+
+// One group of pulse-compression workgroups: segment `seg`, overlap-save block `blk`.
+struct K2Job {
+    int seg, blk, wg_begin, wg_count;
+};
+
+struct Geometry {
+    int C, B, P, N, G;
+    int NT, nU, ntiles, Ppad;
+    int pow2P, logP, nradP, radP[8];
+    int nseg, njobs, nwg_k2;
+    int cfar_RT, cfar_hR, cfar_W;
+    int refR, guardR, refV, guardV;
+    float T;
+    int max_dets;
+};
+
+struct FramePtrs {
+    const float2* in[RSP_MAX_F];   // K1 input cube (PNC) or beam cube
+    float2* z[RSP_MAX_F];          // compacted Doppler-domain rows
+    float2* rdm[RSP_MAX_F];        // [B][P][G]
+    DevDet* dets[RSP_MAX_F];
+    int* count[RSP_MAX_F];
+};
+
+struct DevConsts {
+    const float2* Wc;        // conj(W) [B][C]
+    const float* win;        // MTD window [P]
+    const float2* twP;       // W_P^i table
+    const int* nof;          // compacted index -> sample index (-1 = pad)
+    const SegDesc* segs;
+    const K2Job* jobs;
+    const float* taps;
+    const float2* H;         // overlap-save spectra, 1/M scaled
+    const float2* twM;       // W_M tables
+    const double* range_axis;
+    const double* velocity_axis;
+    const double* beam_angles;
+    const double* klut;
+    double deltaR, deltaV;
+};
+
+struct SynthTarget {          // per-target constants of S4 (fsf:51-73), host-computed
+    int delay;                // delay_samples
+    double amp;
+    double fd_prt;            // doppler_freq * prt   (phase per pulse / 2pi)
+    double dphi;              // channel phase step (rad)
+};
+
+// Launchers (rsp_kernels.hip).  `mode` bits for K1: 1 = apply DBF, 2 = apply MTD.
+hipError_t launch_k1(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int mode,
+                     int ch_in, hipStream_t s);
+hipError_t launch_k2(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int rows,
+                     hipStream_t s);
+hipError_t launch_k3(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, hipStream_t s);
+hipError_t launch_mtd_cols(const Geometry& g, const DevConsts& k, const float2* pc, float2* rdm,
+                           hipStream_t s);
+hipError_t launch_synth(const Geometry& g, const double* tx, const SynthTarget* tg, int nt,
+                        int frame_idx, uint64_t seed, double noise_scale, float2* cube,
+                        hipStream_t s);

@@ -1,0 +1,860 @@
+// rsp_plan.cpp -- host runtime of librsp: plan construction (geometry analysis of the
+// reference's precomputed_data), the C-ABI of include/rsp.h, the device-resident frame
+// queue, and the host stages S10/S11 (two-level BFS clustering, fsf:302-407).
+#include "rsp.h"
+#include "rsp_internal.h"
+
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <string>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                            \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess)                                                                   \
+            return fail(RSP_ERR_DEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                        __FILE__, __LINE__);                                                    \
+    } while (0)
+
+using cd = std::complex<double>;
+
+bool is_pow2(int x) { return x > 0 && (x & (x - 1)) == 0; }
+int ilog2i(int x) { int l = 0; while ((1 << l) < x) ++l; return l; }
+
+// In-place double FFT (sign -1 forward, +1 inverse, unscaled); O(n^2) DFT if n is not 2^k.
+void fft_d(std::vector<cd>& a, int sign) {
+    const int n = (int)a.size();
+    if (!is_pow2(n)) {
+        std::vector<cd> o(n);
+        for (int k = 0; k < n; ++k) {
+            cd s = 0;
+            for (int t = 0; t < n; ++t) s += a[t] * std::polar(1.0, sign * 2.0 * M_PI * ((double)((int64_t)t * k % n)) / n);
+            o[k] = s;
+        }
+        a.swap(o);
+        return;
+    }
+    for (int i = 1, j = 0; i < n; ++i) {
+        int bit = n >> 1;
+        for (; j & bit; bit >>= 1) j ^= bit;
+        j ^= bit;
+        if (i < j) std::swap(a[i], a[j]);
+    }
+    for (int len = 2; len <= n; len <<= 1) {
+        for (int i = 0; i < n; i += len) {
+            for (int k = 0; k < len / 2; ++k) {
+                const cd w = std::polar(1.0, sign * 2.0 * M_PI * k / len);
+                const cd u = a[i + k], v = a[i + k + len / 2] * w;
+                a[i + k] = u + v;
+                a[i + k + len / 2] = u - v;
+            }
+        }
+    }
+}
+
+double mround(double x) { return x < 0 ? -std::floor(-x + 0.5) : std::floor(x + 0.5); }
+
+struct Lane {
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    float2* z = nullptr;        // F frames
+    float2* rdm = nullptr;      // F frames
+    DevDet* dets = nullptr;     // F x max_dets
+    int* count = nullptr;       // F
+    DevDet* h_dets = nullptr;   // pinned F x async_cap
+    int* h_count = nullptr;     // pinned F
+    int nf = 0;
+    int frame_ids[RSP_MAX_F];
+    bool busy = false;
+};
+
+struct FrameResult {
+    int frame_idx;
+    int n_dets;
+    bool overflow;
+    std::vector<rsp_target> targets;
+};
+
+}  // namespace
+
+struct rsp_plan {
+    int device = 0;
+    Geometry g{};
+    DevConsts k{};
+    rsp_cluster_params cl{};
+    double deltaR = 0, deltaV = 0;
+    double p_signal_unscaled = 0, c = 0, fs = 0, wavelength = 0, d = 0, prt = 0;
+    int F = 1;
+    int async_cap = 2048;
+    size_t z_elems = 0, rdm_elems = 0;
+    std::vector<SegDesc> segs;
+    std::vector<K2Job> jobs;
+    std::vector<void*> dev_allocs;
+    double* d_tx = nullptr;
+    SynthTarget* d_tg = nullptr;
+    float2* d_cube = nullptr;     // staging cube for the synchronous paths
+    float2* d_aux = nullptr;      // second map for the stage-2 path
+    float2* h_stage = nullptr;    // pinned staging for uploads
+    size_t h_stage_bytes = 0;
+    Lane lanes[2];
+    int next_lane = 0;
+    // pending batch of the queue
+    const float2* pend_in[RSP_MAX_F];
+    int pend_ids[RSP_MAX_F];
+    int npend = 0;
+    std::deque<FrameResult> results;
+    bool overflow_seen = false;
+
+    ~rsp_plan();
+    template <class T>
+    int dalloc(T** p, size_t n) {
+        void* q = nullptr;
+        if (hipMalloc(&q, n * sizeof(T) + 16) != hipSuccess)
+            return fail(RSP_ERR_NOMEM, "hipMalloc(%zu bytes) failed", n * sizeof(T));
+        dev_allocs.push_back(q);
+        *p = (T*)q;
+        return RSP_OK;
+    }
+    template <class T>
+    int upload(T** p, const std::vector<T>& h) {
+        int rc = dalloc(p, std::max<size_t>(h.size(), 1));
+        if (rc) return rc;
+        if (!h.empty()) HIPCHK(hipMemcpy(*p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+        return RSP_OK;
+    }
+};
+
+rsp_plan::~rsp_plan() {
+    (void)hipSetDevice(device);
+    for (auto& L : lanes) {
+        if (L.stream) (void)hipStreamSynchronize(L.stream);
+        if (L.h_dets) (void)hipHostFree(L.h_dets);
+        if (L.h_count) (void)hipHostFree(L.h_count);
+        if (L.done) (void)hipEventDestroy(L.done);
+        if (L.stream) (void)hipStreamDestroy(L.stream);
+    }
+    if (h_stage) (void)hipHostFree(h_stage);
+    for (void* p : dev_allocs) (void)hipFree(p);
+}
+
+namespace {
+
+// ---- S10 / S11 on the host (fsf:302-407) ---------------------------------------------
+template <class Close>
+int bfs_labels(int n, Close close, std::vector<int>& ids) {
+    ids.assign(n, 0);
+    int cur = 0;
+    std::vector<int> queue;
+    for (int i = 0; i < n; ++i) {
+        if (ids[i]) continue;
+        ++cur;
+        queue.clear();
+        queue.push_back(i);
+        for (size_t h = 0; h < queue.size(); ++h) {
+            const int ci = queue[h];
+            if (ids[ci]) continue;
+            ids[ci] = cur;
+            for (int j = 0; j < n; ++j)
+                if (!ids[j] && close(ci, j)) queue.push_back(j);
+        }
+    }
+    return cur;
+}
+
+void cluster_frame(const rsp_cluster_params& cp, std::vector<rsp_detection>& dets,
+                   std::vector<rsp_target>& final_targets) {
+    // reference order of all_raw_detections: pair, then find() column-major (r, v)  (fsf:181,215-221)
+    std::sort(dets.begin(), dets.end(), [](const rsp_detection& a, const rsp_detection& b) {
+        if (a.pair_idx != b.pair_idx) return a.pair_idx < b.pair_idx;
+        if (a.r_idx != b.r_idx) return a.r_idx < b.r_idx;
+        return a.v_idx < b.v_idx;
+    });
+    final_targets.clear();
+    const int n = (int)dets.size();
+    if (!n) return;
+    std::vector<int> ids;
+    const int n1 = bfs_labels(n, [&](int a, int b) {
+        return std::fabs(dets[a].Range - dets[b].Range) <= cp.max_range_sep &&
+               std::fabs(dets[a].Velocity - dets[b].Velocity) <= cp.max_vel_sep &&
+               std::fabs(dets[a].Angle - dets[b].Angle) <= cp.max_angle_sep;
+    }, ids);
+    std::vector<rsp_target> st1(n1);
+    for (int c = 1; c <= n1; ++c) {   // power-weighted means in index order (fsf:341-351)
+        double tp = 0, sr = 0, sv = 0, sa = 0;
+        for (int i = 0; i < n; ++i) if (ids[i] == c) tp += dets[i].amp;
+        for (int i = 0; i < n; ++i) if (ids[i] == c) sr += dets[i].Range * dets[i].amp;
+        for (int i = 0; i < n; ++i) if (ids[i] == c) sv += dets[i].Velocity * dets[i].amp;
+        for (int i = 0; i < n; ++i) if (ids[i] == c) sa += dets[i].Angle * dets[i].amp;
+        st1[c - 1] = rsp_target{sr / tp, sv / tp, sa / tp, tp};
+    }
+    const int n2 = bfs_labels(n1, [&](int a, int b) {
+        return std::fabs(st1[a].Range - st1[b].Range) <= cp.max_range_sep &&
+               std::fabs(st1[a].Velocity - st1[b].Velocity) <= cp.max_vel_sep;
+    }, ids);
+    for (int c = 1; c <= n2; ++c) {   // winner-take-all, first max (fsf:393-406)
+        int w = -1;
+        for (int i = 0; i < n1; ++i)
+            if (ids[i] == c && (w < 0 || st1[i].Power > st1[w].Power)) w = i;
+        final_targets.push_back(st1[w]);
+    }
+}
+
+// ---- geometry analysis ------------------------------------------------------------------
+struct Interval { int lo, hi; };
+
+int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga, int gb, int seg_lo,
+                      std::vector<float2>& H, std::vector<float2>& twM, std::vector<int>& tw_sizes,
+                      std::vector<int>& tw_offs, const char* name) {
+    std::vector<cd> h(Nfft);
+    for (int i = 0; i < Nfft; ++i) h[i] = cd(mf_fft[2 * i], mf_fft[2 * i + 1]);
+    fft_d(h, +1);
+    double hmax = 0;
+    for (auto& v : h) { v /= (double)Nfft; hmax = std::max(hmax, std::abs(v)); }
+    if (hmax == 0) return fail(RSP_ERR_INVALID, "%s matched filter is all zero", name);
+    int Lh = 0;
+    for (int i = 0; i < Nfft; ++i) if (std::abs(h[i]) > 1e-10 * hmax) Lh = i + 1;
+    if (gb > Nfft)
+        return fail(RSP_ERR_INVALID, "%s gates end at %d beyond N_fft %d (fsf:124-125 index out of range)", name, gb, Nfft);
+    const int Ls = std::min(N - seg_lo, Nfft);   // fft(seg, Nfft) truncates or pads
+    if (ga < Lh - 1 && Ls + (Lh - 1 - ga) > Nfft)
+        return fail(RSP_ERR_UNSUPPORTED, "%s segment: circular aliasing reaches kept gates (L_s=%d L_h=%d N_fft=%d)", name, Ls, Lh, Nfft);
+    s.type = 1;
+    s.ga = ga; s.gb = gb; s.seg_lo = seg_lo;
+    s.Lh = Lh;
+    s.lo = std::max(seg_lo, seg_lo + ga - (Lh - 1));
+    s.hi = std::min(seg_lo + Ls - 1, seg_lo + gb - 1);
+    // overlap-save block size: minimise blocks * M * (log2 M + 2), M <= 2048 so that a
+    // workgroup owns >= 2 adjacent rows (128 B contiguous loads of z)
+    const int nout = gb - ga;
+    double best = 1e300;
+    int bestM = 0;
+    for (int M = 64; M <= 2048; M *= 2) {
+        const int V = M - Lh + 1;
+        if (V < 1) continue;
+        const int nb = (nout + V - 1) / V;
+        const double cost = (double)nb * M * (ilog2i(M) + 2);
+        if (cost < best * 0.999) { best = cost; bestM = M; }
+    }
+    if (!bestM) return fail(RSP_ERR_UNSUPPORTED, "%s filter length %d exceeds the 2048-point block", name, Lh);
+    const int M = bestM;
+    s.M = M; s.logM = ilog2i(M); s.V = M - Lh + 1; s.nblocks = (nout + s.V - 1) / s.V;
+    s.rows_per_wg = RSP_K2_POINTS / M;
+    int m = s.logM; s.nrad = 0;
+    while (m >= 4) { s.rad[s.nrad++] = 16; m -= 4; }
+    if (m > 0) s.rad[s.nrad++] = 1 << m;
+    // spectrum of h zero-padded to M, natural order, 1/M folded in
+    std::vector<cd> hm(M, 0.0);
+    for (int i = 0; i < Lh; ++i) hm[i] = h[i];
+    fft_d(hm, -1);
+    s.H_off = (int)H.size();
+    for (auto& v : hm) { v /= (double)M; H.push_back(make_float2((float)v.real(), (float)v.imag())); }
+    int ti = -1;
+    for (size_t q = 0; q < tw_sizes.size(); ++q) if (tw_sizes[q] == M) ti = (int)q;
+    if (ti < 0) {
+        tw_sizes.push_back(M);
+        tw_offs.push_back((int)twM.size());
+        for (int i = 0; i < M; ++i) {
+            const double a = -2.0 * M_PI * i / M;
+            twM.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
+        }
+        ti = (int)tw_sizes.size() - 1;
+    }
+    s.tw_off = tw_offs[ti];
+    return RSP_OK;
+}
+
+int setup_lane(rsp_plan* p, Lane& L) {
+    HIPCHK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&L.done, hipEventDisableTiming));
+    int rc;
+    if ((rc = p->dalloc(&L.z, p->z_elems * p->F))) return rc;
+    if ((rc = p->dalloc(&L.rdm, p->rdm_elems * p->F))) return rc;
+    if ((rc = p->dalloc(&L.dets, (size_t)p->g.max_dets * p->F))) return rc;
+    if ((rc = p->dalloc(&L.count, (size_t)p->F))) return rc;
+    HIPCHK(hipHostMalloc((void**)&L.h_dets, sizeof(DevDet) * p->async_cap * p->F, hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void**)&L.h_count, sizeof(int) * p->F, hipHostMallocDefault));
+    return RSP_OK;
+}
+
+FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const float2* const* in, int nf) {
+    FramePtrs fp{};
+    for (int f = 0; f < nf; ++f) {
+        fp.in[f] = in[f];
+        fp.z[f] = L.z + p->z_elems * f;
+        fp.rdm[f] = L.rdm + p->rdm_elems * f;
+        fp.dets[f] = L.dets + (size_t)p->g.max_dets * f;
+        fp.count[f] = L.count + f;
+    }
+    return fp;
+}
+
+// Enqueue K1 -> K2 -> K3 for nf frames on lane L, plus the async detection read-back.
+int launch_batch(rsp_plan* p, Lane& L, const float2* const* in, const int* ids, int nf) {
+    const FramePtrs fp = lane_ptrs(p, L, in, nf);
+    HIPCHK(hipMemsetAsync(L.count, 0, sizeof(int) * nf, L.stream));
+    HIPCHK(launch_k1(p->g, p->k, fp, nf, 3, p->g.C, L.stream));
+    HIPCHK(launch_k2(p->g, p->k, fp, nf, p->g.B * p->g.P, L.stream));
+    HIPCHK(launch_k3(p->g, p->k, fp, nf, L.stream));
+    HIPCHK(hipMemcpyAsync(L.h_count, L.count, sizeof(int) * nf, hipMemcpyDeviceToHost, L.stream));
+    HIPCHK(hipMemcpy2DAsync(L.h_dets, sizeof(DevDet) * p->async_cap, L.dets, sizeof(DevDet) * p->g.max_dets,
+                            sizeof(DevDet) * p->async_cap, nf, hipMemcpyDeviceToHost, L.stream));
+    HIPCHK(hipEventRecord(L.done, L.stream));
+    L.nf = nf;
+    for (int f = 0; f < nf; ++f) L.frame_ids[f] = ids[f];
+    L.busy = true;
+    return RSP_OK;
+}
+
+// Wait for lane L, gather its detections (sync copy of any tail past async_cap) and cluster.
+int harvest(rsp_plan* p, Lane& L, std::vector<std::vector<rsp_detection>>* keep_dets = nullptr) {
+    if (!L.busy) return RSP_OK;
+    HIPCHK(hipEventSynchronize(L.done));
+    L.busy = false;
+    if (keep_dets) keep_dets->assign(L.nf, {});
+    for (int f = 0; f < L.nf; ++f) {
+        const int cnt = L.h_count[f];
+        FrameResult fr;
+        fr.frame_idx = L.frame_ids[f];
+        fr.overflow = cnt > p->g.max_dets;
+        const int n = std::min(cnt, p->g.max_dets);
+        fr.n_dets = n;
+        std::vector<rsp_detection> dets(n);
+        const int na = std::min(n, p->async_cap);
+        static_assert(sizeof(DevDet) == sizeof(rsp_detection), "layout");
+        if (na) memcpy(dets.data(), L.h_dets + (size_t)f * p->async_cap, sizeof(DevDet) * na);
+        if (n > na)
+            HIPCHK(hipMemcpy(dets.data() + na, L.dets + (size_t)p->g.max_dets * f + na, sizeof(DevDet) * (n - na),
+                             hipMemcpyDeviceToHost));
+        cluster_frame(p->cl, dets, fr.targets);
+        if (fr.overflow) p->overflow_seen = true;
+        if (keep_dets) (*keep_dets)[f] = dets;
+        p->results.push_back(std::move(fr));
+    }
+    return RSP_OK;
+}
+
+int flush_pending(rsp_plan* p) {
+    if (!p->npend) return RSP_OK;
+    Lane& L = p->lanes[p->next_lane];
+    int rc = harvest(p, L);
+    if (rc) return rc;
+    rc = launch_batch(p, L, p->pend_in, p->pend_ids, p->npend);
+    p->npend = 0;
+    p->next_lane ^= 1;
+    return rc;
+}
+
+int drain_all(rsp_plan* p) {
+    int rc = flush_pending(p);
+    if (rc) return rc;
+    // harvest in launch order: the lane launched first is next_lane
+    for (int q = 0; q < 2; ++q) {
+        rc = harvest(p, p->lanes[(p->next_lane + q) & 1]);
+        if (rc) return rc;
+    }
+    return RSP_OK;
+}
+
+int ensure_stage(rsp_plan* p, size_t bytes) {
+    if (p->h_stage_bytes >= bytes) return RSP_OK;
+    if (p->h_stage) (void)hipHostFree(p->h_stage);
+    p->h_stage = nullptr;
+    HIPCHK(hipHostMalloc((void**)&p->h_stage, bytes, hipHostMallocDefault));
+    p->h_stage_bytes = bytes;
+    return RSP_OK;
+}
+
+// Copy a host cube (any dtype) into d_dst as complex64.
+int upload_cube(rsp_plan* p, const void* cube, int dtype, size_t elems, float2* d_dst, hipStream_t s) {
+    int rc = ensure_stage(p, elems * sizeof(float2));
+    if (rc) return rc;
+    if (dtype == RSP_C64) {
+        memcpy(p->h_stage, cube, elems * sizeof(float2));
+    } else if (dtype == RSP_C128) {
+        const double* src = (const double*)cube;
+        for (size_t i = 0; i < elems; ++i) p->h_stage[i] = make_float2((float)src[2 * i], (float)src[2 * i + 1]);
+    } else {
+        return fail(RSP_ERR_INVALID, "unknown dtype %d", dtype);
+    }
+    HIPCHK(hipMemcpyAsync(d_dst, p->h_stage, elems * sizeof(float2), hipMemcpyHostToDevice, s));
+    return RSP_OK;
+}
+
+// [B][P][G] float maps -> MATLAB column-major [P x G x B] complex double
+void rdm_to_matlab(const rsp_plan* p, const std::vector<float2>& m, double* out) {
+    const int P = p->g.P, G = p->g.G, B = p->g.B;
+    for (int b = 0; b < B; ++b)
+        for (int v = 0; v < P; ++v)
+            for (int r = 0; r < G; ++r) {
+                const float2 x = m[((size_t)b * P + v) * G + r];
+                const size_t o = (size_t)v + (size_t)P * ((size_t)r + (size_t)G * b);
+                out[2 * o] = x.x;
+                out[2 * o + 1] = x.y;
+            }
+}
+
+int run_sync_frame(rsp_plan* p, const float2* d_in, int frame_idx, rsp_frame_out* out) {
+    int rc = drain_all(p);
+    if (rc) return rc;
+    const size_t nres = p->results.size();
+    Lane& L = p->lanes[0];
+    const float2* in[1] = {d_in};
+    int ids[1] = {frame_idx};
+    std::vector<std::vector<rsp_detection>> dets;
+    if ((rc = launch_batch(p, L, in, ids, 1))) return rc;
+    if ((rc = harvest(p, L, &dets))) return rc;
+    FrameResult fr = p->results.back();
+    p->results.resize(nres);   // synchronous frames do not enter the queue's result list
+    if (fr.overflow) return fail(RSP_ERR_OVERFLOW, "frame %d: %d detections exceed capacity %d", frame_idx,
+                                 fr.n_dets, p->g.max_dets);
+    if (out) {
+        std::vector<rsp_detection>& d = dets[0];
+        out->n_dets = (int)d.size();
+        if (out->dets) memcpy(out->dets, d.data(), sizeof(rsp_detection) * std::min<int>(out->dets_cap, (int)d.size()));
+        out->n_targets = (int)fr.targets.size();
+        if (out->targets)
+            memcpy(out->targets, fr.targets.data(), sizeof(rsp_target) * std::min<int>(out->targets_cap, (int)fr.targets.size()));
+        if (out->rdm || out->cfar_maps) {
+            std::vector<float2> m(p->rdm_elems);
+            HIPCHK(hipMemcpy(m.data(), L.rdm, m.size() * sizeof(float2), hipMemcpyDeviceToHost));
+            if (out->rdm) rdm_to_matlab(p, m, out->rdm);
+            if (out->cfar_maps) {   // rdm_for_cfar_all (fsf:184-187)
+                const int P = p->g.P, G = p->g.G, B = p->g.B;
+                for (int b = 0; b + 1 < B; ++b)
+                    for (int v = 0; v < P; ++v)
+                        for (int r = 0; r < G; ++r) {
+                            const float2 a = m[((size_t)b * P + v) * G + r], c = m[((size_t)(b + 1) * P + v) * G + r];
+                            out->cfar_maps[(size_t)v + (size_t)P * ((size_t)r + (size_t)G * b)] =
+                                std::hypot((double)a.x, (double)a.y) + std::hypot((double)c.x, (double)c.y);
+                        }
+            }
+        }
+        if (out->dets && (int)d.size() > out->dets_cap)
+            return fail(RSP_ERR_OVERFLOW, "%d detections exceed dets_cap %d", (int)d.size(), out->dets_cap);
+        if (out->targets && (int)fr.targets.size() > out->targets_cap)
+            return fail(RSP_ERR_OVERFLOW, "%d targets exceed targets_cap %d", (int)fr.targets.size(), out->targets_cap);
+    }
+    return RSP_OK;
+}
+
+const char* kStageNames[] = {"k1_dbf_mtd", "k2_pc", "k3_cfar"};
+
+}  // namespace
+
+// =========================================================================================
+extern "C" {
+
+int32_t rsp_abi_version(void) { return RSP_ABI_VERSION; }
+const char* rsp_last_error(void) { return g_err.c_str(); }
+const char* rsp_stage_name(int32_t s) { return (s >= 0 && s < 3) ? kStageNames[s] : "?"; }
+
+int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, const rsp_cluster_params* cluster,
+                        const rsp_precomputed* pre, int32_t device, int32_t frames_per_launch, rsp_plan** out) {
+    if (!cfg || !cfar || !cluster || !pre || !out) return fail(RSP_ERR_INVALID, "null argument");
+    *out = nullptr;
+    const int C = cfg->channel_num, B = cfg->beam_num, P = cfg->prtNum, N = cfg->point_PRT;
+    const int g1 = pre->N_gate_narrow, g2 = pre->N_gate_medium, g3 = pre->N_gate_long, G = pre->N_total_gate;
+    if (C < 1 || B < 1 || B > 16 || P < 2 || N < 2) return fail(RSP_ERR_INVALID, "bad sizes C=%d B=%d P=%d N=%d (1<=B<=16)", C, B, P, N);
+    if (P % 2) return fail(RSP_ERR_UNSUPPORTED, "odd prtNum %d (pulse pairs are loaded as 16 B)", P);
+    if (g1 < 0 || g2 < 0 || g3 < 0 || G != g1 + g2 + g3 || G < 1) return fail(RSP_ERR_INVALID, "gate counts inconsistent");
+    if (!pre->DBF_coeffs_data_C || !pre->MF_narrow || !pre->MF_medium_fft || !pre->MF_long_fft || !pre->MTD_win ||
+        !pre->range_axis || !pre->velocity_axis || !pre->beam_angles_deg || (B > 1 && !pre->k_slopes_LUT))
+        return fail(RSP_ERR_INVALID, "precomputed_data field missing");
+    if (frames_per_launch < 1 || frames_per_launch > RSP_MAX_F)
+        return fail(RSP_ERR_INVALID, "frames_per_launch must be 1..%d", RSP_MAX_F);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RSP_ERR_DEVICE, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(RSP_ERR_INVALID, "device %d out of range (%d devices)", device, ndev);
+    HIPCHK(hipSetDevice(device));
+
+    rsp_plan* p = new rsp_plan();
+    p->device = device;
+    p->F = frames_per_launch;
+    p->cl = *cluster;
+    p->c = cfg->c; p->fs = cfg->fs; p->wavelength = cfg->wavelength; p->d = cfg->element_spacing; p->prt = cfg->prt;
+    p->p_signal_unscaled = pre->P_signal_unscaled;
+    Geometry& g = p->g;
+    g.C = C; g.B = B; g.P = P; g.N = N; g.G = G;
+    g.refR = cfar->refCells_R; g.guardR = cfar->guardCells_R; g.refV = cfar->refCells_V; g.guardV = cfar->guardCells_V;
+    g.T = (float)cfar->T_CFAR;
+    g.max_dets = 1 << 16;
+    auto bail = [&](int rc) { delete p; return rc; };
+    if (g.refR < 1 || g.refV < 1 || g.guardR < 0 || g.guardV < 0) return bail(fail(RSP_ERR_INVALID, "bad CFAR window"));
+
+    // ---- pulse-compression segments (fsf:105-126)
+    std::vector<float2> H, twM;
+    std::vector<int> tw_sizes, tw_offs;
+    std::vector<float> taps;
+    std::vector<Interval> need;
+    if (g1 > 0) {
+        SegDesc s{};
+        s.type = 0;
+        s.ga = 0; s.gb = g1;
+        s.seg_lo = pre->seg_start_narrow - 1;
+        if (s.seg_lo < 0 || s.seg_lo >= N) return bail(fail(RSP_ERR_INVALID, "seg_start_narrow out of range"));
+        s.Ls = N - s.seg_lo;
+        s.ntaps = pre->n_MF_narrow;
+        s.delay = pre->fir_delay;
+        if (s.ntaps < 1) return bail(fail(RSP_ERR_INVALID, "empty MF_narrow"));
+        int lo = INT32_MAX, hi = -1;
+        for (int gg = 0; gg < g1; ++gg) {
+            int kk = (gg + s.delay) % s.Ls;
+            if (kk < 0) kk += s.Ls;
+            const int top = s.seg_lo + kk;
+            const int bot = std::max(s.seg_lo, top - s.ntaps + 1);
+            lo = std::min(lo, bot);
+            hi = std::max(hi, top);
+        }
+        s.lo = lo; s.hi = hi;
+        const int W = hi - lo + 1;
+        s.rows_per_wg = std::max(1, std::min(8, (RSP_K2_POINTS - s.ntaps / 2 - 8) / W));
+        if (W * s.rows_per_wg + (s.ntaps + 1) / 2 > RSP_K2_POINTS + RSP_K2_POINTS / 16)
+            return bail(fail(RSP_ERR_UNSUPPORTED, "narrow segment window %d samples too long", W));
+        s.taps_off = (int)taps.size();
+        for (int j = 0; j < s.ntaps; ++j) taps.push_back((float)pre->MF_narrow[j]);
+        p->segs.push_back(s);
+    }
+    if (g2 > 0) {
+        SegDesc s{};
+        int rc = build_fft_segment(s, pre->MF_medium_fft, pre->N_fft_med, N, g1, g1 + g2, pre->seg_start_medium - 1, H,
+                                   twM, tw_sizes, tw_offs, "medium");
+        if (rc) return bail(rc);
+        p->segs.push_back(s);
+    }
+    if (g3 > 0) {
+        SegDesc s{};
+        int rc = build_fft_segment(s, pre->MF_long_fft, pre->N_fft_long, N, g1 + g2, G, pre->seg_start_long - 1, H, twM,
+                                   tw_sizes, tw_offs, "long");
+        if (rc) return bail(rc);
+        p->segs.push_back(s);
+    }
+    for (auto& s : p->segs) {
+        if (s.seg_lo < 0 || s.seg_lo >= N) return bail(fail(RSP_ERR_INVALID, "segment start out of range"));
+        if (s.hi >= s.lo) need.push_back({s.lo, s.hi});
+    }
+    // union of needed fast-time windows -> compacted sample list (K1 processes only these)
+    std::sort(need.begin(), need.end(), [](const Interval& a, const Interval& b) { return a.lo < b.lo; });
+    std::vector<Interval> U;
+    for (auto& iv : need) {
+        if (!U.empty() && iv.lo <= U.back().hi + 1) U.back().hi = std::max(U.back().hi, iv.hi);
+        else U.push_back(iv);
+    }
+    std::vector<int> nof;
+    for (auto& iv : U) for (int n = iv.lo; n <= iv.hi; ++n) nof.push_back(n);
+    g.nU = (int)nof.size();
+    for (auto& s : p->segs) {
+        if (s.hi < s.lo) { s.off = 0; continue; }
+        s.off = (int)(std::lower_bound(nof.begin(), nof.end(), s.lo) - nof.begin());
+    }
+    // K1 tile: NT samples per [P][NT] slab; keep LDS <= 80 KB (2 workgroups per CU)
+    g.pow2P = is_pow2(P);
+    g.Ppad = P + 4;
+    g.NT = 8;
+    while (g.NT > 1 && ((size_t)B * g.NT * g.Ppad * sizeof(float2) > 80 * 1024 || (g.pow2P && B * g.NT * P > 8192)))
+        g.NT >>= 1;
+    if ((size_t)B * g.NT * g.Ppad * sizeof(float2) > 160 * 1024 || (g.pow2P && B * g.NT * P > 8192))
+        return bail(fail(RSP_ERR_UNSUPPORTED, "B*P too large for the slow-time FFT tile"));
+    g.ntiles = (g.nU + g.NT - 1) / g.NT;
+    nof.resize((size_t)g.ntiles * g.NT, -1);
+    if (g.pow2P) {
+        g.logP = ilog2i(P);
+        int m = g.logP; g.nradP = 0;
+        while (m >= 4) { g.radP[g.nradP++] = 16; m -= 4; }
+        if (m > 0) g.radP[g.nradP++] = 1 << m;
+    }
+    if (16 * (size_t)g.Ppad * sizeof(float2) > 160 * 1024 || (g.pow2P && 16 * P > 8192))
+        return bail(fail(RSP_ERR_UNSUPPORTED, "prtNum %d too large", P));
+    // K2 jobs
+    const int rows_total = B * P;
+    int wg = 0;
+    for (size_t si = 0; si < p->segs.size(); ++si) {
+        const SegDesc& s = p->segs[si];
+        const int nwg = (rows_total + s.rows_per_wg - 1) / s.rows_per_wg;
+        const int nbl = (s.type == 1) ? s.nblocks : 1;
+        for (int blk = 0; blk < nbl; ++blk) {
+            p->jobs.push_back(K2Job{(int)si, blk, wg, nwg});
+            wg += nwg;
+        }
+    }
+    g.nseg = (int)p->segs.size();
+    g.njobs = (int)p->jobs.size();
+    g.nwg_k2 = wg;
+    // K3 tile
+    g.cfar_hR = std::max(g.refR + g.guardR, 2);
+    g.cfar_RT = 64;
+    while (g.cfar_RT > 8 && (size_t)P * (g.cfar_RT + 2 * g.cfar_hR) * 4 > 96 * 1024) g.cfar_RT >>= 1;
+    g.cfar_W = g.cfar_RT + 2 * g.cfar_hR;
+    if ((size_t)P * g.cfar_W * 4 > 160 * 1024) return bail(fail(RSP_ERR_UNSUPPORTED, "CFAR tile exceeds LDS"));
+
+    // ---- constants to the device
+    int rc;
+    std::vector<float2> Wc((size_t)B * C), twP(P);
+    for (int b = 0; b < B; ++b)
+        for (int c = 0; c < C; ++c) {   // column-major B x C; y = x * W' uses conj(W)  (fsf:95)
+            const size_t i = (size_t)b + (size_t)B * c;
+            Wc[(size_t)b * C + c] = make_float2((float)pre->DBF_coeffs_data_C[2 * i], -(float)pre->DBF_coeffs_data_C[2 * i + 1]);
+        }
+    for (int i = 0; i < P; ++i) {
+        const double a = -2.0 * M_PI * i / P;
+        twP[i] = make_float2((float)std::cos(a), (float)std::sin(a));
+    }
+    std::vector<float> win(pre->MTD_win, pre->MTD_win + P);
+    std::vector<double> ra(pre->range_axis, pre->range_axis + G), va(pre->velocity_axis, pre->velocity_axis + P);
+    std::vector<double> ang(pre->beam_angles_deg, pre->beam_angles_deg + B);
+    std::vector<double> kl(std::max(B - 1, 1), 0.0);
+    for (int i = 0; i + 1 < B; ++i) kl[i] = pre->k_slopes_LUT[i];
+    float2 *dWc, *dtwP, *dH, *dtwM; float *dwin, *dtaps; int* dnof; SegDesc* dsegs; K2Job* djobs;
+    double *dra, *dva, *dang, *dkl;
+    if ((rc = p->upload(&dWc, Wc)) || (rc = p->upload(&dtwP, twP)) || (rc = p->upload(&dwin, win)) ||
+        (rc = p->upload(&dnof, nof)) || (rc = p->upload(&dsegs, p->segs)) || (rc = p->upload(&djobs, p->jobs)) ||
+        (rc = p->upload(&dtaps, taps)) || (rc = p->upload(&dH, H)) || (rc = p->upload(&dtwM, twM)) ||
+        (rc = p->upload(&dra, ra)) || (rc = p->upload(&dva, va)) || (rc = p->upload(&dang, ang)) ||
+        (rc = p->upload(&dkl, kl)))
+        return bail(rc);
+    p->k = DevConsts{dWc, dwin, dtwP, dnof, dsegs, djobs, dtaps, dH, dtwM, dra, dva, dang, dkl, pre->deltaR, pre->deltaV};
+    if (pre->tx_pulse) {
+        std::vector<double> tx(pre->tx_pulse, pre->tx_pulse + 2 * (size_t)N);
+        if ((rc = p->upload(&p->d_tx, tx))) return bail(rc);
+    }
+    if ((rc = p->dalloc(&p->d_tg, 64))) return bail(rc);
+    p->z_elems = (size_t)B * g.ntiles * g.NT * P;
+    p->rdm_elems = (size_t)B * P * G;
+    if ((rc = p->dalloc(&p->d_cube, (size_t)std::max(C, B) * N * P))) return bail(rc);
+    for (auto& L : p->lanes)
+        if ((rc = setup_lane(p, L))) return bail(rc);
+    *out = p;
+    return RSP_OK;
+}
+
+int32_t rsp_plan_destroy(rsp_plan* plan) {
+    delete plan;
+    return RSP_OK;
+}
+
+int32_t rsp_query_sizes(const rsp_plan* p, rsp_sizes* s) {
+    if (!p || !s) return fail(RSP_ERR_INVALID, "null argument");
+    const Geometry& g = p->g;
+    s->cube_elems = (int64_t)g.P * g.N * g.C;
+    s->rdm_elems = (int64_t)g.P * g.G * g.B;
+    s->cfar_map_elems = (int64_t)g.P * g.G * std::max(g.B - 1, 0);
+    s->P = g.P; s->N = g.N; s->C = g.C; s->B = g.B; s->G = g.G;
+    s->used_samples = g.nU;
+    s->max_detections = g.max_dets;
+    s->n_stages = 3;
+    return RSP_OK;
+}
+
+int32_t rsp_process_cube(rsp_plan* p, const void* cube, int32_t dtype, int32_t layout, int32_t frame_idx,
+                         rsp_frame_out* out) {
+    if (!p || !cube) return fail(RSP_ERR_INVALID, "null argument");
+    if (layout != RSP_LAYOUT_PNC) return fail(RSP_ERR_UNSUPPORTED, "layout %d", layout);
+    HIPCHK(hipSetDevice(p->device));
+    int rc = drain_all(p);
+    if (rc) return rc;
+    if ((rc = upload_cube(p, cube, dtype, (size_t)p->g.P * p->g.N * p->g.C, p->d_cube, p->lanes[0].stream))) return rc;
+    return run_sync_frame(p, p->d_cube, frame_idx, out);
+}
+
+static int synth_into(rsp_plan* p, const rsp_target_in* t, int nt, int frame_idx, uint64_t seed, double p_noise,
+                      float2* d_cube, hipStream_t s) {
+    if (!p->d_tx) return fail(RSP_ERR_INVALID, "plan has no tx_pulse (synthesis path needs precomputed_data.tx_pulse)");
+    if (nt < 0 || nt > 64) return fail(RSP_ERR_INVALID, "1..64 targets supported, got %d", nt);
+    std::vector<SynthTarget> tg(nt);
+    for (int i = 0; i < nt; ++i) {   // fsf:51-72
+        const double delay = 2.0 * t[i].Range / p->c;
+        tg[i].delay = (int)mround(delay / (1.0 / p->fs));
+        tg[i].fd_prt = 2.0 * t[i].Velocity / p->wavelength * p->prt;
+        tg[i].amp = std::sqrt(std::pow(10.0, t[i].SNR_dB / 10.0) * p_noise / p->p_signal_unscaled);
+        tg[i].dphi = 2.0 * M_PI * p->d * std::sin(t[i].ElevationAngle * M_PI / 180.0) / p->wavelength;
+    }
+    if (nt) HIPCHK(hipMemcpyAsync(p->d_tg, tg.data(), sizeof(SynthTarget) * nt, hipMemcpyHostToDevice, s));
+    HIPCHK(launch_synth(p->g, p->d_tx, p->d_tg, nt, frame_idx, seed, std::sqrt(p_noise / 2.0), d_cube, s));
+    HIPCHK(hipStreamSynchronize(s));   // targets buffer is reused by the next call
+    return RSP_OK;
+}
+
+int32_t rsp_synthesize_device(rsp_plan* p, const rsp_target_in* t, int32_t nt, int32_t frame_idx, uint64_t seed,
+                              double p_noise, void* d_cube) {
+    if (!p || (!t && nt) || !d_cube) return fail(RSP_ERR_INVALID, "null argument");
+    HIPCHK(hipSetDevice(p->device));
+    return synth_into(p, t, nt, frame_idx, seed, p_noise, (float2*)d_cube, p->lanes[0].stream);
+}
+
+int32_t rsp_process_targets(rsp_plan* p, const rsp_target_in* t, int32_t nt, int32_t frame_idx, uint64_t seed,
+                            double p_noise, rsp_frame_out* out) {
+    if (!p || (!t && nt)) return fail(RSP_ERR_INVALID, "null argument");
+    HIPCHK(hipSetDevice(p->device));
+    int rc = drain_all(p);
+    if (rc) return rc;
+    if ((rc = synth_into(p, t, nt, frame_idx, seed, p_noise, p->d_cube, p->lanes[0].stream))) return rc;
+    return run_sync_frame(p, p->d_cube, frame_idx, out);
+}
+
+int32_t rsp_enqueue_device(rsp_plan* p, const void* d_cube, int32_t frame_idx) {
+    if (!p || !d_cube) return fail(RSP_ERR_INVALID, "null argument");
+    p->pend_in[p->npend] = (const float2*)d_cube;
+    p->pend_ids[p->npend] = frame_idx;
+    if (++p->npend == p->F) return flush_pending(p);
+    return RSP_OK;
+}
+
+int32_t rsp_drain(rsp_plan* p) {
+    if (!p) return fail(RSP_ERR_INVALID, "null argument");
+    HIPCHK(hipSetDevice(p->device));
+    int rc = drain_all(p);
+    if (rc) return rc;
+    if (p->overflow_seen) {
+        p->overflow_seen = false;
+        return fail(RSP_ERR_OVERFLOW, "a queued frame exceeded the detection capacity %d", p->g.max_dets);
+    }
+    return RSP_OK;
+}
+
+int32_t rsp_results_count(const rsp_plan* p, int32_t* n_frames, int64_t* n_targets) {
+    if (!p) return fail(RSP_ERR_INVALID, "null argument");
+    int64_t nt = 0;
+    for (auto& r : p->results) nt += (int64_t)r.targets.size();
+    if (n_frames) *n_frames = (int32_t)p->results.size();
+    if (n_targets) *n_targets = nt;
+    return RSP_OK;
+}
+
+int32_t rsp_results_get(const rsp_plan* p, int32_t i, int32_t* frame_idx, rsp_target* targets, int32_t cap,
+                        int32_t* n_targets, int32_t* n_dets) {
+    if (!p || i < 0 || i >= (int)p->results.size()) return fail(RSP_ERR_INVALID, "result index out of range");
+    const FrameResult& r = p->results[i];
+    if (frame_idx) *frame_idx = r.frame_idx;
+    if (n_targets) *n_targets = (int32_t)r.targets.size();
+    if (n_dets) *n_dets = r.n_dets;
+    if (targets) memcpy(targets, r.targets.data(), sizeof(rsp_target) * std::min<size_t>(cap, r.targets.size()));
+    if (targets && (int)r.targets.size() > cap) return fail(RSP_ERR_OVERFLOW, "cap too small");
+    return RSP_OK;
+}
+
+int32_t rsp_results_clear(rsp_plan* p) {
+    if (!p) return fail(RSP_ERR_INVALID, "null argument");
+    p->results.clear();
+    return RSP_OK;
+}
+
+int32_t rsp_process_stage2(rsp_plan* p, const void* iq, int32_t dtype, double* mtd_out, double* pc_out) {
+    if (!p || !iq) return fail(RSP_ERR_INVALID, "null argument");
+    HIPCHK(hipSetDevice(p->device));
+    int rc = drain_all(p);
+    if (rc) return rc;
+    Lane& L = p->lanes[0];
+    Geometry gs = p->g;
+    gs.C = gs.B;   // input channels are the beams; K1 transposes only (no DBF, no MTD)
+    if ((rc = upload_cube(p, iq, dtype, (size_t)gs.B * gs.N * gs.P, p->d_cube, L.stream))) return rc;
+    if (!p->d_aux && (rc = p->dalloc(&p->d_aux, p->rdm_elems))) return rc;
+    const float2* in[1] = {p->d_cube};
+    const FramePtrs fp = lane_ptrs(p, L, in, 1);
+    HIPCHK(launch_k1(gs, p->k, fp, 1, 0, gs.C, L.stream));
+    HIPCHK(launch_k2(gs, p->k, fp, 1, gs.B * gs.P, L.stream));      // PC rows (b, m) -> L.rdm
+    HIPCHK(launch_mtd_cols(gs, p->k, L.rdm, p->d_aux, L.stream));  // S7 over pulses
+    HIPCHK(hipStreamSynchronize(L.stream));
+    std::vector<float2> m(p->rdm_elems);
+    if (pc_out) {
+        HIPCHK(hipMemcpy(m.data(), L.rdm, m.size() * sizeof(float2), hipMemcpyDeviceToHost));
+        rdm_to_matlab(p, m, pc_out);
+    }
+    if (mtd_out) {
+        HIPCHK(hipMemcpy(m.data(), p->d_aux, m.size() * sizeof(float2), hipMemcpyDeviceToHost));
+        rdm_to_matlab(p, m, mtd_out);
+    }
+    return RSP_OK;
+}
+
+int32_t rsp_profile_stages(rsp_plan* p, const void* d_cube, int32_t iters, float* ms_out, int64_t* bytes_out,
+                           int32_t cap) {
+    if (!p || !d_cube || iters < 1) return fail(RSP_ERR_INVALID, "bad argument");
+    HIPCHK(hipSetDevice(p->device));
+    int rc = drain_all(p);
+    if (rc) return rc;
+    Lane& L = p->lanes[0];
+    const float2* in[1] = {(const float2*)d_cube};
+    const FramePtrs fp = lane_ptrs(p, L, in, 1);
+    const Geometry& g = p->g;
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipMemsetAsync(L.count, 0, sizeof(int), L.stream));
+    for (int s = 0; s < 3 && s < cap; ++s) {
+        auto run = [&]() -> hipError_t {
+            if (s == 0) return launch_k1(g, p->k, fp, 1, 3, g.C, L.stream);
+            if (s == 1) return launch_k2(g, p->k, fp, 1, g.B * g.P, L.stream);
+            hipError_t e = hipMemsetAsync(L.count, 0, sizeof(int), L.stream);
+            return e != hipSuccess ? e : launch_k3(g, p->k, fp, 1, L.stream);
+        };
+        HIPCHK(run());
+        HIPCHK(hipEventRecord(e0, L.stream));
+        for (int i = 0; i < iters; ++i) HIPCHK(run());
+        HIPCHK(hipEventRecord(e1, L.stream));
+        HIPCHK(hipEventSynchronize(e1));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+        if (ms_out) ms_out[s] = ms / iters;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (bytes_out) {   // algorithmic bytes per launch (one frame)
+        const int64_t cube = (int64_t)g.C * g.nU * g.P * 8, z = (int64_t)g.B * g.nU * g.P * 8;
+        const int64_t rdm = (int64_t)g.B * g.P * g.G * 8;
+        if (cap > 0) bytes_out[0] = cube + z;
+        if (cap > 1) bytes_out[1] = z + rdm;
+        if (cap > 2) bytes_out[2] = rdm;
+    }
+    return RSP_OK;
+}
+
+int32_t rsp_device_alloc(rsp_plan* p, int64_t bytes, void** d) {
+    if (!p || !d || bytes <= 0) return fail(RSP_ERR_INVALID, "bad argument");
+    HIPCHK(hipSetDevice(p->device));
+    if (hipMalloc(d, bytes) != hipSuccess) return fail(RSP_ERR_NOMEM, "hipMalloc(%lld) failed", (long long)bytes);
+    return RSP_OK;
+}
+int32_t rsp_device_free(rsp_plan* p, void* d) {
+    if (!p) return fail(RSP_ERR_INVALID, "null plan");
+    HIPCHK(hipFree(d));
+    return RSP_OK;
+}
+int32_t rsp_device_upload(rsp_plan* p, void* d, const void* h, int64_t bytes) {
+    if (!p || !d || !h) return fail(RSP_ERR_INVALID, "null argument");
+    HIPCHK(hipSetDevice(p->device));
+    HIPCHK(hipMemcpy(d, h, bytes, hipMemcpyHostToDevice));
+    return RSP_OK;
+}
+int32_t rsp_device_download(rsp_plan* p, void* h, const void* d, int64_t bytes) {
+    if (!p || !d || !h) return fail(RSP_ERR_INVALID, "null argument");
+    HIPCHK(hipSetDevice(p->device));
+    HIPCHK(hipMemcpy(h, d, bytes, hipMemcpyDeviceToHost));
+    return RSP_OK;
+}
+int32_t rsp_device_sync(rsp_plan* p) {
+    if (!p) return fail(RSP_ERR_INVALID, "null plan");
+    HIPCHK(hipSetDevice(p->device));
+    HIPCHK(hipDeviceSynchronize());
+    return RSP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,130 @@
+"""ctypes binding of include/rsp.h (librsp.so).
+
+This is the Python equivalent of the MEX / ``loadlibrary`` shim the MATLAB
+reference would bind.  The library is built in-tree by
+``csrc/Makefile`` into ``rsp/librsp.so``; importing this module does not touch
+the GPU.  There is no CPU fallback: if the library is missing, ``lib()`` raises.
+"""
+import ctypes as ct
+import os
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'librsp.so')
+
+RSP_OK, RSP_ERR_INVALID, RSP_ERR_UNSUPPORTED, RSP_ERR_DEVICE, RSP_ERR_NOMEM, RSP_ERR_OVERFLOW = 0, -1, -2, -3, -4, -5
+RSP_C64, RSP_C128 = 1, 2
+RSP_LAYOUT_PNC = 0
+
+_dp = ct.POINTER(ct.c_double)
+
+
+class SigConfig(ct.Structure):
+    _fields_ = [('c', ct.c_double), ('fs', ct.c_double), ('fc', ct.c_double), ('prt', ct.c_double),
+                ('wavelength', ct.c_double), ('element_spacing', ct.c_double),
+                ('prtNum', ct.c_int32), ('point_PRT', ct.c_int32), ('channel_num', ct.c_int32),
+                ('beam_num', ct.c_int32)]
+
+
+class CfarParams(ct.Structure):
+    _fields_ = [('refCells_V', ct.c_int32), ('guardCells_V', ct.c_int32), ('refCells_R', ct.c_int32),
+                ('guardCells_R', ct.c_int32), ('T_CFAR', ct.c_double)]
+
+
+class ClusterParams(ct.Structure):
+    _fields_ = [('max_range_sep', ct.c_double), ('max_vel_sep', ct.c_double), ('max_angle_sep', ct.c_double)]
+
+
+class Precomputed(ct.Structure):
+    _fields_ = [('tx_pulse', _dp), ('P_signal_unscaled', ct.c_double), ('DBF_coeffs_data_C', _dp),
+                ('MF_narrow', _dp), ('n_MF_narrow', ct.c_int32), ('fir_delay', ct.c_int32),
+                ('MF_medium_fft', _dp), ('N_fft_med', ct.c_int32), ('MF_long_fft', _dp), ('N_fft_long', ct.c_int32),
+                ('N_gate_narrow', ct.c_int32), ('N_gate_medium', ct.c_int32), ('N_gate_long', ct.c_int32),
+                ('N_total_gate', ct.c_int32), ('seg_start_narrow', ct.c_int32), ('seg_start_medium', ct.c_int32),
+                ('seg_start_long', ct.c_int32), ('MTD_win', _dp), ('range_axis', _dp), ('velocity_axis', _dp),
+                ('deltaR', ct.c_double), ('deltaV', ct.c_double), ('beam_angles_deg', _dp), ('k_slopes_LUT', _dp)]
+
+
+class TargetIn(ct.Structure):
+    _fields_ = [('Range', ct.c_double), ('Velocity', ct.c_double), ('ElevationAngle', ct.c_double),
+                ('SNR_dB', ct.c_double)]
+
+
+class Target(ct.Structure):
+    _fields_ = [('Range', ct.c_double), ('Velocity', ct.c_double), ('Angle', ct.c_double), ('Power', ct.c_double)]
+
+
+class Detection(ct.Structure):
+    _fields_ = [('v_idx', ct.c_int32), ('r_idx', ct.c_int32), ('pair_idx', ct.c_int32), ('reserved', ct.c_int32),
+                ('amp', ct.c_double), ('Range', ct.c_double), ('Velocity', ct.c_double), ('Angle', ct.c_double)]
+
+
+class FrameOut(ct.Structure):
+    _fields_ = [('rdm', _dp), ('cfar_maps', _dp), ('dets', ct.POINTER(Detection)), ('dets_cap', ct.c_int32),
+                ('n_dets', ct.c_int32), ('targets', ct.POINTER(Target)), ('targets_cap', ct.c_int32),
+                ('n_targets', ct.c_int32)]
+
+
+class Sizes(ct.Structure):
+    _fields_ = [('cube_elems', ct.c_int64), ('rdm_elems', ct.c_int64), ('cfar_map_elems', ct.c_int64),
+                ('P', ct.c_int32), ('N', ct.c_int32), ('C', ct.c_int32), ('B', ct.c_int32), ('G', ct.c_int32),
+                ('used_samples', ct.c_int32), ('max_detections', ct.c_int32), ('n_stages', ct.c_int32)]
+
+
+_P = ct.c_void_p
+PROTOTYPES = {
+    'rsp_abi_version': (ct.c_int32, []),
+    'rsp_last_error': (ct.c_char_p, []),
+    'rsp_plan_create': (ct.c_int32, [ct.POINTER(SigConfig), ct.POINTER(CfarParams), ct.POINTER(ClusterParams),
+                                     ct.POINTER(Precomputed), ct.c_int32, ct.c_int32, ct.POINTER(_P)]),
+    'rsp_plan_destroy': (ct.c_int32, [_P]),
+    'rsp_query_sizes': (ct.c_int32, [_P, ct.POINTER(Sizes)]),
+    'rsp_process_cube': (ct.c_int32, [_P, _P, ct.c_int32, ct.c_int32, ct.c_int32, ct.POINTER(FrameOut)]),
+    'rsp_process_targets': (ct.c_int32, [_P, ct.POINTER(TargetIn), ct.c_int32, ct.c_int32, ct.c_uint64,
+                                         ct.c_double, ct.POINTER(FrameOut)]),
+    'rsp_synthesize_device': (ct.c_int32, [_P, ct.POINTER(TargetIn), ct.c_int32, ct.c_int32, ct.c_uint64,
+                                           ct.c_double, _P]),
+    'rsp_enqueue_device': (ct.c_int32, [_P, _P, ct.c_int32]),
+    'rsp_drain': (ct.c_int32, [_P]),
+    'rsp_results_count': (ct.c_int32, [_P, ct.POINTER(ct.c_int32), ct.POINTER(ct.c_int64)]),
+    'rsp_results_get': (ct.c_int32, [_P, ct.c_int32, ct.POINTER(ct.c_int32), ct.POINTER(Target), ct.c_int32,
+                                     ct.POINTER(ct.c_int32), ct.POINTER(ct.c_int32)]),
+    'rsp_results_clear': (ct.c_int32, [_P]),
+    'rsp_process_stage2': (ct.c_int32, [_P, _P, ct.c_int32, _dp, _dp]),
+    'rsp_profile_stages': (ct.c_int32, [_P, _P, ct.c_int32, ct.POINTER(ct.c_float), ct.POINTER(ct.c_int64),
+                                        ct.c_int32]),
+    'rsp_stage_name': (ct.c_char_p, [ct.c_int32]),
+    'rsp_device_alloc': (ct.c_int32, [_P, ct.c_int64, ct.POINTER(_P)]),
+    'rsp_device_free': (ct.c_int32, [_P, _P]),
+    'rsp_device_upload': (ct.c_int32, [_P, _P, _P, ct.c_int64]),
+    'rsp_device_download': (ct.c_int32, [_P, _P, _P, ct.c_int64]),
+    'rsp_device_sync': (ct.c_int32, [_P]),
+}
+
+_lib = None
+
+
+class RspError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__('rsp error %d: %s' % (code, msg))
+        self.code = code
+
+
+def lib():
+    """Load librsp.so (raises if it was not built: there is no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError('librsp.so not found at %s -- build it with __graft_entry__.build() '
+                               'or `make -C csrc`' % LIB_PATH)
+        h = ct.CDLL(LIB_PATH)
+        for name, (res, args) in PROTOTYPES.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = h
+    return _lib
+
+
+def check(rc):
+    if rc != RSP_OK:
+        raise RspError(rc, lib().rsp_last_error().decode(errors='replace'))
+    return rc

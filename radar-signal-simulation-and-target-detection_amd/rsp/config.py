@@ -1,0 +1,156 @@
+"""Configuration structs mirroring the reference drivers.
+
+The reference builds MATLAB structs literally in each driver script
+(``main_simulate_echoes_with_array_v8.m:28-70``):  ``config.Sig_Config.*``,
+``config.Array.*``, ``cfar_params``, ``cluster_params`` and a ``targets`` struct
+array.  Here they are plain dicts with the same field names, so host code reads
+like the reference.  ``make_config`` derives ``wavelength`` and ``point_PRT``
+exactly as v8:66-69 does.
+
+Named configurations:
+  * ``'reference'``  - the v8 reference frame: 16C x 13B x 5819 x 332.
+  * ``'plumbing'``   - BASELINE config #1: 8C x 1B x 1024 x 32 (scaled waveform).
+  * ``'x2'``         - BASELINE config #2: 16C x 8B x 4096 x 128 (the bench workload).
+  * ``'x4'``         - BASELINE config #4: 32C x 16B x 8192 x 256 (synthetic weights).
+  * ``'small'``      - a 16C x 4B x 3072 x 64 frame for fast parity tests.
+"""
+import os
+import numpy as np
+
+DATA_DIR = os.path.join(os.path.dirname(__file__), 'data')
+
+# v8:101 -- 35-tap narrow-pulse FIR (integer taps, normalised later by 6/max).
+V8_FIR = [794, 1403, 2143, 2672, 2591, 1711, -58, -2351, -4592, -5855, -5338, -2389, 3005,
+          10341, 18410, 25779, 30907, 32768, 30907, 25779, 18410, 10341, 3005, -2389, -5338,
+          -5855, -4592, -2351, -58, 1711, 2591, 2672, 2143, 1403, 794]
+# v8:138 -- measured monopulse slope LUT for the 12 adjacent beam pairs (opaque data).
+V8_K_LUT = [-4.6391, -4.6888, -4.7578, -4.7891, -4.7214, -4.7513, -5.2343, -5.4529, -5.7323,
+            -6.1685, -7.0256, -8.7612]
+# v8:144 -- beam pointing angles of the 13 CSV beams.
+V8_BEAM_ANGLES = [-16, -9.6, -3.2, 3.2, 9.6, 16, 22.6, 29.2, 36.1, 43.3, 51, 59.6, 70.3]
+
+C_LIGHT = 2.99792458e8
+
+
+def load_reference_dbf():
+    """13 x 16 complex DBF weights of the reference CSV (v8:148-150), via the repo data file."""
+    return np.load(os.path.join(DATA_DIR, 'dbf_coef_13x16.npy'))
+
+
+def make_config(*, prtNum, point_PRT=None, prt=None, channel_num, beam_num,
+                tao=(0.16e-6, 8e-6, 28e-6), gap_duration=(11.4e-6, 31.8e-6, 153.4e-6),
+                point_prt_segments=(228, 723, 2453), fs=25e6, fc=9450e6, B=20e6,
+                element_spacing=0.0138):
+    """Build ``config`` like v8:54-69.  Give either ``prt`` (seconds) or ``point_PRT``."""
+    if prt is None:
+        prt = point_PRT / fs
+    sc = dict(c=C_LIGHT, fs=fs, fc=fc, prtNum=int(prtNum), prt=prt, B=B, tao=list(tao),
+              gap_duration=list(gap_duration), point_prt_segments=[int(s) for s in point_prt_segments],
+              channel_num=int(channel_num), beam_num=int(beam_num))
+    sc['wavelength'] = sc['c'] / sc['fc']
+    sc['point_PRT'] = int(np.floor(prt * fs + 0.5))
+    return {'Sig_Config': sc, 'Array': {'element_spacing': element_spacing}}
+
+
+def default_cfar_params():
+    """v8:45-47."""
+    return dict(refCells_V=5, guardCells_V=10, refCells_R=5, guardCells_R=10, T_CFAR=8.0, method='GOCA')
+
+
+def default_cluster_params():
+    """v8:49-51."""
+    return dict(max_range_sep=30.0, max_vel_sep=0.4, max_angle_sep=5.0)
+
+
+def steering_weights(angles_deg, C, d, wl, taper=None):
+    """Synthetic DBF weights: W[b, c] = t_c exp(j 2 pi d c sin(theta_b) / wl) / sum(t).
+
+    With the kernel's convention y = x * W' (fsf:95) and channel phases
+    exp(j c dphi) (fsf:163-169), beam b peaks at theta_b.
+    """
+    t = np.ones(C) if taper is None else np.asarray(taper, float)
+    n = np.arange(C)
+    W = np.exp(1j * 2 * np.pi * d * np.outer(np.sin(np.deg2rad(angles_deg)), n) / wl)
+    return W * t[None, :] / t.sum()
+
+
+def calibrate_k_slopes(W, beam_angles_deg, d, wl):
+    """Restatement of calibrate_all_monopulse_slopes.m:35-73 for arbitrary B x C weights.
+
+    For each adjacent pair: scan 501 angles over +-|dtheta| around the crossover,
+    responses w * a(theta) with a = exp(j 2 pi d n sin(theta)/wl), n = 0..C-1,
+    ratio (A-B)/(A+B), and the slope of polyfit(real(ratio), angle_offset, 1) over
+    the 11 points nearest the crossover.  Used for synthetic-weight configs; the
+    amplitude monopulse of fsf:280-290 is what consumes it.
+    """
+    B, C = W.shape
+    n = np.arange(C)[:, None]
+    k = np.zeros(B - 1)
+    for p in range(B - 1):
+        a0, a1 = beam_angles_deg[p], beam_angles_deg[p + 1]
+        xo = (a0 + a1) / 2
+        wdt = abs(a0 - a1)
+        ang = np.linspace(xo - wdt, xo + wdt, 501)
+        sv = np.exp(1j * 2 * np.pi * d * n * np.sin(np.deg2rad(ang))[None, :] / wl)
+        # amplitude responses, consistent with the kernel's |.| monopulse (fsf:282-285)
+        rA = np.abs(np.conj(W[p]) @ sv)
+        rB = np.abs(np.conj(W[p + 1]) @ sv)
+        ratio = (rA - rB) / (rA + rB)
+        ci = int(np.argmin(np.abs(ang - xo)))
+        sl = slice(ci - 5, ci + 6)
+        k[p] = np.polyfit(ratio[sl], ang[sl] - xo, 1)[0]
+    return k
+
+
+def named_config(name):
+    """Return (config, cfar_params, cluster_params, dbf_W, beam_angles, k_lut)."""
+    cfar, clus = default_cfar_params(), default_cluster_params()
+    if name == 'reference':
+        cfg = make_config(prtNum=332, prt=232.76e-6, channel_num=16, beam_num=13)
+        W = load_reference_dbf()
+        return cfg, cfar, clus, W, list(V8_BEAM_ANGLES), list(V8_K_LUT)
+    if name == 'x2':
+        cfg = make_config(prtNum=128, point_PRT=4096, channel_num=16, beam_num=8,
+                          point_prt_segments=(228, 723, 1860))
+        W = load_reference_dbf()[:8]
+        return cfg, cfar, clus, W, list(V8_BEAM_ANGLES[:8]), list(V8_K_LUT[:7])
+    if name == 'small':
+        cfg = make_config(prtNum=64, point_PRT=3072, channel_num=16, beam_num=4,
+                          point_prt_segments=(228, 723, 836))
+        W = load_reference_dbf()[4:8]
+        return cfg, cfar, clus, W, list(V8_BEAM_ANGLES[4:8]), list(V8_K_LUT[4:7])
+    if name == 'plumbing':
+        cfg = make_config(prtNum=32, point_PRT=1024, channel_num=8, beam_num=1,
+                          tao=(0.16e-6, 2e-6, 6e-6), gap_duration=(2.84e-6, 8e-6, 12e-6),
+                          point_prt_segments=(64, 192, 256))
+        sc = cfg['Sig_Config']
+        W = steering_weights([10.0], 8, cfg['Array']['element_spacing'], sc['wavelength'])
+        return cfg, cfar, clus, W, [10.0], []
+    if name == 'x4':
+        import scipy.signal.windows as sw
+        cfg = make_config(prtNum=256, point_PRT=8192, channel_num=32, beam_num=16,
+                          point_prt_segments=(228, 723, 5956))
+        sc = cfg['Sig_Config']
+        d, wl = cfg['Array']['element_spacing'], sc['wavelength']
+        s = np.linspace(np.sin(np.deg2rad(-48.6)), np.sin(np.deg2rad(48.6)), 16)
+        ang = np.rad2deg(np.arcsin(s))
+        W = steering_weights(ang, 32, d, wl, taper=sw.taylor(32, nbar=4, sll=30, norm=False))
+        k = calibrate_k_slopes(W, ang, d, wl)
+        return cfg, cfar, clus, W, list(ang), list(k)
+    raise KeyError(name)
+
+
+def v8_2_targets():
+    """The five targets of main_simulate_echoes_with_array_v8_2.m:28-51."""
+    return [dict(Range=3000.0, Velocity=15.0, ElevationAngle=10.0, SNR_dB=-10.0),
+            dict(Range=5000.0, Velocity=20.0, ElevationAngle=5.0, SNR_dB=1.0),
+            dict(Range=6500.0, Velocity=10.0, ElevationAngle=15.0, SNR_dB=-20.0),
+            dict(Range=8000.0, Velocity=5.0, ElevationAngle=20.0, SNR_dB=5.0),
+            dict(Range=10000.0, Velocity=8.0, ElevationAngle=8.0, SNR_dB=15.0)]
+
+
+def evolve_targets(targets, config):
+    """v8:170-173: Range -= Velocity * T_frame (T_frame = prtNum * prt)."""
+    sc = config['Sig_Config']
+    T = sc['prtNum'] * sc['prt']
+    return [dict(t, Range=t['Range'] - t['Velocity'] * T) for t in targets]

@@ -1,0 +1,219 @@
+"""Host-side plan object over the C-ABI (include/rsp.h).
+
+Arrays use MATLAB index order (the reference's), stored column-major so they are
+passed to the library exactly as a MEX gateway would pass mxArray data:
+echo cube ``[P, N, C]``, range-Doppler maps ``[P, G, B]``, CFAR maps
+``[P, G, B-1]``.
+"""
+import ctypes as ct
+import numpy as np
+
+from . import _abi
+from ._abi import check, lib
+
+
+def _dptr(a):
+    return a.ctypes.data_as(ct.POINTER(ct.c_double))
+
+
+def _det_dict(d):
+    return {'v_idx': d.v_idx, 'r_idx': d.r_idx, 'pair_idx': d.pair_idx, 'amp': d.amp,
+            'Range': d.Range, 'Velocity': d.Velocity, 'Angle': d.Angle}
+
+
+def _tgt_dict(t):
+    return {'Range': t.Range, 'Velocity': t.Velocity, 'Angle': t.Angle, 'Power': t.Power}
+
+
+class Plan:
+    """One device plan = the reference's per-frame kernel bound to fixed config/precompute.
+
+    Parameters mirror ``fun_process_single_frame(targets, config, cfar_params,
+    cluster_params, precomputed_data, frame_idx)`` (fun_process_single_frame.m:13).
+    """
+
+    def __init__(self, config, cfar_params, cluster_params, precomputed_data, device=0, frames_per_launch=1):
+        sc = config['Sig_Config']
+        pre = precomputed_data
+        self.config = config
+        self._keep = []
+
+        def arr(x, cplx=False):
+            a = np.ascontiguousarray(np.asarray(x, np.complex128 if cplx else np.float64))
+            if cplx:
+                a = a.view(np.float64)
+            self._keep.append(a)
+            return _dptr(a)
+
+        self.cfg = _abi.SigConfig(c=sc['c'], fs=sc['fs'], fc=sc['fc'], prt=sc['prt'], wavelength=sc['wavelength'],
+                                  element_spacing=config['Array']['element_spacing'], prtNum=sc['prtNum'],
+                                  point_PRT=sc['point_PRT'], channel_num=sc['channel_num'], beam_num=sc['beam_num'])
+        self.cfar = _abi.CfarParams(refCells_V=cfar_params['refCells_V'], guardCells_V=cfar_params['guardCells_V'],
+                                    refCells_R=cfar_params['refCells_R'], guardCells_R=cfar_params['guardCells_R'],
+                                    T_CFAR=cfar_params['T_CFAR'])
+        self.cluster = _abi.ClusterParams(max_range_sep=cluster_params['max_range_sep'],
+                                          max_vel_sep=cluster_params['max_vel_sep'],
+                                          max_angle_sep=cluster_params['max_angle_sep'])
+        W = np.asarray(pre['DBF_coeffs_data_C'], np.complex128)
+        Wcm = np.asfortranarray(W).ravel(order='F')      # B x C column-major (MATLAB)
+        klut = np.asarray(pre['k_slopes_LUT'], float)
+        self.pre = _abi.Precomputed(
+            tx_pulse=arr(pre['tx_pulse'], True) if 'tx_pulse' in pre else None,
+            P_signal_unscaled=pre.get('P_signal_unscaled', 0.0),
+            DBF_coeffs_data_C=arr(Wcm, True), MF_narrow=arr(pre['MF_narrow']), n_MF_narrow=len(pre['MF_narrow']),
+            fir_delay=int(pre['fir_delay']), MF_medium_fft=arr(pre['MF_medium_fft'], True),
+            N_fft_med=int(pre['N_fft_med']), MF_long_fft=arr(pre['MF_long_fft'], True),
+            N_fft_long=int(pre['N_fft_long']), N_gate_narrow=int(pre['N_gate_narrow']),
+            N_gate_medium=int(pre['N_gate_medium']), N_gate_long=int(pre['N_gate_long']),
+            N_total_gate=int(pre['N_total_gate']), seg_start_narrow=int(pre['seg_start_narrow']),
+            seg_start_medium=int(pre['seg_start_medium']), seg_start_long=int(pre['seg_start_long']),
+            MTD_win=arr(pre['MTD_win']), range_axis=arr(pre['range_axis']), velocity_axis=arr(pre['velocity_axis']),
+            deltaR=float(pre['deltaR']), deltaV=float(pre['deltaV']), beam_angles_deg=arr(pre['beam_angles_deg']),
+            k_slopes_LUT=arr(klut if klut.size else np.zeros(1)))
+        h = ct.c_void_p()
+        check(lib().rsp_plan_create(ct.byref(self.cfg), ct.byref(self.cfar), ct.byref(self.cluster),
+                                    ct.byref(self.pre), int(device), int(frames_per_launch), ct.byref(h)))
+        self.h = h
+        s = _abi.Sizes()
+        check(lib().rsp_query_sizes(self.h, ct.byref(s)))
+        self.sizes = s
+        self.P, self.N, self.C, self.B, self.G = s.P, s.N, s.C, s.B, s.G
+
+    def close(self):
+        if getattr(self, 'h', None):
+            lib().rsp_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- synchronous frame paths ---------------------------------------------------------
+    def _frame_out(self, want_rdm, want_cfar, dets_cap=1 << 16, tcap=4096):
+        o = _abi.FrameOut()
+        bufs = {}
+        if want_rdm:
+            bufs['rdm'] = np.empty((self.P, self.G, self.B), np.complex128, order='F')
+            o.rdm = bufs['rdm'].ctypes.data_as(ct.POINTER(ct.c_double))
+        if want_cfar and self.B > 1:
+            bufs['cfar'] = np.empty((self.P, self.G, self.B - 1), np.float64, order='F')
+            o.cfar_maps = _dptr(bufs['cfar'])
+        dets = (_abi.Detection * dets_cap)()
+        tg = (_abi.Target * tcap)()
+        o.dets, o.dets_cap, o.targets, o.targets_cap = dets, dets_cap, tg, tcap
+        return o, bufs, dets, tg
+
+    @staticmethod
+    def _collect(o, bufs, dets, tg):
+        res = {'final_targets': [_tgt_dict(tg[i]) for i in range(o.n_targets)],
+               'detections': [_det_dict(dets[i]) for i in range(o.n_dets)]}
+        if 'rdm' in bufs:
+            res['rdm'] = bufs['rdm']
+        if 'cfar' in bufs:
+            res['cfar_maps'] = bufs['cfar']
+        return res
+
+    def process_cube(self, cube, frame_idx=1, want_rdm=False, want_cfar=False):
+        """S5..S11 on a noisy echo cube ``cube[m, n, c]`` (MATLAB [P x N x C])."""
+        cube = np.asarray(cube)
+        if cube.shape != (self.P, self.N, self.C):
+            raise ValueError('cube shape %r != (P, N, C) = %r' % (cube.shape, (self.P, self.N, self.C)))
+        if cube.dtype == np.complex64:
+            a, dt = np.asfortranarray(cube), _abi.RSP_C64
+        else:
+            a, dt = np.asfortranarray(cube, np.complex128), _abi.RSP_C128
+        o, bufs, dets, tg = self._frame_out(want_rdm, want_cfar)
+        check(lib().rsp_process_cube(self.h, a.ctypes.data_as(ct.c_void_p), dt, _abi.RSP_LAYOUT_PNC,
+                                     int(frame_idx), ct.byref(o)))
+        return self._collect(o, bufs, dets, tg)
+
+    def process_targets(self, targets, frame_idx=1, seed=20250101, p_noise=1.0, want_rdm=False, want_cfar=False):
+        """fsf:13 path: device S4 synthesis + S4.1 Philox noise + S5..S11."""
+        tin = self._targets_in(targets)
+        o, bufs, dets, tg = self._frame_out(want_rdm, want_cfar)
+        check(lib().rsp_process_targets(self.h, tin, len(targets), int(frame_idx), int(seed), float(p_noise),
+                                        ct.byref(o)))
+        return self._collect(o, bufs, dets, tg)
+
+    @staticmethod
+    def _targets_in(targets):
+        arr = (_abi.TargetIn * max(len(targets), 1))()
+        for i, t in enumerate(targets):
+            arr[i] = _abi.TargetIn(t['Range'], t['Velocity'], t['ElevationAngle'], t['SNR_dB'])
+        return arr
+
+    def process_stage2(self, iq_beams):
+        """process_stage2_mtd backing: beams ``iq[m, n, b]`` -> (MTD [P,G,B], PC [P,G,B])."""
+        iq = np.asarray(iq_beams)
+        if iq.shape != (self.P, self.N, self.B):
+            raise ValueError('iq shape %r != (P, N, B) = %r' % (iq.shape, (self.P, self.N, self.B)))
+        if iq.dtype == np.complex64:
+            a, dt = np.asfortranarray(iq), _abi.RSP_C64
+        else:
+            a, dt = np.asfortranarray(iq, np.complex128), _abi.RSP_C128
+        mtd = np.empty((self.P, self.G, self.B), np.complex128, order='F')
+        pc = np.empty((self.P, self.G, self.B), np.complex128, order='F')
+        check(lib().rsp_process_stage2(self.h, a.ctypes.data_as(ct.c_void_p), dt,
+                                       mtd.ctypes.data_as(ct.POINTER(ct.c_double)),
+                                       pc.ctypes.data_as(ct.POINTER(ct.c_double))))
+        return mtd, pc
+
+    # ---- device-resident queue -------------------------------------------------------------
+    def device_alloc(self, nbytes):
+        p = ct.c_void_p()
+        check(lib().rsp_device_alloc(self.h, int(nbytes), ct.byref(p)))
+        return p.value
+
+    def device_free(self, ptr):
+        check(lib().rsp_device_free(self.h, ct.c_void_p(ptr)))
+
+    def device_upload(self, ptr, host):
+        host = np.ascontiguousarray(host)
+        check(lib().rsp_device_upload(self.h, ct.c_void_p(ptr), host.ctypes.data_as(ct.c_void_p), host.nbytes))
+
+    def device_download(self, ptr, count, dtype):
+        out = np.empty(int(count), dtype)
+        check(lib().rsp_device_download(self.h, out.ctypes.data_as(ct.c_void_p), ct.c_void_p(ptr), out.nbytes))
+        return out
+
+    def upload_cube(self, ptr, cube):
+        """Upload a [P, N, C] cube as complex64 column-major to device pointer ``ptr``."""
+        a = np.asfortranarray(np.asarray(cube).astype(np.complex64))
+        check(lib().rsp_device_upload(self.h, ct.c_void_p(ptr), a.ctypes.data_as(ct.c_void_p), a.nbytes))
+
+    def synthesize_device(self, ptr, targets, frame_idx, seed=20250101, p_noise=1.0):
+        tin = self._targets_in(targets)
+        check(lib().rsp_synthesize_device(self.h, tin, len(targets), int(frame_idx), int(seed), float(p_noise),
+                                          ct.c_void_p(ptr)))
+
+    def enqueue(self, ptr, frame_idx):
+        check(lib().rsp_enqueue_device(self.h, ct.c_void_p(ptr), int(frame_idx)))
+
+    def drain(self):
+        check(lib().rsp_drain(self.h))
+
+    def sync(self):
+        check(lib().rsp_device_sync(self.h))
+
+    def results(self, clear=True):
+        nf, nt = ct.c_int32(), ct.c_int64()
+        check(lib().rsp_results_count(self.h, ct.byref(nf), ct.byref(nt)))
+        out = []
+        buf = (_abi.Target * 4096)()
+        for i in range(nf.value):
+            fi, n, nd = ct.c_int32(), ct.c_int32(), ct.c_int32()
+            check(lib().rsp_results_get(self.h, i, ct.byref(fi), buf, 4096, ct.byref(n), ct.byref(nd)))
+            out.append({'frame_idx': fi.value, 'n_dets': nd.value,
+                        'final_targets': [_tgt_dict(buf[j]) for j in range(n.value)]})
+        if clear:
+            check(lib().rsp_results_clear(self.h))
+        return out
+
+    def profile_stages(self, d_cube, iters=20):
+        n = self.sizes.n_stages
+        ms = (ct.c_float * n)()
+        by = (ct.c_int64 * n)()
+        check(lib().rsp_profile_stages(self.h, ct.c_void_p(d_cube), int(iters), ms, by, n))
+        return [{'stage': lib().rsp_stage_name(i).decode(), 'ms': ms[i], 'bytes': by[i]} for i in range(n)]
