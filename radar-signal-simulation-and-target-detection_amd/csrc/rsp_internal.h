@@ -37,7 +37,10 @@ struct K2Job {
 
 struct Geometry {
     int C, B, P, N, G;
+    int Gp;          // row stride of the magnitude maps (G rounded up to 4 floats)
     int NT, nU, ntiles, Ppad;
+    int wc_elems;    // conj(W) entries, [CP][BMAX]
+    int twPp_elems;  // per-pass twiddles of the P-point FFT
     int pow2P, logP, nradP, radP[8];
     int nseg, njobs, nwg_k2;
     int cfar_RT, cfar_hR, cfar_W;
@@ -50,6 +53,7 @@ struct FramePtrs {
     const float2* in[RSP_MAX_F];   // K1 input cube (PNC) or beam cube
     float2* z[RSP_MAX_F];          // compacted Doppler-domain rows
     float2* rdm[RSP_MAX_F];        // [B][P][G]
+    float* mag[RSP_MAX_F];         // |rdm| [B][P][Gp] (K2 epilogue, read by K3)
     DevDet* dets[RSP_MAX_F];
     int* count[RSP_MAX_F];
 };
@@ -57,13 +61,14 @@ struct FramePtrs {
 struct DevConsts {
     const float2* Wc;        // conj(W) [B][C]
     const float* win;        // MTD window [P]
-    const float2* twP;       // W_P^i table
+    const float2* twP;       // W_P^i table (direct DFT path)
+    const float2* twPp;      // per-pass Stockham twiddles of the P-point FFT
     const int* nof;          // compacted index -> sample index (-1 = pad)
     const SegDesc* segs;
     const K2Job* jobs;
     const float* taps;
     const float2* H;         // overlap-save spectra, 1/M scaled
-    const float2* twM;       // W_M tables
+    const float2* twM;       // per-pass Stockham twiddles of each overlap-save block size
     const double* range_axis;
     const double* velocity_axis;
     const double* beam_angles;

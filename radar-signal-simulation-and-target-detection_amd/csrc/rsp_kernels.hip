@@ -102,48 +102,49 @@ template <> struct Log2R<4> { static constexpr int v = 2; };
 template <> struct Log2R<8> { static constexpr int v = 3; };
 template <> struct Log2R<16> { static constexpr int v = 4; };
 
-// LDS index inside a row: PAD inserts one complex every 16 to break power-of-two strides.
-template <bool PAD>
-__device__ __forceinline__ int lidx(int i) { return PAD ? i + (i >> 4) : i; }
+// LDS index inside a row: SH > 0 inserts one complex every 2^SH to break power-of-two
+// strides (tools/lds_conflicts.py models the gfx950 bank rules for each pass).
+template <int SH>
+__device__ __forceinline__ int lidx(int i) { return SH ? i + (i >> SH) : i; }
 
 // Store policies for the Stockham pass output.
 struct StoreLds {
     float2* buf; int rs; const float2* H;   // optional pointwise multiply (natural order)
-    template <bool PAD>
+    template <int SH>
     __device__ __forceinline__ void put(int row, int o, float2 x) const {
         if (H) x = cmul(x, H[o]);
-        buf[row * rs + lidx<PAD>(o)] = x;
+        buf[row * rs + lidx<SH>(o)] = x;
     }
 };
 
 // One Stockham radix-R pass (Govindaraju et al. formulation) over `nrows` rows of
-// length L (= 2^lgL) held in LDS (row stride rs).  Ns = product of earlier radices.
-// Reads stride L/R (conflict-light), twiddle W_{Ns R}^{(j mod Ns) r} from the W_L table,
+// length L = 2^LGL held in LDS (row stride rs).  Ns = 2^LGNS = product of the earlier
+// radices.  Reads stride L/R, twiddle W_{Ns R}^{(j mod Ns) r} from this pass's table
+// tw[k][r-1] (LDS; built by build_pass_twiddles() in rsp_plan.cpp),
 // radix-R DFT, writes positions expand(j, Ns, R) + r Ns.  In place: all reads, barrier,
-// all writes, barrier.
-template <int R, bool INV, int NB, bool PAD, class St>
-__device__ __forceinline__ void sh_pass(float2* buf, int rs, int lgL, int lgNs, int nrows,
-                                        const float2* __restrict__ tw, const St& st) {
+// all writes, barrier.  Every size is a compile-time constant, so a pass is straight-line
+// code and no address math is carried across passes.
+template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, class St>
+__device__ __forceinline__ void sh_pass(float2* buf, int rs, int nrows, const float2* tw, const St& st) {
     constexpr int lgR = Log2R<R>::v;
-    const int lgnb = lgL - lgR;
-    const int nb = 1 << lgnb;
+    constexpr int lgnb = LGL - lgR;
+    constexpr int nb = 1 << lgnb;
+    constexpr int Ns = 1 << LGNS;
     const int total = nb * nrows;
-    const int Ns = 1 << lgNs;
     const int tid = threadIdx.x;
     float2 v[NB][R];
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
-        const int beta = tid + t * RSP_THREADS;
+        const int beta = tid + t * NTHR;
         if (beta < total) {
             const int row = beta >> lgnb, j = beta & (nb - 1);
             const int k = j & (Ns - 1);
             const float2* src = buf + row * rs;
-            const int step = k << (lgL - lgNs - lgR);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                float2 x = src[lidx<PAD>(j + r * nb)];
-                if (r > 0 && lgNs > 0) {
-                    float2 w = tw[r * step];
+                float2 x = src[lidx<SH>(j + r * nb)];
+                if (r > 0 && LGNS > 0) {
+                    float2 w = tw[k * (R - 1) + r - 1];   // per-pass table [k][r-1]: consecutive k -> stride R-1
                     if (INV) w.y = -w.y;
                     x = cmul(x, w);
                 }
@@ -154,27 +155,63 @@ __device__ __forceinline__ void sh_pass(float2* buf, int rs, int lgL, int lgNs, 
     __syncthreads();
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
-        const int beta = tid + t * RSP_THREADS;
+        const int beta = tid + t * NTHR;
         if (beta < total) {
             const int row = beta >> lgnb, j = beta & (nb - 1);
             const int k = j & (Ns - 1);
             Dft<R, INV>::run(v[t]);
-            const int idxD = ((j >> lgNs) << (lgNs + lgR)) + k;
+            const int idxD = ((j >> LGNS) << (LGNS + lgR)) + k;
 #pragma unroll
-            for (int r = 0; r < R; ++r) st.template put<PAD>(row, idxD + r * Ns, v[t][r]);
+            for (int r = 0; r < R; ++r) st.template put<SH>(row, idxD + r * Ns, v[t][r]);
         }
     }
     __syncthreads();
 }
 
-template <int PTS, bool INV, bool PAD, class St>
-__device__ __forceinline__ void run_pass(int R, float2* buf, int rs, int lgL, int lgNs, int nrows,
-                                         const float2* __restrict__ tw, const St& st) {
-    switch (R) {
-        case 16: sh_pass<16, INV, (PTS + 15) / 16, PAD>(buf, rs, lgL, lgNs, nrows, tw, st); break;
-        case 8: sh_pass<8, INV, (PTS + 7) / 8, PAD>(buf, rs, lgL, lgNs, nrows, tw, st); break;
-        case 4: sh_pass<4, INV, (PTS + 3) / 4, PAD>(buf, rs, lgL, lgNs, nrows, tw, st); break;
-        default: sh_pass<2, INV, (PTS + 1) / 2, PAD>(buf, rs, lgL, lgNs, nrows, tw, st); break;
+// Radix plan of a 2^m-point FFT: radix-16 passes, remainder as 8/4 (m = 5 -> 8 x 4);
+// must match radix_plan() in rsp_plan.cpp.
+constexpr int rad_bits(int m, int q) {
+    for (int i = 0; i < q; ++i) m -= (m == 5) ? 3 : (m >= 4 ? 4 : m);
+    return (m == 5) ? 3 : (m >= 4 ? 4 : m);
+}
+constexpr int n_passes(int m) {
+    int n = 0;
+    while (m > 0) {
+        m -= (m == 5) ? 3 : (m >= 4 ? 4 : m);
+        ++n;
+    }
+    return n;
+}
+
+// Offset of pass q's twiddle table inside the concatenated per-pass tables of a 2^LG FFT:
+// pass i >= 1 owns Ns_i * (R_i - 1) entries (pass 0 has Ns = 1, no twiddles).
+constexpr int tw_pass_off(int LG, int q) {
+    int off = 0, lgns = 0;
+    for (int i = 0; i < q; ++i) {
+        const int rb = rad_bits(LG, i);
+        if (i > 0) off += (1 << lgns) * ((1 << rb) - 1);
+        lgns += rb;
+    }
+    return off;
+}
+constexpr int tw_total(int LG) { return tw_pass_off(LG, n_passes(LG)); }
+
+// All passes of a 2^LG-point FFT over `nrows` rows; the last pass stores through `last`.
+// PTS = complex points per thread (nrows * L / NTHR).
+template <int LG, int Q, int LGNS, int PTS, bool INV, int SH, int NTHR, class StMid, class StLast>
+__device__ __forceinline__ void fft_passes(float2* buf, int rs, int nrows, const float2* tw, const StMid& mid,
+                                           const StLast& last) {
+    constexpr int NP = n_passes(LG);
+    if constexpr (Q < NP) {
+        constexpr int RB = rad_bits(LG, Q);
+        constexpr int R = 1 << RB;
+        constexpr int NB = (PTS + R - 1) / R;
+        const float2* twq = tw + tw_pass_off(LG, Q);
+        if constexpr (Q == NP - 1)
+            sh_pass<R, INV, NB, SH, NTHR, LG, LGNS>(buf, rs, nrows, twq, last);
+        else
+            sh_pass<R, INV, NB, SH, NTHR, LG, LGNS>(buf, rs, nrows, twq, mid);
+        fft_passes<LG, Q + 1, LGNS + RB, PTS, INV, SH, NTHR>(buf, rs, nrows, tw, mid, last);
     }
 }
 
@@ -189,99 +226,117 @@ __device__ __forceinline__ size_t zaddr(const Geometry& g, int b, int v, int np)
 // ======================================================================================
 // K1: DBF + MTD window + slow-time FFT + fftshift -> compacted rows
 // ======================================================================================
-template <int BMAX>
-__global__ __launch_bounds__(RSP_THREADS, 2) void k1_dbf_mtd(Geometry g, DevConsts k, FramePtrs fp, int mode) {
-    extern __shared__ __attribute__((aligned(16))) float2 Y[];   // [B][NT][Ppad]
+#define K1_THREADS 512
+#define K1_SH 4   // LDS pad shift of the slow-time FFT rows (row stride P + P/16)
+
+// Slow-time FFT of every (beam, sample) column in LDS for the runtime log2(P).
+__device__ __forceinline__ void k1_fft(int lgp, float2* Y, int Ppad, int ncols, const float2* twl) {
+    StoreLds st{Y, Ppad, nullptr};
+    switch (lgp) {
+        case 4: fft_passes<4, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, st); break;
+        case 5: fft_passes<5, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, st); break;
+        case 6: fft_passes<6, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, st); break;
+        case 7: fft_passes<7, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, st); break;
+        case 8: fft_passes<8, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, st); break;
+        default: fft_passes<9, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, st); break;
+    }
+}
+
+// BMAX = beams rounded up (4/8/16), CP = channels rounded up (8/16/32).  Weights are conj(W)
+// laid out [CP][BMAX] in LDS, zero for padded beams/channels, so the DBF has no data-dependent
+// branches: CP unconditional 8-B loads per (sample, pulse) all in flight together, then
+// BMAX*CP complex FMAs whose weights are LDS broadcast reads.
+template <int BMAX, int CP>
+__global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConsts k, FramePtrs fp, int mode) {
+    extern __shared__ __attribute__((aligned(16))) float2 Y[];   // [B][NT][Ppad] | twiddles | W
     const int f = blockIdx.y, tile = blockIdx.x;
     const int B = g.B, C = g.C, P = g.P, NT = g.NT, Ppad = g.Ppad;
+    float2* twl = Y + B * NT * Ppad;
+    float2* Wl = twl + ((g.P + 1) & ~1);   // 16-B aligned
+    const bool fft = (mode & 2) && g.pow2P;
+    const int sh = fft ? K1_SH : 0;
+    if (fft)
+        for (int i = threadIdx.x; i < g.twPp_elems; i += K1_THREADS) twl[i] = k.twPp[i];
+    if (mode & 1)
+        for (int i = threadIdx.x; i < CP * BMAX; i += K1_THREADS) Wl[i] = k.Wc[i];
+    __syncthreads();
     const float2* __restrict__ x = fp.in[f];
-    const size_t NP4 = (size_t)g.N * P / 2;   // channel stride in float4 (2 pulses)
-    const int halfP = P >> 1;
-    const int items = NT * halfP;
-    // ---- Phase A: DBF (fsf:93-97) + MTD window (fsf:134), two pulses per thread (16 B loads)
-    for (int it = threadIdx.x; it < items; it += RSP_THREADS) {
-        const int nl = it / halfP, pp = it - nl * halfP;
+    const size_t NP = (size_t)g.N * P;   // channel stride
+    const int items = NT * P;
+    // ---- Phase A: DBF (fsf:93-97) + MTD window (fsf:134), one pulse per thread item
+    for (int it = threadIdx.x; it < items; it += K1_THREADS) {
+        const int nl = it / P, p = it - nl * P;
         const int n = k.nof[tile * NT + nl];
-        float4 acc[BMAX];
+        float2 acc[BMAX];
 #pragma unroll
-        for (int b = 0; b < BMAX; ++b) acc[b] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int b = 0; b < BMAX; ++b) acc[b] = make_float2(0.f, 0.f);
         if (n >= 0) {
-            const float4* __restrict__ src = reinterpret_cast<const float4*>(x + (size_t)n * P) + pp;
+            const float2* __restrict__ src = x + (size_t)n * P + p;
             if (mode & 1) {
-                for (int c0 = 0; c0 < C; c0 += 8) {
-                    float4 xv[8];
+                float2 xv[CP];
 #pragma unroll
-                    for (int u = 0; u < 8; ++u)
-                        xv[u] = (c0 + u < C) ? src[(size_t)(c0 + u) * NP4] : make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int u = 0; u < CP; ++u) xv[u] = src[(size_t)min(u, C - 1) * NP];   // padded: weight 0
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        if (c0 + u < C) {
+                for (int u = 0; u < CP; ++u) {
+                    const float4* wrow = reinterpret_cast<const float4*>(Wl + u * BMAX);
 #pragma unroll
-                            for (int b = 0; b < BMAX; ++b) {
-                                if (b < B) {
-                                    const float2 w = k.Wc[b * C + c0 + u];   // conj(W[b][c])
-                                    acc[b].x += xv[u].x * w.x - xv[u].y * w.y;
-                                    acc[b].y += xv[u].x * w.y + xv[u].y * w.x;
-                                    acc[b].z += xv[u].z * w.x - xv[u].w * w.y;
-                                    acc[b].w += xv[u].z * w.y + xv[u].w * w.x;
-                                }
-                            }
-                        }
+                    for (int b2 = 0; b2 < BMAX / 2; ++b2) {
+                        const float4 w2 = wrow[b2];
+                        acc[2 * b2].x += xv[u].x * w2.x - xv[u].y * w2.y;
+                        acc[2 * b2].y += xv[u].x * w2.y + xv[u].y * w2.x;
+                        acc[2 * b2 + 1].x += xv[u].x * w2.z - xv[u].y * w2.w;
+                        acc[2 * b2 + 1].y += xv[u].x * w2.w + xv[u].y * w2.z;
                     }
+                    __builtin_amdgcn_sched_barrier(0);   // weight reads stay next to their FMAs
                 }
             } else {
 #pragma unroll
                 for (int b = 0; b < BMAX; ++b)
-                    if (b < B) acc[b] = src[(size_t)b * NP4];
+                    if (b < B) acc[b] = src[(size_t)b * NP];
             }
             if (mode & 2) {
-                const float w0 = k.win[2 * pp], w1 = k.win[2 * pp + 1];
+                const float w = k.win[p];
 #pragma unroll
                 for (int b = 0; b < BMAX; ++b) {
-                    acc[b].x *= w0; acc[b].y *= w0;
-                    acc[b].z *= w1; acc[b].w *= w1;
+                    acc[b].x *= w;
+                    acc[b].y *= w;
                 }
             }
         }
+        const int ip = sh ? p + (p >> K1_SH) : p;
 #pragma unroll
         for (int b = 0; b < BMAX; ++b)
-            if (b < B) *reinterpret_cast<float4*>(&Y[(b * NT + nl) * Ppad + 2 * pp]) = acc[b];
+            if (b < B) Y[(b * NT + nl) * Ppad + ip] = acc[b];
     }
     __syncthreads();
     float2* __restrict__ z = fp.z[f];
     const int zslab = P * NT;   // contiguous [P][NT] slab per (b, tile)
+    const int lgNT = ilog2(NT);
     if (!(mode & 2)) {
-        for (int e = threadIdx.x; e < B * zslab; e += RSP_THREADS) {
+        for (int e = threadIdx.x; e < B * zslab; e += K1_THREADS) {
             const int b = e / zslab, rem = e - b * zslab;
-            const int v = rem / NT, nl = rem - v * NT;
+            const int v = rem >> lgNT, nl = rem & (NT - 1);
             z[((size_t)b * g.ntiles + tile) * zslab + rem] = Y[(b * NT + nl) * Ppad + v];
         }
         return;
     }
     const int half = P >> 1;
-    if (g.pow2P) {
+    if (fft) {
         // ---- Phase B: P-point FFT of every (b, nl) column (fsf:135)
-        const int ncols = B * NT;
-        StoreLds st{Y, Ppad, nullptr};
-        int lgNs = 0;
-        for (int q = 0; q < g.nradP; ++q) {
-            const int R = g.radP[q];
-            run_pass<32, false, false>(R, Y, Ppad, g.logP, lgNs, ncols, k.twP, st);
-            lgNs += ilog2(R);
-        }
+        k1_fft(g.logP, Y, Ppad, B * NT, twl);
         // ---- Phase C: fftshift (fsf:135) + coalesced store of the [P][NT] slabs
-        for (int e = threadIdx.x; e < B * zslab; e += RSP_THREADS) {
+        for (int e = threadIdx.x; e < B * zslab; e += K1_THREADS) {
             const int b = e / zslab, rem = e - b * zslab;
-            const int v = rem / NT, nl = rem - v * NT;
+            const int v = rem >> lgNT, nl = rem & (NT - 1);
             int src = v - half;
             if (src < 0) src += P;
-            z[((size_t)b * g.ntiles + tile) * zslab + rem] = Y[(b * NT + nl) * Ppad + src];
+            z[((size_t)b * g.ntiles + tile) * zslab + rem] = Y[(b * NT + nl) * Ppad + src + (src >> K1_SH)];
         }
     } else {
         // non power-of-two P: direct DFT straight to global (O(P^2) per column)
-        for (int e = threadIdx.x; e < B * zslab; e += RSP_THREADS) {
+        for (int e = threadIdx.x; e < B * zslab; e += K1_THREADS) {
             const int b = e / zslab, rem = e - b * zslab;
-            const int v = rem / NT, nl = rem - v * NT;
+            const int v = rem >> lgNT, nl = rem & (NT - 1);
             int kk = v - half;
             if (kk < 0) kk += P;
             const float2* col = Y + (b * NT + nl) * Ppad;
@@ -300,18 +355,89 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k1_dbf_mtd(Geometry g, DevCons
 // ======================================================================================
 // K2: pulse compression of every row (fsf:101-126)
 // ======================================================================================
-struct StoreRdm {   // last inverse pass: keep outputs i in [Lh-1, Lh-1+V) that map to gates < gend
-    float2* rdm; int G; int row0; int rows_total; int Lh1; int g0; int gend;
-    template <bool PAD>
+__device__ __forceinline__ float cabsf(float2 a) { return sqrtf(a.x * a.x + a.y * a.y); }
+
+struct StoreRdm {   // last inverse pass: keep outputs i in [Lh-1, Lh-1+V) that map to gates < gend;
+                    // also writes |x| (the CFAR input, fsf:184-185) into the magnitude map
+    float2* rdm; float* mag; int G; int Gp; int row0; int rows_total; int Lh1; int g0; int gend;
+    template <int SH>
     __device__ __forceinline__ void put(int row, int o, float2 x) const {
         const int gg = g0 + o - Lh1;
         const int rho = row0 + row;
-        if (o >= Lh1 && gg < gend && rho < rows_total) rdm[(size_t)rho * G + gg] = x;
+        if (o >= Lh1 && gg < gend && rho < rows_total) {
+            rdm[(size_t)rho * G + gg] = x;
+            mag[(size_t)rho * Gp + gg] = cabsf(x);
+        }
     }
 };
 
+#define K2_SH 5   // one pad complex per 32 (tools/lds_conflicts.py)
+#define K2_LDS_DATA (RSP_K2_POINTS + (RSP_K2_POINTS >> K2_SH))
+#define K2_MAXM 2048
+
+// One overlap-save block of one FFT segment for RSP_K2_POINTS / 2^LGM adjacent rows.
+template <int LGM>
+__device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k, const SegDesc& sd, const K2Job& job,
+                                           const float2* __restrict__ z, float2* __restrict__ rdm,
+                                           float* __restrict__ mag, int row0, int rows_total, float2* L) {
+    constexpr int M = 1 << LGM;
+    constexpr int rows = RSP_K2_POINTS / M;
+    constexpr int rs = M + (M >> K2_SH);
+    const int P = g.P, G = g.G;
+    const int lo = sd.lo, hi = sd.hi, off = sd.off;
+    const int tid = threadIdx.x;
+    const int Lh1 = sd.Lh - 1;
+    const int g0 = sd.ga + job.blk * sd.V;
+    const int a = sd.seg_lo + g0 - Lh1;           // sample index of u[0]
+    float2* twl = L + K2_LDS_DATA;
+    float2* Hl = twl + K2_MAXM;
+    // issue every global load of the workgroup before the first LDS store:
+    // 16 samples + 2 x M/256 table entries per thread in flight together
+    float2 val[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const int e = tid + u * RSP_THREADS;
+        const int rl = e >> LGM, i = e & (M - 1);
+        const int rho = row0 + rl;
+        const int n = a + i;
+        val[u] = make_float2(0.f, 0.f);
+        if (rho < rows_total && n >= lo && n <= hi) {
+            const int b = rho / P, v = rho - b * P;
+            val[u] = z[zaddr(g, b, v, n - lo + off)];
+        }
+    }
+    constexpr int NT_TAB = (M + RSP_THREADS - 1) / RSP_THREADS;
+    constexpr int NTW = tw_total(LGM);
+    float2 tv[NT_TAB], hv[NT_TAB];
+#pragma unroll
+    for (int u = 0; u < NT_TAB; ++u) {
+        const int i = tid + u * RSP_THREADS;
+        if (i < NTW) tv[u] = k.twM[sd.tw_off + i];
+        if (i < M) hv[u] = k.H[sd.H_off + i];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const int e = tid + u * RSP_THREADS;
+        L[(e >> LGM) * rs + lidx<K2_SH>(e & (M - 1))] = val[u];
+    }
+#pragma unroll
+    for (int u = 0; u < NT_TAB; ++u) {
+        const int i = tid + u * RSP_THREADS;
+        if (i < NTW) twl[i] = tv[u];
+        if (i < M) Hl[i] = hv[u];
+    }
+    __syncthreads();
+    // forward FFT; the last pass multiplies by the block filter spectrum H (1/M folded in)
+    fft_passes<LGM, 0, 0, 16, false, K2_SH, RSP_THREADS>(L, rs, rows, twl, StoreLds{L, rs, nullptr},
+                                                        StoreLds{L, rs, Hl});
+    // inverse FFT; the last pass keeps the valid overlap-save outputs = stitched gates
+    const int gend = min(sd.gb, g0 + sd.V);
+    fft_passes<LGM, 0, 0, 16, true, K2_SH, RSP_THREADS>(L, rs, rows, twl, StoreLds{L, rs, nullptr},
+                                                       StoreRdm{rdm, mag, G, g.Gp, row0, rows_total, Lh1, g0, gend});
+}
+
 __global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k, FramePtrs fp, int rows_total) {
-    extern __shared__ __attribute__((aligned(16))) float2 L[];
+    extern __shared__ __attribute__((aligned(16))) float2 L[];   // data | twiddles (M) | H (M)
     const int f = blockIdx.y;
     const int wg = blockIdx.x;
     int ji = 0;
@@ -322,65 +448,50 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k,
     const int row0 = (wg - job.wg_begin) * rows;
     const float2* __restrict__ z = fp.z[f];
     float2* __restrict__ rdm = fp.rdm[f];
+    float* __restrict__ mag = fp.mag[f];
     const int P = g.P, G = g.G;
     const int lo = sd.lo, hi = sd.hi, off = sd.off;
+    const int tid = threadIdx.x;
 
     if (sd.type == 1) {
-        const int M = sd.M, lgM = sd.logM, Lh1 = sd.Lh - 1;
-        const int g0 = sd.ga + job.blk * sd.V;
-        const int a = sd.seg_lo + g0 - Lh1;           // sample index of u[0]
-        const int rs = M + (M >> 4);
-        // load u (masked to the needed window) into padded LDS rows
-        for (int e = threadIdx.x; e < rows * M; e += RSP_THREADS) {
-            const int rl = e >> lgM, i = e & (M - 1);
-            const int rho = row0 + rl;
-            const int n = a + i;
-            float2 val = make_float2(0.f, 0.f);
-            if (rho < rows_total && n >= lo && n <= hi) {
-                const int b = rho / P, v = rho - b * P;
-                val = z[zaddr(g, b, v, n - lo + off)];
-            }
-            L[rl * rs + lidx<true>(i)] = val;
-        }
-        __syncthreads();
-        const float2* tw = k.twM + sd.tw_off;
-        const float2* H = k.H + sd.H_off;
-        int lgNs = 0;
-        for (int q = 0; q < sd.nrad; ++q) {                       // forward FFT, last pass x H
-            StoreLds st{L, rs, (q == sd.nrad - 1) ? H : nullptr};
-            run_pass<16, false, true>(sd.rad[q], L, rs, lgM, lgNs, rows, tw, st);
-            lgNs += ilog2(sd.rad[q]);
-        }
-        lgNs = 0;
-        const int gend = min(sd.gb, g0 + sd.V);
-        for (int q = 0; q < sd.nrad; ++q) {                       // inverse FFT (1/M folded in H)
-            if (q == sd.nrad - 1) {
-                StoreRdm st{rdm, G, row0, rows_total, Lh1, g0, gend};
-                run_pass<16, true, true>(sd.rad[q], L, rs, lgM, lgNs, rows, tw, st);
-            } else {
-                StoreLds st{L, rs, nullptr};
-                run_pass<16, true, true>(sd.rad[q], L, rs, lgM, lgNs, rows, tw, st);
-            }
-            lgNs += ilog2(sd.rad[q]);
+        switch (sd.logM) {
+            case 6: k2_fft_job<6>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+            case 7: k2_fft_job<7>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+            case 8: k2_fft_job<8>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+            case 9: k2_fft_job<9>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+            case 10: k2_fft_job<10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+            default: k2_fft_job<11>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
         }
     } else {
         // direct FIR (narrow segment): filter() + circshift(-fir_delay) (fsf:111-112)
         const int W = hi - lo + 1;
-        float* taps = reinterpret_cast<float*>(L + rows * W);
-        for (int e = threadIdx.x; e < sd.ntaps; e += RSP_THREADS) taps[e] = k.taps[sd.taps_off + e];
-        for (int e = threadIdx.x; e < rows * W; e += RSP_THREADS) {
-            const int rl = e / W, i = e - rl * W;
-            const int rho = row0 + rl;
-            float2 val = make_float2(0.f, 0.f);
-            if (rho < rows_total) {
-                const int b = rho / P, v = rho - b * P;
-                val = z[zaddr(g, b, v, i + off)];
+        const int nw = rows * W;
+        float* taps = reinterpret_cast<float*>(L + nw);
+        for (int e = tid; e < sd.ntaps; e += RSP_THREADS) taps[e] = k.taps[sd.taps_off + e];
+        for (int e0 = 0; e0 < nw; e0 += 16 * RSP_THREADS) {
+            float2 val[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int e = e0 + tid + u * RSP_THREADS;
+                val[u] = make_float2(0.f, 0.f);
+                if (e < nw) {
+                    const int rl = e / W, i = e - rl * W;
+                    const int rho = row0 + rl;
+                    if (rho < rows_total) {
+                        const int b = rho / P, v = rho - b * P;
+                        val[u] = z[zaddr(g, b, v, i + off)];
+                    }
+                }
             }
-            L[e] = val;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int e = e0 + tid + u * RSP_THREADS;
+                if (e < nw) L[e] = val[u];
+            }
         }
         __syncthreads();
         const int nout = sd.gb - sd.ga;
-        for (int e = threadIdx.x; e < rows * nout; e += RSP_THREADS) {
+        for (int e = tid; e < rows * nout; e += RSP_THREADS) {
             const int rl = e / nout, gi = e - rl * nout;
             const int rho = row0 + rl;
             if (rho >= rows_total) continue;
@@ -400,6 +511,7 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k,
                 }
             }
             rdm[(size_t)rho * G + gg] = acc;
+            mag[(size_t)rho * g.Gp + gg] = cabsf(acc);
         }
     }
 }
@@ -411,29 +523,31 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k,
 // equally spaced points (fsf:257-260, 272-275); returns the first-argmax abscissa.
 __device__ double spline_peak(const double* y, int n, int interp) {
     const int nq = (n - 1) * interp + 1;
+    const double dx = (interp == 8) ? 0.125 : (interp == 4 ? 0.25 : 1.0 / interp);   // exact steps
+    const double sixth = 1.0 / 6.0;
     double Mv[5] = {0, 0, 0, 0, 0};
-    if (n == 5) {
+    if (n == 5) {   // not-a-knot second derivatives, unit spacing (closed form of the 5x5 system)
         Mv[1] = y[0] - 2.0 * y[1] + y[2];
         Mv[3] = y[2] - 2.0 * y[3] + y[4];
         Mv[2] = (6.0 * (y[1] - 2.0 * y[2] + y[3]) - Mv[1] - Mv[3]) * 0.25;
         Mv[0] = 2.0 * Mv[1] - Mv[2];
         Mv[4] = 2.0 * Mv[3] - Mv[2];
     }
+    const double d1 = y[1] - y[0], d2 = y[2] - 2.0 * y[1] + y[0];
+    const double d3 = (n >= 4) ? y[3] - 3.0 * y[2] + 3.0 * y[1] - y[0] : 0.0;
     double best = -INFINITY, bx = 0.0;
     for (int q = 0; q < nq; ++q) {
-        const double xq = (double)q / interp;
+        const double xq = q * dx;
         double val;
         if (n == 5) {
-            int i = (int)xq;
+            int i = q / interp;
             if (i > 3) i = 3;
             const double t = xq - i, u = 1.0 - t;
-            val = u * y[i] + t * y[i + 1] + ((u * u * u - u) * Mv[i] + (t * t * t - t) * Mv[i + 1]) / 6.0;
-        } else if (n == 4) {
-            const double d1 = y[1] - y[0], d2 = y[2] - 2.0 * y[1] + y[0];
-            const double d3 = y[3] - 3.0 * y[2] + 3.0 * y[1] - y[0];
-            val = y[0] + xq * d1 + xq * (xq - 1.0) * 0.5 * d2 + xq * (xq - 1.0) * (xq - 2.0) / 6.0 * d3;
-        } else {
-            val = y[0] + xq * (y[1] - y[0]) + xq * (xq - 1.0) * 0.5 * (y[2] - 2.0 * y[1] + y[0]);
+            val = u * y[i] + t * y[i + 1] + ((u * u * u - u) * Mv[i] + (t * t * t - t) * Mv[i + 1]) * sixth;
+        } else if (n == 4) {   // the single cubic through 4 points
+            val = y[0] + xq * d1 + xq * (xq - 1.0) * 0.5 * d2 + xq * (xq - 1.0) * (xq - 2.0) * sixth * d3;
+        } else {               // parabola through 3 points
+            val = y[0] + xq * d1 + xq * (xq - 1.0) * 0.5 * d2;
         }
         if (val > best) {
             best = val;
@@ -443,97 +557,163 @@ __device__ double spline_peak(const double* y, int n, int interp) {
     return bx;
 }
 
-__device__ __forceinline__ float cabsf(float2 a) { return sqrtf(a.x * a.x + a.y * a.y); }
+// S9 of one detection from the workgroup's S tile (fsf:237-290).
+__device__ __forceinline__ void s9_estimate(const DevConsts& k, const float* S, int W, int c0, int P, int G, int Gp,
+                                            int v, int r, int pair, const float* __restrict__ MA,
+                                            const float* __restrict__ MB, DevDet* out) {
+    const int c = r - c0;
+    double yr[5], yv[5];
+    int nrc = 0, rfirst = -1;
+    for (int q = -2; q <= 2; ++q) {
+        const int rr = r + q;
+        if (rr >= 0 && rr < G) {
+            if (rfirst < 0) rfirst = rr;
+            yr[nrc++] = (double)S[v * W + c + q];
+        }
+    }
+    int nvc = 0, vfirst = -1;
+    for (int q = -2; q <= 2; ++q) {
+        const int vv = v + q;
+        if (vv >= 0 && vv < P) {
+            if (vfirst < 0) vfirst = vv;
+            yv[nvc++] = (double)S[vv * W + c];
+        }
+    }
+    const double rmax = (nrc < 3) ? (double)r : rfirst + spline_peak(yr, nrc, 8);
+    const double vmax = (nvc < 3) ? (double)v : vfirst + spline_peak(yv, nvc, 4);
+    // amplitude monopulse on the integer cell (fsf:282-290)
+    const double SA = (double)MA[(size_t)v * Gp + r];
+    const double SB = (double)MB[(size_t)v * Gp + r];
+    const double ratio = (SA - SB) / (SA + SB + 2.220446049250313e-16);
+    DevDet d;
+    d.v_idx = v + 1;
+    d.r_idx = r + 1;
+    d.pair_idx = pair + 1;
+    d.reserved = 0;
+    d.amp = (double)S[v * W + c];
+    d.range = k.range_axis[r] + (rmax - r) * k.deltaR;
+    d.velocity = k.velocity_axis[v] + (vmax - v) * k.deltaV;
+    d.angle = 0.5 * (k.beam_angles[pair] + k.beam_angles[pair + 1]) + k.klut[pair] * ratio;
+    *out = d;
+}
+
+#define K3_QCAP 1024
+#define K3_VEC 12   // float4 loads per beam per thread in flight
 
 __global__ __launch_bounds__(RSP_THREADS) void k3_cfar(Geometry g, DevConsts k, FramePtrs fp) {
-    extern __shared__ __attribute__((aligned(16))) float S[];   // [P][W]
+    extern __shared__ __attribute__((aligned(16))) float S[];   // [P][W] | queue[K3_QCAP] | qn, base
     const int f = blockIdx.z, pair = blockIdx.y, tile = blockIdx.x;
     const int P = g.P, G = g.G, W = g.cfar_W, hR = g.cfar_hR;
     const int rR = g.refR, gR = g.guardR, rV = g.refV, gV = g.guardV;
     const int r_begin = rR + gR + tile * g.cfar_RT;
     const int r_end = min(r_begin + g.cfar_RT, G - rR - gR);
     const int c0 = r_begin - hR;
-    const float2* __restrict__ A = fp.rdm[f] + (size_t)pair * P * G;
-    const float2* __restrict__ Bm = A + (size_t)P * G;
-    for (int e = threadIdx.x; e < P * W; e += RSP_THREADS) {
-        const int v = e / W, c = e - v * W;
-        const int r = c0 + c;
-        float val = 0.f;
-        if (r >= 0 && r < G) val = cabsf(A[(size_t)v * G + r]) + cabsf(Bm[(size_t)v * G + r]);
-        S[e] = val;
+    int* queue = reinterpret_cast<int*>(S + P * W);
+    int* qn = queue + K3_QCAP;
+    const int Gp = g.Gp;
+    const float* __restrict__ MA = fp.mag[f] + (size_t)pair * P * Gp;   // |RDM| of beams pair, pair+1
+    const float* __restrict__ MB = MA + (size_t)P * Gp;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;   // 4 waves
+    if (threadIdx.x == 0) qn[0] = 0;
+    // ---- load S = |A| + |B| (fsf:184-187) from the magnitude maps: 16 B per lane,
+    //      K3_VEC float4 of each beam in flight per thread
+    if ((c0 & 3) == 0 && (W & 3) == 0) {
+        const int W4 = W >> 2, n4 = P * W4;
+        for (int e0 = 0; e0 < n4; e0 += K3_VEC * RSP_THREADS) {
+            float4 xa[K3_VEC], xb[K3_VEC];
+#pragma unroll
+            for (int u = 0; u < K3_VEC; ++u) {
+                const int e = e0 + threadIdx.x + u * RSP_THREADS;
+                xa[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                xb[u] = xa[u];
+                if (e < n4) {
+                    const int v = e / W4, r = c0 + 4 * (e - v * W4);
+                    if (r < G) {   // rows are padded to Gp (multiple of 4): r + 3 < Gp
+                        xa[u] = *reinterpret_cast<const float4*>(MA + (size_t)v * Gp + r);
+                        xb[u] = *reinterpret_cast<const float4*>(MB + (size_t)v * Gp + r);
+                        if (r + 1 >= G) { xa[u].y = 0.f; xb[u].y = 0.f; }
+                        if (r + 2 >= G) { xa[u].z = 0.f; xb[u].z = 0.f; }
+                        if (r + 3 >= G) { xa[u].w = 0.f; xb[u].w = 0.f; }
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < K3_VEC; ++u) {
+                const int e = e0 + threadIdx.x + u * RSP_THREADS;
+                if (e < n4)
+                    reinterpret_cast<float4*>(S)[e] =
+                        make_float4(xa[u].x + xb[u].x, xa[u].y + xb[u].y, xa[u].z + xb[u].z, xa[u].w + xb[u].w);
+            }
+        }
+    } else {
+        for (int e = threadIdx.x; e < P * W; e += RSP_THREADS) {
+            const int v = e / W, r = c0 + (e - v * W);
+            S[e] = (r >= 0 && r < G) ? MA[(size_t)v * Gp + r] + MB[(size_t)v * Gp + r] : 0.f;
+        }
     }
     __syncthreads();
     const int v0 = rV + gV, v1 = P - rV - gV;
     const int nr = r_end - r_begin;
     if (v1 <= v0 || nr <= 0) return;
     const float invR = 1.0f / (float)rR, invV = 1.0f / (float)rV;
-    const int ncut = (v1 - v0) * nr;
-    for (int e = threadIdx.x; e < ncut; e += RSP_THREADS) {
-        const int vi = e / nr, ri = e - vi * nr;
-        const int v = v0 + vi, r = r_begin + ri;
+    // ---- cross GOCA-CFAR (fsf:192-213); hits go to an LDS queue so that the S9 work is
+    //      spread over the whole workgroup instead of serialising in the lane that owns a range cell
+    for (int rb = 0; rb < nr; rb += 64) {
+        const int ri = rb + lane;
+        if (ri >= nr) continue;
+        const int r = r_begin + ri;
         const int c = r - c0;
-        const float* rowp = S + v * W;
-        float lr = 0.f, tr = 0.f, lv = 0.f, tv = 0.f;
-        for (int q = 0; q < rR; ++q) {
-            lr += rowp[c - gR - rR + q];
-            tr += rowp[c + gR + 1 + q];
-        }
-        for (int q = 0; q < rV; ++q) {
-            lv += S[(v - gV - rV + q) * W + c];
-            tv += S[(v + gV + 1 + q) * W + c];
-        }
-        const float nR = fmaxf(lr * invR, tr * invR);   // mean() = sum / n
-        const float nV = fmaxf(lv * invV, tv * invV);
-        const float thr = g.T * fmaxf(nR, nV);
-        const float cut = rowp[c];
-        if (cut > thr) {
-            const int idx = atomicAdd(fp.count[f], 1);
-            if (idx < g.max_dets) {
-                // ---- S9 (fsf:237-290)
-                double yr[5], yv[5];
-                int nrc = 0, rfirst = -1;
-                for (int q = -2; q <= 2; ++q) {
-                    const int rr = r + q;
-                    if (rr >= 0 && rr < G) {
-                        if (rfirst < 0) rfirst = rr;
-                        yr[nrc++] = (double)rowp[c + q];
-                    }
+        for (int v = v0 + wv; v < v1; v += 4) {
+            const float* rowp = S + v * W;
+            float lr = 0.f, tr = 0.f, lv = 0.f, tv = 0.f;
+            for (int q = 0; q < rR; ++q) {
+                lr += rowp[c - gR - rR + q];
+                tr += rowp[c + gR + 1 + q];
+            }
+            for (int q = 0; q < rV; ++q) {
+                lv += S[(v - gV - rV + q) * W + c];
+                tv += S[(v + gV + 1 + q) * W + c];
+            }
+            const float nR = fmaxf(lr * invR, tr * invR);   // mean() = sum / n
+            const float nV = fmaxf(lv * invV, tv * invV);
+            const float thr = g.T * fmaxf(nR, nV);
+            if (rowp[c] > thr) {
+                const int qi = atomicAdd(qn, 1);
+                if (qi < K3_QCAP) {
+                    queue[qi] = (v << 16) | c;
+                } else {   // queue overflow (pathological): estimate in place
+                    const int idx = atomicAdd(fp.count[f], 1);
+                    if (idx < g.max_dets) s9_estimate(k, S, W, c0, P, G, Gp, v, r, pair, MA, MB, &fp.dets[f][idx]);
                 }
-                int nvc = 0, vfirst = -1;
-                for (int q = -2; q <= 2; ++q) {
-                    const int vv = v + q;
-                    if (vv >= 0 && vv < P) {
-                        if (vfirst < 0) vfirst = vv;
-                        yv[nvc++] = (double)S[vv * W + c];
-                    }
-                }
-                const double rmax = (nrc < 3) ? (double)r : rfirst + spline_peak(yr, nrc, 8);
-                const double vmax = (nvc < 3) ? (double)v : vfirst + spline_peak(yv, nvc, 4);
-                const double SA = (double)cabsf(A[(size_t)v * G + r]);
-                const double SB = (double)cabsf(Bm[(size_t)v * G + r]);
-                const double ratio = (SA - SB) / (SA + SB + 2.220446049250313e-16);
-                DevDet d;
-                d.v_idx = v + 1;
-                d.r_idx = r + 1;
-                d.pair_idx = pair + 1;
-                d.reserved = 0;
-                d.amp = (double)cut;
-                d.range = k.range_axis[r] + (rmax - r) * k.deltaR;
-                d.velocity = k.velocity_axis[v] + (vmax - v) * k.deltaV;
-                d.angle = 0.5 * (k.beam_angles[pair] + k.beam_angles[pair + 1]) + k.klut[pair] * ratio;
-                fp.dets[f][idx] = d;
             }
         }
+    }
+    __syncthreads();
+    const int n = min(qn[0], K3_QCAP);
+    if (n == 0) return;
+    if (threadIdx.x == 0) qn[1] = atomicAdd(fp.count[f], n);   // one global reservation per workgroup
+    __syncthreads();
+    const int base = qn[1];
+    for (int i = threadIdx.x; i < n; i += RSP_THREADS) {
+        const int idx = base + i;
+        if (idx >= g.max_dets) break;
+        const int e = queue[i];
+        const int v = e >> 16, c = e & 0xFFFF;
+        s9_estimate(k, S, W, c0, P, G, Gp, v, c0 + c, pair, MA, MB, &fp.dets[f][idx]);
     }
 }
 
 // ======================================================================================
 // MTD over pulses of a pulse-compressed cube pc[B][P][G] -> rdm[B][P][G] (fsf:131-136)
 // ======================================================================================
+template <int LGP>
 __global__ __launch_bounds__(RSP_THREADS, 2) void k_mtd_cols(Geometry g, DevConsts k, const float2* __restrict__ pc,
                                                         float2* __restrict__ rdm) {
-    extern __shared__ __attribute__((aligned(16))) float2 Y[];   // [GT][Ppad]
-    const int GT = 16;
+    extern __shared__ __attribute__((aligned(16))) float2 Y[];   // [GT][Ppad] + W_P table
+    constexpr int GT = 16;
+    float2* twl = Y + GT * g.Ppad;
+    if constexpr (LGP > 0)
+        for (int i = threadIdx.x; i < tw_total(LGP); i += RSP_THREADS) twl[i] = k.twPp[i];
     const int b = blockIdx.y, gt0 = blockIdx.x * GT;
     const int P = g.P, G = g.G, Ppad = g.Ppad;
     for (int e = threadIdx.x; e < P * GT; e += RSP_THREADS) {
@@ -549,13 +729,9 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k_mtd_cols(Geometry g, DevCons
     }
     __syncthreads();
     const int half = P >> 1;
-    if (g.pow2P) {
+    if constexpr (LGP > 0) {
         StoreLds st{Y, Ppad, nullptr};
-        int lgNs = 0;
-        for (int q = 0; q < g.nradP; ++q) {
-            run_pass<32, false, false>(g.radP[q], Y, Ppad, g.logP, lgNs, GT, k.twP, st);
-            lgNs += ilog2(g.radP[q]);
-        }
+        fft_passes<LGP, 0, 0, (16 << LGP) / RSP_THREADS, false, 0, RSP_THREADS>(Y, Ppad, GT, twl, st, st);
         for (int e = threadIdx.x; e < P * GT; e += RSP_THREADS) {
             const int v = e / GT, gl = e - v * GT;
             const int gg = gt0 + gl;
@@ -650,27 +826,36 @@ static hipError_t allow_lds(K kernel, size_t bytes) {
                                (int)bytes);
 }
 
+template <int BMAX, int CP>
+static hipError_t launch_k1_t(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int mode,
+                              hipStream_t s) {
+    const size_t lds = ((size_t)g.B * g.NT * g.Ppad + ((g.P + 1) & ~1) + CP * BMAX) * sizeof(float2);
+    hipError_t e = allow_lds(k1_dbf_mtd<BMAX, CP>, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k1_dbf_mtd<BMAX, CP>), dim3(g.ntiles, nf), dim3(K1_THREADS), lds, s, g, k, fp, mode);
+    return hipGetLastError();
+}
+
+template <int BMAX>
+static hipError_t launch_k1_b(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int mode,
+                              int ch, hipStream_t s) {
+    if (ch <= 8) return launch_k1_t<BMAX, 8>(g, k, fp, nf, mode, s);
+    if (ch <= 16) return launch_k1_t<BMAX, 16>(g, k, fp, nf, mode, s);
+    return launch_k1_t<BMAX, 32>(g, k, fp, nf, mode, s);
+}
+
 hipError_t launch_k1(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int mode, int,
                      hipStream_t s) {
-    const size_t lds = (size_t)g.B * g.NT * g.Ppad * sizeof(float2);
-    dim3 grid(g.ntiles, nf), blk(RSP_THREADS);
-    hipError_t e;
-    if (g.B <= 4) {
-        if ((e = allow_lds(k1_dbf_mtd<4>, lds)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k1_dbf_mtd<4>, grid, blk, lds, s, g, k, fp, mode);
-    } else if (g.B <= 8) {
-        if ((e = allow_lds(k1_dbf_mtd<8>, lds)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k1_dbf_mtd<8>, grid, blk, lds, s, g, k, fp, mode);
-    } else {
-        if ((e = allow_lds(k1_dbf_mtd<16>, lds)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k1_dbf_mtd<16>, grid, blk, lds, s, g, k, fp, mode);
-    }
-    return hipGetLastError();
+    if (g.B <= 4) return launch_k1_b<4>(g, k, fp, nf, mode, g.C, s);
+    if (g.B <= 8) return launch_k1_b<8>(g, k, fp, nf, mode, g.C, s);
+    return launch_k1_b<16>(g, k, fp, nf, mode, g.C, s);
 }
 
 hipError_t launch_k2(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int rows,
                      hipStream_t s) {
-    const size_t lds = (size_t)(RSP_K2_POINTS + RSP_K2_POINTS / 16) * sizeof(float2);
+    const size_t lds = (size_t)(K2_LDS_DATA + 2 * K2_MAXM) * sizeof(float2);
+    hipError_t e = allow_lds(k2_pc, lds);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k2_pc, dim3(g.nwg_k2, nf), dim3(RSP_THREADS), lds, s, g, k, fp, rows);
     return hipGetLastError();
 }
@@ -679,19 +864,32 @@ hipError_t launch_k3(const Geometry& g, const DevConsts& k, const FramePtrs& fp,
     const int ncut_r = g.G - 2 * (g.refR + g.guardR);
     if (g.B < 2 || ncut_r <= 0) return hipSuccess;
     const int tiles = (ncut_r + g.cfar_RT - 1) / g.cfar_RT;
-    const size_t lds = (size_t)g.P * g.cfar_W * sizeof(float);
+    const size_t lds = (size_t)g.P * g.cfar_W * sizeof(float) + (K3_QCAP + 4) * sizeof(int);
     hipError_t e = allow_lds(k3_cfar, lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k3_cfar, dim3(tiles, g.B - 1, nf), dim3(RSP_THREADS), lds, s, g, k, fp);
     return hipGetLastError();
 }
 
-hipError_t launch_mtd_cols(const Geometry& g, const DevConsts& k, const float2* pc, float2* rdm, hipStream_t s) {
-    const size_t lds = (size_t)16 * g.Ppad * sizeof(float2);
-    hipError_t e = allow_lds(k_mtd_cols, lds);
+template <int LGP>
+static hipError_t launch_mtd_t(const Geometry& g, const DevConsts& k, const float2* pc, float2* rdm, hipStream_t s) {
+    const size_t lds = ((size_t)16 * g.Ppad + g.P) * sizeof(float2);
+    hipError_t e = allow_lds(k_mtd_cols<LGP>, lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_mtd_cols, dim3((g.G + 15) / 16, g.B), dim3(RSP_THREADS), lds, s, g, k, pc, rdm);
+    hipLaunchKernelGGL(k_mtd_cols<LGP>, dim3((g.G + 15) / 16, g.B), dim3(RSP_THREADS), lds, s, g, k, pc, rdm);
     return hipGetLastError();
+}
+
+hipError_t launch_mtd_cols(const Geometry& g, const DevConsts& k, const float2* pc, float2* rdm, hipStream_t s) {
+    switch (g.pow2P ? g.logP : 0) {
+        case 4: return launch_mtd_t<4>(g, k, pc, rdm, s);
+        case 5: return launch_mtd_t<5>(g, k, pc, rdm, s);
+        case 6: return launch_mtd_t<6>(g, k, pc, rdm, s);
+        case 7: return launch_mtd_t<7>(g, k, pc, rdm, s);
+        case 8: return launch_mtd_t<8>(g, k, pc, rdm, s);
+        case 9: return launch_mtd_t<9>(g, k, pc, rdm, s);
+        default: return launch_mtd_t<0>(g, k, pc, rdm, s);
+    }
 }
 
 hipError_t launch_synth(const Geometry& g, const double* tx, const SynthTarget* tg, int nt, int frame_idx,

@@ -72,6 +72,36 @@ void fft_d(std::vector<cd>& a, int sign) {
     }
 }
 
+// Radix sequence for a 2^m-point Stockham FFT: radix 16 passes, remainder as 8/4
+// (never a lone radix-2 pass unless m == 1).
+void radix_plan(int m, int* nrad, int* rad) {
+    *nrad = 0;
+    while (m > 0) {
+        const int p = (m == 5) ? 3 : (m >= 4 ? 4 : m);
+        rad[(*nrad)++] = 1 << p;
+        m -= p;
+    }
+}
+
+// Per-pass Stockham twiddle tables of a 2^m-point FFT, concatenated: pass q >= 1 owns
+// Ns_q x (R_q - 1) entries T[k][r-1] = exp(-2 pi i k r / (Ns_q R_q)) (must match
+// tw_pass_off() in rsp_kernels.hip).
+void build_pass_twiddles(int m, std::vector<float2>& out) {
+    int nrad, rad[8];
+    radix_plan(m, &nrad, rad);
+    int Ns = 1;
+    for (int q = 0; q < nrad; ++q) {
+        const int R = rad[q];
+        if (q > 0)
+            for (int k = 0; k < Ns; ++k)
+                for (int r = 1; r < R; ++r) {
+                    const double a = -2.0 * M_PI * (double)k * r / ((double)Ns * R);
+                    out.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
+                }
+        Ns *= R;
+    }
+}
+
 double mround(double x) { return x < 0 ? -std::floor(-x + 0.5) : std::floor(x + 0.5); }
 
 struct Lane {
@@ -79,6 +109,7 @@ struct Lane {
     hipEvent_t done = nullptr;
     float2* z = nullptr;        // F frames
     float2* rdm = nullptr;      // F frames
+    float* mag = nullptr;       // F frames
     DevDet* dets = nullptr;     // F x max_dets
     int* count = nullptr;       // F
     DevDet* h_dets = nullptr;   // pinned F x async_cap
@@ -106,7 +137,7 @@ struct rsp_plan {
     double p_signal_unscaled = 0, c = 0, fs = 0, wavelength = 0, d = 0, prt = 0;
     int F = 1;
     int async_cap = 2048;
-    size_t z_elems = 0, rdm_elems = 0;
+    size_t z_elems = 0, rdm_elems = 0, mag_elems = 0;
     std::vector<SegDesc> segs;
     std::vector<K2Job> jobs;
     std::vector<void*> dev_allocs;
@@ -259,9 +290,7 @@ int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga,
     const int M = bestM;
     s.M = M; s.logM = ilog2i(M); s.V = M - Lh + 1; s.nblocks = (nout + s.V - 1) / s.V;
     s.rows_per_wg = RSP_K2_POINTS / M;
-    int m = s.logM; s.nrad = 0;
-    while (m >= 4) { s.rad[s.nrad++] = 16; m -= 4; }
-    if (m > 0) s.rad[s.nrad++] = 1 << m;
+    radix_plan(s.logM, &s.nrad, s.rad);
     // spectrum of h zero-padded to M, natural order, 1/M folded in
     std::vector<cd> hm(M, 0.0);
     for (int i = 0; i < Lh; ++i) hm[i] = h[i];
@@ -273,10 +302,7 @@ int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga,
     if (ti < 0) {
         tw_sizes.push_back(M);
         tw_offs.push_back((int)twM.size());
-        for (int i = 0; i < M; ++i) {
-            const double a = -2.0 * M_PI * i / M;
-            twM.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
-        }
+        build_pass_twiddles(s.logM, twM);
         ti = (int)tw_sizes.size() - 1;
     }
     s.tw_off = tw_offs[ti];
@@ -289,6 +315,7 @@ int setup_lane(rsp_plan* p, Lane& L) {
     int rc;
     if ((rc = p->dalloc(&L.z, p->z_elems * p->F))) return rc;
     if ((rc = p->dalloc(&L.rdm, p->rdm_elems * p->F))) return rc;
+    if ((rc = p->dalloc(&L.mag, p->mag_elems * p->F))) return rc;
     if ((rc = p->dalloc(&L.dets, (size_t)p->g.max_dets * p->F))) return rc;
     if ((rc = p->dalloc(&L.count, (size_t)p->F))) return rc;
     HIPCHK(hipHostMalloc((void**)&L.h_dets, sizeof(DevDet) * p->async_cap * p->F, hipHostMallocDefault));
@@ -302,6 +329,7 @@ FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const float2* const* in, i
         fp.in[f] = in[f];
         fp.z[f] = L.z + p->z_elems * f;
         fp.rdm[f] = L.rdm + p->rdm_elems * f;
+        fp.mag[f] = L.mag + p->mag_elems * f;
         fp.dets[f] = L.dets + (size_t)p->g.max_dets * f;
         fp.count[f] = L.count + f;
     }
@@ -474,7 +502,8 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     *out = nullptr;
     const int C = cfg->channel_num, B = cfg->beam_num, P = cfg->prtNum, N = cfg->point_PRT;
     const int g1 = pre->N_gate_narrow, g2 = pre->N_gate_medium, g3 = pre->N_gate_long, G = pre->N_total_gate;
-    if (C < 1 || B < 1 || B > 16 || P < 2 || N < 2) return fail(RSP_ERR_INVALID, "bad sizes C=%d B=%d P=%d N=%d (1<=B<=16)", C, B, P, N);
+    if (C < 1 || C > 32 || B < 1 || B > 16 || P < 2 || N < 2)
+        return fail(RSP_ERR_INVALID, "bad sizes C=%d B=%d P=%d N=%d (1<=C<=32, 1<=B<=16)", C, B, P, N);
     if (P % 2) return fail(RSP_ERR_UNSUPPORTED, "odd prtNum %d (pulse pairs are loaded as 16 B)", P);
     if (g1 < 0 || g2 < 0 || g3 < 0 || G != g1 + g2 + g3 || G < 1) return fail(RSP_ERR_INVALID, "gate counts inconsistent");
     if (!pre->DBF_coeffs_data_C || !pre->MF_narrow || !pre->MF_medium_fft || !pre->MF_long_fft || !pre->MTD_win ||
@@ -567,8 +596,8 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
         s.off = (int)(std::lower_bound(nof.begin(), nof.end(), s.lo) - nof.begin());
     }
     // K1 tile: NT samples per [P][NT] slab; keep LDS <= 80 KB (2 workgroups per CU)
-    g.pow2P = is_pow2(P);
-    g.Ppad = P + 4;
+    g.pow2P = is_pow2(P) && P >= 16 && P <= 512;   // Stockham range of k1_fft; else direct DFT
+    g.Ppad = g.pow2P ? P + P / 16 : P + 4;   // pow2: + one pad per 16 (K1_SH), see rsp_kernels.hip
     g.NT = 8;
     while (g.NT > 1 && ((size_t)B * g.NT * g.Ppad * sizeof(float2) > 80 * 1024 || (g.pow2P && B * g.NT * P > 8192)))
         g.NT >>= 1;
@@ -578,9 +607,7 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     nof.resize((size_t)g.ntiles * g.NT, -1);
     if (g.pow2P) {
         g.logP = ilog2i(P);
-        int m = g.logP; g.nradP = 0;
-        while (m >= 4) { g.radP[g.nradP++] = 16; m -= 4; }
-        if (m > 0) g.radP[g.nradP++] = 1 << m;
+        radix_plan(g.logP, &g.nradP, g.radP);
     }
     if (16 * (size_t)g.Ppad * sizeof(float2) > 160 * 1024 || (g.pow2P && 16 * P > 8192))
         return bail(fail(RSP_ERR_UNSUPPORTED, "prtNum %d too large", P));
@@ -603,17 +630,24 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     g.cfar_hR = std::max(g.refR + g.guardR, 2);
     g.cfar_RT = 64;
     while (g.cfar_RT > 8 && (size_t)P * (g.cfar_RT + 2 * g.cfar_hR) * 4 > 96 * 1024) g.cfar_RT >>= 1;
-    g.cfar_W = g.cfar_RT + 2 * g.cfar_hR;
+    g.cfar_W = (g.cfar_RT + 2 * g.cfar_hR + 3) & ~3;   // LDS row stride, float4 aligned
     if ((size_t)P * g.cfar_W * 4 > 160 * 1024) return bail(fail(RSP_ERR_UNSUPPORTED, "CFAR tile exceeds LDS"));
 
     // ---- constants to the device
     int rc;
-    std::vector<float2> Wc((size_t)B * C), twP(P);
+    // conj(W) laid out [C][BMAX] (BMAX = the K1 instantiation's beam count, zero padded) so
+    // that one channel's beam weights are one contiguous scalar load in k1_dbf_mtd
+    const int bmax = B <= 4 ? 4 : (B <= 8 ? 8 : 16);
+    const int cpad = C <= 8 ? 8 : (C <= 16 ? 16 : 32);   // CP of k1_dbf_mtd<BMAX, CP>
+    std::vector<float2> Wc((size_t)bmax * cpad, make_float2(0.f, 0.f)), twP(P), twPp;
     for (int b = 0; b < B; ++b)
         for (int c = 0; c < C; ++c) {   // column-major B x C; y = x * W' uses conj(W)  (fsf:95)
             const size_t i = (size_t)b + (size_t)B * c;
-            Wc[(size_t)b * C + c] = make_float2((float)pre->DBF_coeffs_data_C[2 * i], -(float)pre->DBF_coeffs_data_C[2 * i + 1]);
+            Wc[(size_t)c * bmax + b] = make_float2((float)pre->DBF_coeffs_data_C[2 * i], -(float)pre->DBF_coeffs_data_C[2 * i + 1]);
         }
+    if (g.pow2P) build_pass_twiddles(g.logP, twPp);
+    g.wc_elems = (int)Wc.size();
+    g.twPp_elems = (int)twPp.size();
     for (int i = 0; i < P; ++i) {
         const double a = -2.0 * M_PI * i / P;
         twP[i] = make_float2((float)std::cos(a), (float)std::sin(a));
@@ -623,15 +657,15 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     std::vector<double> ang(pre->beam_angles_deg, pre->beam_angles_deg + B);
     std::vector<double> kl(std::max(B - 1, 1), 0.0);
     for (int i = 0; i + 1 < B; ++i) kl[i] = pre->k_slopes_LUT[i];
-    float2 *dWc, *dtwP, *dH, *dtwM; float *dwin, *dtaps; int* dnof; SegDesc* dsegs; K2Job* djobs;
+    float2 *dWc, *dtwP, *dtwPp, *dH, *dtwM; float *dwin, *dtaps; int* dnof; SegDesc* dsegs; K2Job* djobs;
     double *dra, *dva, *dang, *dkl;
-    if ((rc = p->upload(&dWc, Wc)) || (rc = p->upload(&dtwP, twP)) || (rc = p->upload(&dwin, win)) ||
+    if ((rc = p->upload(&dWc, Wc)) || (rc = p->upload(&dtwP, twP)) || (rc = p->upload(&dtwPp, twPp)) || (rc = p->upload(&dwin, win)) ||
         (rc = p->upload(&dnof, nof)) || (rc = p->upload(&dsegs, p->segs)) || (rc = p->upload(&djobs, p->jobs)) ||
         (rc = p->upload(&dtaps, taps)) || (rc = p->upload(&dH, H)) || (rc = p->upload(&dtwM, twM)) ||
         (rc = p->upload(&dra, ra)) || (rc = p->upload(&dva, va)) || (rc = p->upload(&dang, ang)) ||
         (rc = p->upload(&dkl, kl)))
         return bail(rc);
-    p->k = DevConsts{dWc, dwin, dtwP, dnof, dsegs, djobs, dtaps, dH, dtwM, dra, dva, dang, dkl, pre->deltaR, pre->deltaV};
+    p->k = DevConsts{dWc, dwin, dtwP, dtwPp, dnof, dsegs, djobs, dtaps, dH, dtwM, dra, dva, dang, dkl, pre->deltaR, pre->deltaV};
     if (pre->tx_pulse) {
         std::vector<double> tx(pre->tx_pulse, pre->tx_pulse + 2 * (size_t)N);
         if ((rc = p->upload(&p->d_tx, tx))) return bail(rc);
@@ -639,6 +673,8 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     if ((rc = p->dalloc(&p->d_tg, 64))) return bail(rc);
     p->z_elems = (size_t)B * g.ntiles * g.NT * P;
     p->rdm_elems = (size_t)B * P * G;
+    g.Gp = (G + 3) & ~3;
+    p->mag_elems = (size_t)B * P * g.Gp;
     if ((rc = p->dalloc(&p->d_cube, (size_t)std::max(C, B) * N * P))) return bail(rc);
     for (auto& L : p->lanes)
         if ((rc = setup_lane(p, L))) return bail(rc);
