@@ -148,7 +148,8 @@ def main():
     cells = sz.B * sz.G * sz.P
     out = None
     if rank == 0:
-        prof = plan.profile_stages(ring[0], iters=a.profile_iters)
+        # per-stage HIP-event timing of batched launches (frames_per_launch distinct ring cubes)
+        prof = plan.profile_stages(ring[:a.fpl], iters=a.profile_iters)
         dom = max(prof, key=lambda s: s['ms'])
         achieved = dom['bytes'] / (dom['ms'] * 1e-3) / 1e9
         traffic = None
@@ -171,6 +172,7 @@ def main():
             'roofline': {'bound': 'hbm', 'kernel': dom['stage'], 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
                          'kernel_ms': dom['ms'], 'alg_bytes_per_launch': dom['bytes'],
+                         'frames_per_launch': dom['frames'],
                          'stages': prof},
         }
         if world == 1 and not a.no_cpu_baseline:

@@ -195,13 +195,19 @@ int32_t rsp_process_stage2(rsp_plan* plan, const void* iq_beams, int32_t dtype,
                            double* mtd_out, double* pc_out);
 
 /* ---- measurement ----
- * Time each device stage `iters` times on the plan's stream with HIP events over a
- * device-resident complex64 cube; ms_out[i] = average ms per launch of stage i
- * (one frame per launch).  bytes_out[i] = algorithmic HBM bytes per launch.
+ * Time each device stage `iters` times on the plan's stream with HIP events.  Each launch
+ * batches nf = min(n_cubes, frames_per_launch) frames taken from the device-resident
+ * complex64 cubes d_cubes[0..nf-1].  ms_out[i] = average ms per launch of stage i,
+ * bytes_out[i] = algorithmic HBM bytes per launch (nf frames), *frames_out = nf.
  * Stage names via rsp_stage_name. */
-int32_t rsp_profile_stages(rsp_plan* plan, const void* d_cube, int32_t iters, float* ms_out,
-                           int64_t* bytes_out, int32_t cap);
+int32_t rsp_profile_stages(rsp_plan* plan, const void* const* d_cubes, int32_t n_cubes, int32_t iters,
+                           float* ms_out, int64_t* bytes_out, int32_t cap, int32_t* frames_out);
 const char* rsp_stage_name(int32_t stage);
+
+/* Host-only S10 + S11 (fun_cluster_stage1_10 / fun_cluster_stage2_11, fsf:302-407) on a
+ * detection list (any order; sorted into the reference's find() order first).  No GPU. */
+int32_t rsp_cluster_detections(const rsp_detection* dets, int32_t n, const rsp_cluster_params* cluster,
+                               rsp_target* out, int32_t cap, int32_t* n_out);
 
 /* Device memory helpers (so hosts without a GPU runtime binding can stage cubes). */
 int32_t rsp_device_alloc(rsp_plan* plan, int64_t bytes, void** d_ptr);

@@ -35,6 +35,10 @@ struct K2Job {
     int seg, blk, wg_begin, wg_count;
 };
 
+#define RSP_MAX_SEG 3
+#define RSP_MAX_JOBS 16
+#define RSP_MAX_IVL 4
+
 struct Geometry {
     int C, B, P, N, G;
     int Gp;          // row stride of the magnitude maps (G rounded up to 4 floats)
@@ -47,6 +51,14 @@ struct Geometry {
     int refR, guardR, refV, guardV;
     float T;
     int max_dets;
+    int dbg;         // RSP_ABLATE bit mask: timing-only ablations (outputs invalid when set)
+    // used fast-time samples as <= RSP_MAX_IVL intervals: compacted n' in [ivl_start[q],
+    // ivl_start[q+1]) is sample ivl_lo[q] + n' - ivl_start[q] (kernel-argument lookup, no
+    // dependent global load before the cube loads)
+    int nivl, ivl_lo[RSP_MAX_IVL], ivl_start[RSP_MAX_IVL];
+    // pulse-compression segment and job tables travel as kernel arguments too
+    SegDesc segs[RSP_MAX_SEG];
+    K2Job jobs[RSP_MAX_JOBS];
 };
 
 struct FramePtrs {
@@ -54,12 +66,14 @@ struct FramePtrs {
     float2* z[RSP_MAX_F];          // compacted Doppler-domain rows
     float2* rdm[RSP_MAX_F];        // [B][P][G]
     float* mag[RSP_MAX_F];         // |rdm| [B][P][Gp] (K2 epilogue, read by K3)
+    unsigned long long* trace;     // diagnostic: 4 s_memrealtime stamps per workgroup, or null
     DevDet* dets[RSP_MAX_F];
     int* count[RSP_MAX_F];
 };
 
 struct DevConsts {
-    const float2* Wc;        // conj(W) [B][C]
+    const float2* Wc;        // conj(W) [CP][BMAX]
+    const float* Atab;       // DBF MFMA A operands per lane: [MB][CP/4][Re,Im][64] (build_dbf_atab)
     const float* win;        // MTD window [P]
     const float2* twP;       // W_P^i table (direct DFT path)
     const float2* twPp;      // per-pass Stockham twiddles of the P-point FFT

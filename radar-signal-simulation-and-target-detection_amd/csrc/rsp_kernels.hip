@@ -107,14 +107,21 @@ template <> struct Log2R<16> { static constexpr int v = 4; };
 template <int SH>
 __device__ __forceinline__ int lidx(int i) { return SH ? i + (i >> SH) : i; }
 
-// Store policies for the Stockham pass output.
+// Store policies for the Stockham pass output.  put(idx, row, o, loff, x): idx = t * R + r for
+// butterfly t / element r of this thread (a constant after unrolling), row, natural position
+// o, and the padded LDS offset loff of (row, o).
 struct StoreLds {
-    float2* buf; int rs; const float2* H;   // optional pointwise multiply (natural order)
-    template <int SH>
-    __device__ __forceinline__ void put(int row, int o, float2 x) const {
-        if (H) x = cmul(x, H[o]);
-        buf[row * rs + lidx<SH>(o)] = x;
-    }
+    float2* buf;
+    __device__ __forceinline__ void put(int, int, int, int loff, float2 x) const { buf[loff] = x; }
+};
+
+// Last forward pass of the overlap-save FFT: multiply by the block filter spectrum H (1/M
+// folded in), prefetched into registers at kernel start (h[t * R + r] for this thread's outputs).
+template <int NH>
+struct StoreLdsH {
+    float2* buf;
+    const float2 (&h)[NH];
+    __device__ __forceinline__ void put(int idx, int, int, int loff, float2 x) const { buf[loff] = cmul(x, h[idx]); }
 };
 
 // One Stockham radix-R pass (Govindaraju et al. formulation) over `nrows` rows of
@@ -132,6 +139,9 @@ __device__ __forceinline__ void sh_pass(float2* buf, int rs, int nrows, const fl
     constexpr int Ns = 1 << LGNS;
     const int total = nb * nrows;
     const int tid = threadIdx.x;
+    // With power-of-two nb, Ns and pads every 2^SH, lidx(j + r nb) = lidx(j) + r nb + ((r nb) >> SH)
+    // and lidx(idxD + r Ns) = lidx(idxD) + r Ns + ((r Ns) >> SH): every LDS address of a butterfly
+    // is a per-thread base plus a compile-time offset (ds_read/ds_write immediate offsets).
     float2 v[NB][R];
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
@@ -139,12 +149,13 @@ __device__ __forceinline__ void sh_pass(float2* buf, int rs, int nrows, const fl
         if (beta < total) {
             const int row = beta >> lgnb, j = beta & (nb - 1);
             const int k = j & (Ns - 1);
-            const float2* src = buf + row * rs;
+            const float2* src = buf + row * rs + lidx<SH>(j);
+            const float2* twk = tw + k * (R - 1) - 1;   // per-pass table [k][r-1]
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                float2 x = src[lidx<SH>(j + r * nb)];
+                float2 x = src[r * nb + (SH ? (r * nb) >> SH : 0)];
                 if (r > 0 && LGNS > 0) {
-                    float2 w = tw[k * (R - 1) + r - 1];   // per-pass table [k][r-1]: consecutive k -> stride R-1
+                    float2 w = twk[r];
                     if (INV) w.y = -w.y;
                     x = cmul(x, w);
                 }
@@ -161,8 +172,10 @@ __device__ __forceinline__ void sh_pass(float2* buf, int rs, int nrows, const fl
             const int k = j & (Ns - 1);
             Dft<R, INV>::run(v[t]);
             const int idxD = ((j >> LGNS) << (LGNS + lgR)) + k;
+            const int wbase = row * rs + lidx<SH>(idxD);
 #pragma unroll
-            for (int r = 0; r < R; ++r) st.template put<SH>(row, idxD + r * Ns, v[t][r]);
+            for (int r = 0; r < R; ++r)
+                st.put(t * R + r, row, idxD + r * Ns, wbase + r * Ns + (SH ? (r * Ns) >> SH : 0), v[t][r]);
         }
     }
     __syncthreads();
@@ -217,6 +230,17 @@ __device__ __forceinline__ void fft_passes(float2* buf, int rs, int nrows, const
 
 __device__ __forceinline__ int ilog2(int x) { return 31 - __clz(x); }
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Diagnostic phase stamps (only when FramePtrs::trace is set: rsp_profile_stages with
+// RSP_TRACE_FILE).  Stamp i of the linear workgroup id; 100 MHz constant clock.
+__device__ __forceinline__ void trace_stamp(const FramePtrs& fp, int i) {
+    if (fp.trace && threadIdx.x == 0) {
+        const size_t wg = blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z);
+        fp.trace[wg * 4 + i] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
 // z (compacted Doppler-domain rows) addressing: row (b, v), compacted sample n'.
 __device__ __forceinline__ size_t zaddr(const Geometry& g, int b, int v, int np) {
     const int lgNT = ilog2(g.NT);
@@ -231,7 +255,7 @@ __device__ __forceinline__ size_t zaddr(const Geometry& g, int b, int v, int np)
 
 // Slow-time FFT of every (beam, sample) column in LDS for the runtime log2(P).
 __device__ __forceinline__ void k1_fft(int lgp, float2* Y, int Ppad, int ncols, const float2* twl) {
-    StoreLds st{Y, Ppad, nullptr};
+    StoreLds st{Y};
     switch (lgp) {
         case 4: fft_passes<4, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, st); break;
         case 5: fft_passes<5, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, st); break;
@@ -251,64 +275,140 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
     extern __shared__ __attribute__((aligned(16))) float2 Y[];   // [B][NT][Ppad] | twiddles | W
     const int f = blockIdx.y, tile = blockIdx.x;
     const int B = g.B, C = g.C, P = g.P, NT = g.NT, Ppad = g.Ppad;
+    trace_stamp(fp, 0);
     float2* twl = Y + B * NT * Ppad;
-    float2* Wl = twl + ((g.P + 1) & ~1);   // 16-B aligned
     const bool fft = (mode & 2) && g.pow2P;
     const int sh = fft ? K1_SH : 0;
     if (fft)
         for (int i = threadIdx.x; i < g.twPp_elems; i += K1_THREADS) twl[i] = k.twPp[i];
-    if (mode & 1)
-        for (int i = threadIdx.x; i < CP * BMAX; i += K1_THREADS) Wl[i] = k.Wc[i];
     __syncthreads();
     const float2* __restrict__ x = fp.in[f];
     const size_t NP = (size_t)g.N * P;   // channel stride
-    const int items = NT * P;
-    // ---- Phase A: DBF (fsf:93-97) + MTD window (fsf:134), one pulse per thread item
-    for (int it = threadIdx.x; it < items; it += K1_THREADS) {
-        const int nl = it / P, p = it - nl * P;
-        const int n = k.nof[tile * NT + nl];
-        float2 acc[BMAX];
+    if (mode & 1) {
+        // ---- Phase A (MFMA): DBF (fsf:93-97) + MTD window (fsf:134) as a real GEMM on the
+        // f32 matrix cores: D[16 x 16 pulses] += A[16 x 4 channels] * B[4 channels x 16 pulses],
+        // rows = (Re, Im) x 8 beams, one MFMA per (channel group, Re/Im part, even/odd pulses).
+        // Each lane loads 16 B = pulses (p, p+1) of one channel: B operand of two column blocks.
+        constexpr int NJ = CP / 4, MB = BMAX <= 8 ? 1 : 2, TPW = (16 / NJ) / MB > 0 ? (16 / NJ) / MB : 1;
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, grp = lane >> 4, col = lane & 15;
+        float are[MB][NJ], aim[MB][NJ];   // this lane's A operand: row lane&15, channel 4j + lane>>4
 #pragma unroll
-        for (int b = 0; b < BMAX; ++b) acc[b] = make_float2(0.f, 0.f);
-        if (n >= 0) {
-            const float2* __restrict__ src = x + (size_t)n * P + p;
-            if (mode & 1) {
-                float2 xv[CP];
+        for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
-                for (int u = 0; u < CP; ++u) xv[u] = src[(size_t)min(u, C - 1) * NP];   // padded: weight 0
-#pragma unroll
-                for (int u = 0; u < CP; ++u) {
-                    const float4* wrow = reinterpret_cast<const float4*>(Wl + u * BMAX);
-#pragma unroll
-                    for (int b2 = 0; b2 < BMAX / 2; ++b2) {
-                        const float4 w2 = wrow[b2];
-                        acc[2 * b2].x += xv[u].x * w2.x - xv[u].y * w2.y;
-                        acc[2 * b2].y += xv[u].x * w2.y + xv[u].y * w2.x;
-                        acc[2 * b2 + 1].x += xv[u].x * w2.z - xv[u].y * w2.w;
-                        acc[2 * b2 + 1].y += xv[u].x * w2.w + xv[u].y * w2.z;
-                    }
-                    __builtin_amdgcn_sched_barrier(0);   // weight reads stay next to their FMAs
-                }
-            } else {
-#pragma unroll
-                for (int b = 0; b < BMAX; ++b)
-                    if (b < B) acc[b] = src[(size_t)b * NP];
+            for (int j = 0; j < NJ; ++j) {
+                are[mb][j] = k.Atab[((mb * NJ + j) * 2 + 0) * 64 + lane];
+                aim[mb][j] = k.Atab[((mb * NJ + j) * 2 + 1) * 64 + lane];
             }
-            if (mode & 2) {
-                const float w = k.win[p];
+        const int ptiles = (P + 31) >> 5;
+        const int ntp = NT * ptiles;
+        float* Yf = reinterpret_cast<float*>(Y);
+        // a wave takes TPW consecutive tiles (pulse tiles of the same sample first), so the
+        // 1 KB pulse row of each (channel, sample) is fetched by one wave in one burst
+        for (int t0 = wv * TPW; t0 < ntp; t0 += (K1_THREADS / 64) * TPW) {
+            float4 xv[TPW][NJ];
+            int nlv[TPW], pv[TPW];
 #pragma unroll
-                for (int b = 0; b < BMAX; ++b) {
-                    acc[b].x *= w;
-                    acc[b].y *= w;
+            for (int u = 0; u < TPW; ++u) {      // every load of TPW tiles in flight together
+                const int t = t0 + u;
+                const int nl = t / ptiles;
+                const int p = ((t - nl * ptiles) << 5) + 2 * col;
+                const int np = tile * NT + nl;
+                int n = -1;
+                if (t < ntp && np < g.nU && p < P) {
+                    int q = 0;
+#pragma unroll
+                    for (int i = 1; i < RSP_MAX_IVL; ++i)
+                        if (i < g.nivl && np >= g.ivl_start[i]) q = i;
+                    n = g.ivl_lo[q] + np - g.ivl_start[q];
+                }
+                nlv[u] = t < ntp ? nl : -1;
+                pv[u] = p;
+                if (g.dbg & 32) {   // ablation: same bytes, 1 KB-contiguous wave loads (timing only)
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) {
+                        const int c = min(4 * j + (u & 3), C - 1);
+                        const int pp = (2 * lane) % P;
+                        xv[u][j] = n >= 0 ? *reinterpret_cast<const float4*>(x + (size_t)c * NP + (size_t)n * P + pp)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) {
+                        const int c = min(4 * j + grp, C - 1);   // padded channels carry zero weights
+                        xv[u][j] = n >= 0 ? *reinterpret_cast<const float4*>(x + (size_t)c * NP + (size_t)n * P + p)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < TPW; ++u) {
+                if (nlv[u] < 0) continue;
+                f32x4 acc[MB][2];
+#pragma unroll
+                for (int mb = 0; mb < MB; ++mb) {
+                    acc[mb][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    acc[mb][1] = acc[mb][0];
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) {
+                        acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(are[mb][j], xv[u][j].x, acc[mb][0], 0, 0, 0);
+                        acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(aim[mb][j], xv[u][j].y, acc[mb][0], 0, 0, 0);
+                        acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(are[mb][j], xv[u][j].z, acc[mb][1], 0, 0, 0);
+                        acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(aim[mb][j], xv[u][j].w, acc[mb][1], 0, 0, 0);
+                    }
+                }
+                const int p = pv[u];
+                if (p >= P) continue;
+                float w0 = 1.f, w1 = 1.f;
+                if (mode & 2) {
+                    const float2 w01 = *reinterpret_cast<const float2*>(k.win + p);
+                    w0 = w01.x;
+                    w1 = w01.y;
+                }
+                const int i0 = sh ? p + (p >> K1_SH) : p, i1 = sh ? (p + 1) + ((p + 1) >> K1_SH) : p + 1;
+#pragma unroll
+                for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {   // D row m = 4*grp + i: beam mb*8 + (m & 7), part m >> 3
+                        const int m = 4 * grp + i;
+                        const int b = mb * 8 + (m & 7);
+                        if (b < B) {
+                            float* colp = Yf + 2 * (b * NT + nlv[u]) * Ppad + (m >> 3);
+                            colp[2 * i0] = acc[mb][0][i] * w0;
+                            colp[2 * i1] = acc[mb][1][i] * w1;
+                        }
+                    }
+            }
+        }
+    } else {
+        // ---- transpose only (stage-2 path: input channels are the beams)
+        const int items = NT * P;
+        for (int it = threadIdx.x; it < items; it += K1_THREADS) {
+            const int nl = it / P, p = it - nl * P;
+            const int np = tile * NT + nl;
+            int n = -1;
+            if (np < g.nU) {
+                int q = 0;
+#pragma unroll
+                for (int i = 1; i < RSP_MAX_IVL; ++i)
+                    if (i < g.nivl && np >= g.ivl_start[i]) q = i;
+                n = g.ivl_lo[q] + np - g.ivl_start[q];
+            }
+            const int ip = sh ? p + (p >> K1_SH) : p;
+#pragma unroll
+            for (int b = 0; b < BMAX; ++b) {
+                if (b < B) {
+                    float2 val = n >= 0 ? x[(size_t)b * NP + (size_t)n * P + p] : make_float2(0.f, 0.f);
+                    if (mode & 2) {
+                        val.x *= k.win[p];
+                        val.y *= k.win[p];
+                    }
+                    Y[(b * NT + nl) * Ppad + ip] = val;
                 }
             }
         }
-        const int ip = sh ? p + (p >> K1_SH) : p;
-#pragma unroll
-        for (int b = 0; b < BMAX; ++b)
-            if (b < B) Y[(b * NT + nl) * Ppad + ip] = acc[b];
     }
     __syncthreads();
+    trace_stamp(fp, 1);
     float2* __restrict__ z = fp.z[f];
     const int zslab = P * NT;   // contiguous [P][NT] slab per (b, tile)
     const int lgNT = ilog2(NT);
@@ -323,7 +423,8 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
     const int half = P >> 1;
     if (fft) {
         // ---- Phase B: P-point FFT of every (b, nl) column (fsf:135)
-        k1_fft(g.logP, Y, Ppad, B * NT, twl);
+        if (!(g.dbg & 2)) k1_fft(g.logP, Y, Ppad, B * NT, twl);   // RSP_ABLATE=2 skips it
+        trace_stamp(fp, 2);
         // ---- Phase C: fftshift (fsf:135) + coalesced store of the [P][NT] slabs
         for (int e = threadIdx.x; e < B * zslab; e += K1_THREADS) {
             const int b = e / zslab, rem = e - b * zslab;
@@ -331,6 +432,10 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
             int src = v - half;
             if (src < 0) src += P;
             z[((size_t)b * g.ntiles + tile) * zslab + rem] = Y[(b * NT + nl) * Ppad + src + (src >> K1_SH)];
+        }
+        if (fp.trace) {
+            __syncthreads();
+            trace_stamp(fp, 3);
         }
     } else {
         // non power-of-two P: direct DFT straight to global (O(P^2) per column)
@@ -360,8 +465,7 @@ __device__ __forceinline__ float cabsf(float2 a) { return sqrtf(a.x * a.x + a.y 
 struct StoreRdm {   // last inverse pass: keep outputs i in [Lh-1, Lh-1+V) that map to gates < gend;
                     // also writes |x| (the CFAR input, fsf:184-185) into the magnitude map
     float2* rdm; float* mag; int G; int Gp; int row0; int rows_total; int Lh1; int g0; int gend;
-    template <int SH>
-    __device__ __forceinline__ void put(int row, int o, float2 x) const {
+    __device__ __forceinline__ void put(int, int row, int o, int, float2 x) const {
         const int gg = g0 + o - Lh1;
         const int rho = row0 + row;
         if (o >= Lh1 && gg < gend && rho < rows_total) {
@@ -373,16 +477,21 @@ struct StoreRdm {   // last inverse pass: keep outputs i in [Lh-1, Lh-1+V) that 
 
 #define K2_SH 5   // one pad complex per 32 (tools/lds_conflicts.py)
 #define K2_LDS_DATA (RSP_K2_POINTS + (RSP_K2_POINTS >> K2_SH))
+#define K2_LDS_TW 2048   // >= tw_total(log2 M) for M <= 2048
 #define K2_MAXM 2048
 
 // One overlap-save block of one FFT segment for RSP_K2_POINTS / 2^LGM adjacent rows.
 template <int LGM>
 __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k, const SegDesc& sd, const K2Job& job,
                                            const float2* __restrict__ z, float2* __restrict__ rdm,
-                                           float* __restrict__ mag, int row0, int rows_total, float2* L) {
+                                           float* __restrict__ mag, int row0, int rows_total, float2* L,
+                                           const FramePtrs& fp) {
     constexpr int M = 1 << LGM;
     constexpr int rows = RSP_K2_POINTS / M;
     constexpr int rs = M + (M >> K2_SH);
+    constexpr int NP = n_passes(LGM);
+    constexpr int RL = 1 << rad_bits(LGM, NP - 1);   // radix of the last forward pass
+    constexpr int NBL = 16 / RL;                     // its butterflies per thread
     const int P = g.P, G = g.G;
     const int lo = sd.lo, hi = sd.hi, off = sd.off;
     const int tid = threadIdx.x;
@@ -390,9 +499,9 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     const int g0 = sd.ga + job.blk * sd.V;
     const int a = sd.seg_lo + g0 - Lh1;           // sample index of u[0]
     float2* twl = L + K2_LDS_DATA;
-    float2* Hl = twl + K2_MAXM;
-    // issue every global load of the workgroup before the first LDS store:
-    // 16 samples + 2 x M/256 table entries per thread in flight together
+    // issue every global load of the workgroup before the first LDS store: 16 samples,
+    // the pass twiddles and this thread's 16 filter-spectrum values (kept in registers
+    // for the last forward pass) in flight together
     float2 val[16];
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
@@ -406,14 +515,20 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
             val[u] = z[zaddr(g, b, v, n - lo + off)];
         }
     }
-    constexpr int NT_TAB = (M + RSP_THREADS - 1) / RSP_THREADS;
+    float2 hreg[16];
+#pragma unroll
+    for (int t = 0; t < NBL; ++t) {
+        const int j = (tid + t * RSP_THREADS) & (M / RL - 1);   // last pass: Ns = nb = M / RL, idxD = j
+#pragma unroll
+        for (int r = 0; r < RL; ++r) hreg[t * RL + r] = k.H[sd.H_off + j + r * (M / RL)];
+    }
     constexpr int NTW = tw_total(LGM);
-    float2 tv[NT_TAB], hv[NT_TAB];
+    constexpr int NT_TAB = (NTW + RSP_THREADS - 1) / RSP_THREADS;
+    float2 tv[NT_TAB];
 #pragma unroll
     for (int u = 0; u < NT_TAB; ++u) {
         const int i = tid + u * RSP_THREADS;
         if (i < NTW) tv[u] = k.twM[sd.tw_off + i];
-        if (i < M) hv[u] = k.H[sd.H_off + i];
     }
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
@@ -424,16 +539,18 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     for (int u = 0; u < NT_TAB; ++u) {
         const int i = tid + u * RSP_THREADS;
         if (i < NTW) twl[i] = tv[u];
-        if (i < M) Hl[i] = hv[u];
     }
     __syncthreads();
+    trace_stamp(fp, 1);
     // forward FFT; the last pass multiplies by the block filter spectrum H (1/M folded in)
-    fft_passes<LGM, 0, 0, 16, false, K2_SH, RSP_THREADS>(L, rs, rows, twl, StoreLds{L, rs, nullptr},
-                                                        StoreLds{L, rs, Hl});
+    fft_passes<LGM, 0, 0, 16, false, K2_SH, RSP_THREADS>(L, rs, rows, twl, StoreLds{L},
+                                                        StoreLdsH<16>{L, hreg});
+    trace_stamp(fp, 2);
     // inverse FFT; the last pass keeps the valid overlap-save outputs = stitched gates
     const int gend = min(sd.gb, g0 + sd.V);
-    fft_passes<LGM, 0, 0, 16, true, K2_SH, RSP_THREADS>(L, rs, rows, twl, StoreLds{L, rs, nullptr},
+    fft_passes<LGM, 0, 0, 16, true, K2_SH, RSP_THREADS>(L, rs, rows, twl, StoreLds{L},
                                                        StoreRdm{rdm, mag, G, g.Gp, row0, rows_total, Lh1, g0, gend});
+    trace_stamp(fp, 3);
 }
 
 __global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k, FramePtrs fp, int rows_total) {
@@ -441,11 +558,12 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k,
     const int f = blockIdx.y;
     const int wg = blockIdx.x;
     int ji = 0;
-    while (ji + 1 < g.njobs && wg >= k.jobs[ji + 1].wg_begin) ++ji;
-    const K2Job job = k.jobs[ji];
-    const SegDesc& sd = k.segs[job.seg];
+    while (ji + 1 < g.njobs && wg >= g.jobs[ji + 1].wg_begin) ++ji;
+    const K2Job job = g.jobs[ji];
+    const SegDesc& sd = g.segs[job.seg];
     const int rows = sd.rows_per_wg;
     const int row0 = (wg - job.wg_begin) * rows;
+    trace_stamp(fp, 0);
     const float2* __restrict__ z = fp.z[f];
     float2* __restrict__ rdm = fp.rdm[f];
     float* __restrict__ mag = fp.mag[f];
@@ -455,12 +573,12 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k,
 
     if (sd.type == 1) {
         switch (sd.logM) {
-            case 6: k2_fft_job<6>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-            case 7: k2_fft_job<7>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-            case 8: k2_fft_job<8>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-            case 9: k2_fft_job<9>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-            case 10: k2_fft_job<10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-            default: k2_fft_job<11>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+            case 6: k2_fft_job<6>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
+            case 7: k2_fft_job<7>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
+            case 8: k2_fft_job<8>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
+            case 9: k2_fft_job<9>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
+            case 10: k2_fft_job<10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
+            default: k2_fft_job<11>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
         }
     } else {
         // direct FIR (narrow segment): filter() + circshift(-fir_delay) (fsf:111-112)
@@ -521,37 +639,49 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k,
 // ======================================================================================
 // Peak of MATLAB interp1(...,'spline') (not-a-knot) sampled at step 1/interp over n
 // equally spaced points (fsf:257-260, 272-275); returns the first-argmax abscissa.
-__device__ double spline_peak(const double* y, int n, int interp) {
-    const int nq = (n - 1) * interp + 1;
-    const double dx = (interp == 8) ? 0.125 : (interp == 4 ? 0.25 : 1.0 / interp);   // exact steps
-    const double sixth = 1.0 / 6.0;
-    double Mv[5] = {0, 0, 0, 0, 0};
+template <int INTERP>
+__device__ double spline_peak(const double* y, int n) {
+    // Piecewise-cubic coefficients per unit interval, then Horner at q / INTERP; the sample
+    // grid and the first-argmax rule are the reference's (interp1 on cells(1):1/INTERP:cells(end)).
+    constexpr double dx = 1.0 / INTERP;   // 1/8, 1/4: exact
+    double c0[4], c1[4], c2[4], c3[4];   // value on [i, i+1]: ((c3 t + c2) t + c1) t + c0
     if (n == 5) {   // not-a-knot second derivatives, unit spacing (closed form of the 5x5 system)
+        double Mv[5];
         Mv[1] = y[0] - 2.0 * y[1] + y[2];
         Mv[3] = y[2] - 2.0 * y[3] + y[4];
         Mv[2] = (6.0 * (y[1] - 2.0 * y[2] + y[3]) - Mv[1] - Mv[3]) * 0.25;
         Mv[0] = 2.0 * Mv[1] - Mv[2];
         Mv[4] = 2.0 * Mv[3] - Mv[2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            c0[i] = y[i];
+            c1[i] = (y[i + 1] - y[i]) - (2.0 * Mv[i] + Mv[i + 1]) * (1.0 / 6.0);
+            c2[i] = 0.5 * Mv[i];
+            c3[i] = (Mv[i + 1] - Mv[i]) * (1.0 / 6.0);
+        }
+    } else {          // n == 4: the single cubic through 4 points; n == 3: the parabola
+        const double d1 = y[1] - y[0], d2 = y[2] - 2.0 * y[1] + y[0];
+        const double d3 = (n == 4) ? y[3] - 3.0 * y[2] + 3.0 * y[1] - y[0] : 0.0;
+        // Newton form about x = 0 expanded at each integer knot i
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const double x = i;
+            c0[i] = y[0] + x * d1 + x * (x - 1.0) * 0.5 * d2 + x * (x - 1.0) * (x - 2.0) * (1.0 / 6.0) * d3;
+            c1[i] = d1 + (2.0 * x - 1.0) * 0.5 * d2 + (3.0 * x * x - 6.0 * x + 2.0) * (1.0 / 6.0) * d3;
+            c2[i] = 0.5 * d2 + (3.0 * x - 3.0) * (1.0 / 6.0) * d3;
+            c3[i] = (1.0 / 6.0) * d3;
+        }
     }
-    const double d1 = y[1] - y[0], d2 = y[2] - 2.0 * y[1] + y[0];
-    const double d3 = (n >= 4) ? y[3] - 3.0 * y[2] + 3.0 * y[1] - y[0] : 0.0;
+    const int nq = (n - 1) * INTERP + 1;
     double best = -INFINITY, bx = 0.0;
     for (int q = 0; q < nq; ++q) {
-        const double xq = q * dx;
-        double val;
-        if (n == 5) {
-            int i = q / interp;
-            if (i > 3) i = 3;
-            const double t = xq - i, u = 1.0 - t;
-            val = u * y[i] + t * y[i + 1] + ((u * u * u - u) * Mv[i] + (t * t * t - t) * Mv[i + 1]) * sixth;
-        } else if (n == 4) {   // the single cubic through 4 points
-            val = y[0] + xq * d1 + xq * (xq - 1.0) * 0.5 * d2 + xq * (xq - 1.0) * (xq - 2.0) * sixth * d3;
-        } else {               // parabola through 3 points
-            val = y[0] + xq * d1 + xq * (xq - 1.0) * 0.5 * d2;
-        }
+        int i = q / INTERP;
+        if (i > n - 2) i = n - 2;
+        const double t = (q - i * INTERP) * dx;
+        const double val = ((c3[i] * t + c2[i]) * t + c1[i]) * t + c0[i];
         if (val > best) {
             best = val;
-            bx = xq;
+            bx = q * dx;
         }
     }
     return bx;
@@ -579,8 +709,8 @@ __device__ __forceinline__ void s9_estimate(const DevConsts& k, const float* S, 
             yv[nvc++] = (double)S[vv * W + c];
         }
     }
-    const double rmax = (nrc < 3) ? (double)r : rfirst + spline_peak(yr, nrc, 8);
-    const double vmax = (nvc < 3) ? (double)v : vfirst + spline_peak(yv, nvc, 4);
+    const double rmax = (nrc < 3) ? (double)r : rfirst + spline_peak<8>(yr, nrc);
+    const double vmax = (nvc < 3) ? (double)v : vfirst + spline_peak<4>(yv, nvc);
     // amplitude monopulse on the integer cell (fsf:282-290)
     const double SA = (double)MA[(size_t)v * Gp + r];
     const double SB = (double)MB[(size_t)v * Gp + r];
@@ -600,11 +730,13 @@ __device__ __forceinline__ void s9_estimate(const DevConsts& k, const float* S, 
 #define K3_QCAP 1024
 #define K3_VEC 12   // float4 loads per beam per thread in flight
 
+// RR/RV = reference-cell counts when known at compile time (the reference's 5/5), 0 = runtime.
+template <int RR, int RV>
 __global__ __launch_bounds__(RSP_THREADS) void k3_cfar(Geometry g, DevConsts k, FramePtrs fp) {
     extern __shared__ __attribute__((aligned(16))) float S[];   // [P][W] | queue[K3_QCAP] | qn, base
     const int f = blockIdx.z, pair = blockIdx.y, tile = blockIdx.x;
     const int P = g.P, G = g.G, W = g.cfar_W, hR = g.cfar_hR;
-    const int rR = g.refR, gR = g.guardR, rV = g.refV, gV = g.guardV;
+    const int rR = RR ? RR : g.refR, gR = g.guardR, rV = RV ? RV : g.refV, gV = g.guardV;
     const int r_begin = rR + gR + tile * g.cfar_RT;
     const int r_end = min(r_begin + g.cfar_RT, G - rR - gR);
     const int c0 = r_begin - hR;
@@ -614,6 +746,7 @@ __global__ __launch_bounds__(RSP_THREADS) void k3_cfar(Geometry g, DevConsts k, 
     const float* __restrict__ MA = fp.mag[f] + (size_t)pair * P * Gp;   // |RDM| of beams pair, pair+1
     const float* __restrict__ MB = MA + (size_t)P * Gp;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;   // 4 waves
+    trace_stamp(fp, 0);
     if (threadIdx.x == 0) qn[0] = 0;
     // ---- load S = |A| + |B| (fsf:184-187) from the magnitude maps: 16 B per lane,
     //      K3_VEC float4 of each beam in flight per thread
@@ -652,10 +785,11 @@ __global__ __launch_bounds__(RSP_THREADS) void k3_cfar(Geometry g, DevConsts k, 
         }
     }
     __syncthreads();
+    trace_stamp(fp, 1);
     const int v0 = rV + gV, v1 = P - rV - gV;
     const int nr = r_end - r_begin;
     if (v1 <= v0 || nr <= 0) return;
-    const float invR = 1.0f / (float)rR, invV = 1.0f / (float)rV;
+    const float fR = (float)rR, fV = (float)rV;
     // ---- cross GOCA-CFAR (fsf:192-213); hits go to an LDS queue so that the S9 work is
     //      spread over the whole workgroup instead of serialising in the lane that owns a range cell
     for (int rb = 0; rb < nr; rb += 64) {
@@ -665,17 +799,25 @@ __global__ __launch_bounds__(RSP_THREADS) void k3_cfar(Geometry g, DevConsts k, 
         const int c = r - c0;
         for (int v = v0 + wv; v < v1; v += 4) {
             const float* rowp = S + v * W;
+            // window sums left to right like mean() over the slices of fsf:197-203; with RR/RV
+            // known the 2*(RR+RV) LDS reads are independent and issue back to back
             float lr = 0.f, tr = 0.f, lv = 0.f, tv = 0.f;
-            for (int q = 0; q < rR; ++q) {
-                lr += rowp[c - gR - rR + q];
-                tr += rowp[c + gR + 1 + q];
+            const float* lrp = rowp + c - gR - rR;
+            const float* trp = rowp + c + gR + 1;
+            const float* lvp = S + (v - gV - rV) * W + c;
+            const float* tvp = S + (v + gV + 1) * W + c;
+#pragma unroll
+            for (int q = 0; q < (RR ? RR : rR); ++q) {
+                lr += lrp[q];
+                tr += trp[q];
             }
-            for (int q = 0; q < rV; ++q) {
-                lv += S[(v - gV - rV + q) * W + c];
-                tv += S[(v + gV + 1 + q) * W + c];
+#pragma unroll
+            for (int q = 0; q < (RV ? RV : rV); ++q) {
+                lv += lvp[q * W];
+                tv += tvp[q * W];
             }
-            const float nR = fmaxf(lr * invR, tr * invR);   // mean() = sum / n
-            const float nV = fmaxf(lv * invV, tv * invV);
+            const float nR = fmaxf(lr / fR, tr / fR);   // mean() = sum / n
+            const float nV = fmaxf(lv / fV, tv / fV);
             const float thr = g.T * fmaxf(nR, nV);
             if (rowp[c] > thr) {
                 const int qi = atomicAdd(qn, 1);
@@ -689,8 +831,12 @@ __global__ __launch_bounds__(RSP_THREADS) void k3_cfar(Geometry g, DevConsts k, 
         }
     }
     __syncthreads();
+    trace_stamp(fp, 2);
     const int n = min(qn[0], K3_QCAP);
-    if (n == 0) return;
+    if (n == 0) {
+        trace_stamp(fp, 3);
+        return;
+    }
     if (threadIdx.x == 0) qn[1] = atomicAdd(fp.count[f], n);   // one global reservation per workgroup
     __syncthreads();
     const int base = qn[1];
@@ -700,6 +846,10 @@ __global__ __launch_bounds__(RSP_THREADS) void k3_cfar(Geometry g, DevConsts k, 
         const int e = queue[i];
         const int v = e >> 16, c = e & 0xFFFF;
         s9_estimate(k, S, W, c0, P, G, Gp, v, c0 + c, pair, MA, MB, &fp.dets[f][idx]);
+    }
+    if (fp.trace) {
+        __syncthreads();
+        trace_stamp(fp, 3);
     }
 }
 
@@ -730,7 +880,7 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k_mtd_cols(Geometry g, DevCons
     __syncthreads();
     const int half = P >> 1;
     if constexpr (LGP > 0) {
-        StoreLds st{Y, Ppad, nullptr};
+        StoreLds st{Y};
         fft_passes<LGP, 0, 0, (16 << LGP) / RSP_THREADS, false, 0, RSP_THREADS>(Y, Ppad, GT, twl, st, st);
         for (int e = threadIdx.x; e < P * GT; e += RSP_THREADS) {
             const int v = e / GT, gl = e - v * GT;
@@ -829,7 +979,7 @@ static hipError_t allow_lds(K kernel, size_t bytes) {
 template <int BMAX, int CP>
 static hipError_t launch_k1_t(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int mode,
                               hipStream_t s) {
-    const size_t lds = ((size_t)g.B * g.NT * g.Ppad + ((g.P + 1) & ~1) + CP * BMAX) * sizeof(float2);
+    const size_t lds = ((size_t)g.B * g.NT * g.Ppad + g.P) * sizeof(float2);
     hipError_t e = allow_lds(k1_dbf_mtd<BMAX, CP>, lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k1_dbf_mtd<BMAX, CP>), dim3(g.ntiles, nf), dim3(K1_THREADS), lds, s, g, k, fp, mode);
@@ -853,7 +1003,7 @@ hipError_t launch_k1(const Geometry& g, const DevConsts& k, const FramePtrs& fp,
 
 hipError_t launch_k2(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int rows,
                      hipStream_t s) {
-    const size_t lds = (size_t)(K2_LDS_DATA + 2 * K2_MAXM) * sizeof(float2);
+    const size_t lds = (size_t)(K2_LDS_DATA + K2_LDS_TW) * sizeof(float2);
     hipError_t e = allow_lds(k2_pc, lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k2_pc, dim3(g.nwg_k2, nf), dim3(RSP_THREADS), lds, s, g, k, fp, rows);
@@ -865,9 +1015,15 @@ hipError_t launch_k3(const Geometry& g, const DevConsts& k, const FramePtrs& fp,
     if (g.B < 2 || ncut_r <= 0) return hipSuccess;
     const int tiles = (ncut_r + g.cfar_RT - 1) / g.cfar_RT;
     const size_t lds = (size_t)g.P * g.cfar_W * sizeof(float) + (K3_QCAP + 4) * sizeof(int);
-    hipError_t e = allow_lds(k3_cfar, lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k3_cfar, dim3(tiles, g.B - 1, nf), dim3(RSP_THREADS), lds, s, g, k, fp);
+    const dim3 grid(tiles, g.B - 1, nf);
+    hipError_t e;
+    if (g.refR == 5 && g.refV == 5) {   // the reference's cfar_params (v8:45-46)
+        if ((e = allow_lds(k3_cfar<5, 5>, lds)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k3_cfar<5, 5>), grid, dim3(RSP_THREADS), lds, s, g, k, fp);
+    } else {
+        if ((e = allow_lds(k3_cfar<0, 0>, lds)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k3_cfar<0, 0>), grid, dim3(RSP_THREADS), lds, s, g, k, fp);
+    }
     return hipGetLastError();
 }
 

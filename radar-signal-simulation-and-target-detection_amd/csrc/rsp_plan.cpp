@@ -10,6 +10,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <deque>
 #include <string>
 #include <vector>
@@ -136,7 +137,7 @@ struct rsp_plan {
     double deltaR = 0, deltaV = 0;
     double p_signal_unscaled = 0, c = 0, fs = 0, wavelength = 0, d = 0, prt = 0;
     int F = 1;
-    int async_cap = 2048;
+    int async_cap = 512;
     size_t z_elems = 0, rdm_elems = 0, mag_elems = 0;
     std::vector<SegDesc> segs;
     std::vector<K2Job> jobs;
@@ -191,23 +192,42 @@ rsp_plan::~rsp_plan() {
 namespace {
 
 // ---- S10 / S11 on the host (fsf:302-407) ---------------------------------------------
-template <class Close>
-int bfs_labels(int n, Close close, std::vector<int>& ids) {
+// The reference labels clusters with a BFS that scans every point for every visited point
+// (O(n^2)).  Its clusters are exactly the connected components of the "close" relation, and
+// cluster k is the component whose smallest index is the k-th smallest such index.  We find
+// the same components with union-find over the edges of a sweep in Range order (close()
+// requires |dR| <= max_range_sep, so no other pair can be an edge) and number them the same
+// way; member sums then run in index order like the reference's cluster_mask loops.
+struct DSU {
+    std::vector<int> p;
+    explicit DSU(int n) : p(n) { for (int i = 0; i < n; ++i) p[i] = i; }
+    int find(int x) {
+        while (p[x] != x) x = p[x] = p[p[x]];
+        return x;
+    }
+    void unite(int a, int b) {
+        a = find(a); b = find(b);
+        if (a != b) p[a < b ? b : a] = a < b ? a : b;
+    }
+};
+
+template <class Item, class Close>
+int component_labels(const std::vector<Item>& it, double rsep, Close close, std::vector<int>& ids) {
+    const int n = (int)it.size();
+    std::vector<int> ord(n);
+    for (int i = 0; i < n; ++i) ord[i] = i;
+    std::sort(ord.begin(), ord.end(), [&](int a, int b) { return it[a].Range < it[b].Range; });
+    DSU d(n);
+    for (int x = 0; x < n; ++x)
+        for (int y = x + 1; y < n && it[ord[y]].Range - it[ord[x]].Range <= rsep; ++y)
+            if (close(it[ord[x]], it[ord[y]])) d.unite(ord[x], ord[y]);
     ids.assign(n, 0);
+    std::vector<int> lab(n, 0);
     int cur = 0;
-    std::vector<int> queue;
     for (int i = 0; i < n; ++i) {
-        if (ids[i]) continue;
-        ++cur;
-        queue.clear();
-        queue.push_back(i);
-        for (size_t h = 0; h < queue.size(); ++h) {
-            const int ci = queue[h];
-            if (ids[ci]) continue;
-            ids[ci] = cur;
-            for (int j = 0; j < n; ++j)
-                if (!ids[j] && close(ci, j)) queue.push_back(j);
-        }
+        const int r = d.find(i);
+        if (!lab[r]) lab[r] = ++cur;
+        ids[i] = lab[r];
     }
     return cur;
 }
@@ -224,30 +244,32 @@ void cluster_frame(const rsp_cluster_params& cp, std::vector<rsp_detection>& det
     const int n = (int)dets.size();
     if (!n) return;
     std::vector<int> ids;
-    const int n1 = bfs_labels(n, [&](int a, int b) {
-        return std::fabs(dets[a].Range - dets[b].Range) <= cp.max_range_sep &&
-               std::fabs(dets[a].Velocity - dets[b].Velocity) <= cp.max_vel_sep &&
-               std::fabs(dets[a].Angle - dets[b].Angle) <= cp.max_angle_sep;
+    const int n1 = component_labels(dets, cp.max_range_sep, [&](const rsp_detection& a, const rsp_detection& b) {
+        return std::fabs(a.Range - b.Range) <= cp.max_range_sep && std::fabs(a.Velocity - b.Velocity) <= cp.max_vel_sep &&
+               std::fabs(a.Angle - b.Angle) <= cp.max_angle_sep;
     }, ids);
-    std::vector<rsp_target> st1(n1);
-    for (int c = 1; c <= n1; ++c) {   // power-weighted means in index order (fsf:341-351)
-        double tp = 0, sr = 0, sv = 0, sa = 0;
-        for (int i = 0; i < n; ++i) if (ids[i] == c) tp += dets[i].amp;
-        for (int i = 0; i < n; ++i) if (ids[i] == c) sr += dets[i].Range * dets[i].amp;
-        for (int i = 0; i < n; ++i) if (ids[i] == c) sv += dets[i].Velocity * dets[i].amp;
-        for (int i = 0; i < n; ++i) if (ids[i] == c) sa += dets[i].Angle * dets[i].amp;
-        st1[c - 1] = rsp_target{sr / tp, sv / tp, sa / tp, tp};
+    std::vector<rsp_target> st1(n1, rsp_target{0, 0, 0, 0});
+    std::vector<double> sr(n1, 0.0), sv(n1, 0.0), sa(n1, 0.0);
+    for (int i = 0; i < n; ++i) st1[ids[i] - 1].Power += dets[i].amp;   // power-weighted means (fsf:341-351)
+    for (int i = 0; i < n; ++i) {
+        const int c = ids[i] - 1;
+        sr[c] += dets[i].Range * dets[i].amp;
+        sv[c] += dets[i].Velocity * dets[i].amp;
+        sa[c] += dets[i].Angle * dets[i].amp;
     }
-    const int n2 = bfs_labels(n1, [&](int a, int b) {
-        return std::fabs(st1[a].Range - st1[b].Range) <= cp.max_range_sep &&
-               std::fabs(st1[a].Velocity - st1[b].Velocity) <= cp.max_vel_sep;
+    for (int c = 0; c < n1; ++c) {
+        const double tp = st1[c].Power;
+        st1[c] = rsp_target{sr[c] / tp, sv[c] / tp, sa[c] / tp, tp};
+    }
+    const int n2 = component_labels(st1, cp.max_range_sep, [&](const rsp_target& a, const rsp_target& b) {
+        return std::fabs(a.Range - b.Range) <= cp.max_range_sep && std::fabs(a.Velocity - b.Velocity) <= cp.max_vel_sep;
     }, ids);
-    for (int c = 1; c <= n2; ++c) {   // winner-take-all, first max (fsf:393-406)
-        int w = -1;
-        for (int i = 0; i < n1; ++i)
-            if (ids[i] == c && (w < 0 || st1[i].Power > st1[w].Power)) w = i;
-        final_targets.push_back(st1[w]);
+    std::vector<int> win(n2, -1);   // winner-take-all, first max in index order (fsf:393-406)
+    for (int i = 0; i < n1; ++i) {
+        int& w = win[ids[i] - 1];
+        if (w < 0 || st1[i].Power > st1[w].Power) w = i;
     }
+    for (int c = 0; c < n2; ++c) final_targets.push_back(st1[win[c]]);
 }
 
 // ---- geometry analysis ------------------------------------------------------------------
@@ -527,6 +549,7 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     g.refR = cfar->refCells_R; g.guardR = cfar->guardCells_R; g.refV = cfar->refCells_V; g.guardV = cfar->guardCells_V;
     g.T = (float)cfar->T_CFAR;
     g.max_dets = 1 << 16;
+    if (const char* ab = getenv("RSP_ABLATE")) g.dbg = atoi(ab);   // timing experiments only
     auto bail = [&](int rc) { delete p; return rc; };
     if (g.refR < 1 || g.refV < 1 || g.guardR < 0 || g.guardV < 0) return bail(fail(RSP_ERR_INVALID, "bad CFAR window"));
 
@@ -605,6 +628,13 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
         return bail(fail(RSP_ERR_UNSUPPORTED, "B*P too large for the slow-time FFT tile"));
     g.ntiles = (g.nU + g.NT - 1) / g.NT;
     nof.resize((size_t)g.ntiles * g.NT, -1);
+    if ((int)U.size() > RSP_MAX_IVL) return bail(fail(RSP_ERR_UNSUPPORTED, "too many sample intervals"));
+    g.nivl = (int)U.size();
+    for (int q = 0, st = 0; q < g.nivl; ++q) {
+        g.ivl_lo[q] = U[q].lo;
+        g.ivl_start[q] = st;
+        st += U[q].hi - U[q].lo + 1;
+    }
     if (g.pow2P) {
         g.logP = ilog2i(P);
         radix_plan(g.logP, &g.nradP, g.radP);
@@ -625,6 +655,10 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     }
     g.nseg = (int)p->segs.size();
     g.njobs = (int)p->jobs.size();
+    if (g.nseg > RSP_MAX_SEG || g.njobs > RSP_MAX_JOBS)
+        return bail(fail(RSP_ERR_UNSUPPORTED, "%d overlap-save jobs exceed %d", g.njobs, RSP_MAX_JOBS));
+    for (int q = 0; q < g.nseg; ++q) g.segs[q] = p->segs[q];
+    for (int q = 0; q < g.njobs; ++q) g.jobs[q] = p->jobs[q];
     g.nwg_k2 = wg;
     // K3 tile
     g.cfar_hR = std::max(g.refR + g.guardR, 2);
@@ -647,6 +681,23 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
         }
     if (g.pow2P) build_pass_twiddles(g.logP, twPp);
     g.wc_elems = (int)Wc.size();
+    // per-lane A operands of the DBF MFMA (k1_dbf_mtd): lane l holds A[row l&15][channel 4j + l>>4];
+    // row m: beam mb*8 + (m&7), m<8 -> Re(y), m>=8 -> Im(y); y = sum_c conj(W[b][c]) x_c (fsf:95)
+    const int mblk = bmax <= 8 ? 1 : 2, nj = cpad / 4;
+    std::vector<float> atab((size_t)mblk * nj * 2 * 64, 0.f);
+    for (int mb = 0; mb < mblk; ++mb)
+        for (int j = 0; j < nj; ++j)
+            for (int lane = 0; lane < 64; ++lane) {
+                const int m = lane & 15, c = 4 * j + (lane >> 4), b = mb * 8 + (m & 7);
+                float wr = 0.f, wi = 0.f;
+                if (b < B && c < C) {
+                    wr = Wc[(size_t)c * bmax + b].x;
+                    wi = Wc[(size_t)c * bmax + b].y;
+                }
+                const bool im = m >= 8;
+                atab[((mb * nj + j) * 2 + 0) * 64 + lane] = im ? wi : wr;    // coefficient of Re(x_c)
+                atab[((mb * nj + j) * 2 + 1) * 64 + lane] = im ? wr : -wi;   // coefficient of Im(x_c)
+            }
     g.twPp_elems = (int)twPp.size();
     for (int i = 0; i < P; ++i) {
         const double a = -2.0 * M_PI * i / P;
@@ -657,15 +708,15 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     std::vector<double> ang(pre->beam_angles_deg, pre->beam_angles_deg + B);
     std::vector<double> kl(std::max(B - 1, 1), 0.0);
     for (int i = 0; i + 1 < B; ++i) kl[i] = pre->k_slopes_LUT[i];
-    float2 *dWc, *dtwP, *dtwPp, *dH, *dtwM; float *dwin, *dtaps; int* dnof; SegDesc* dsegs; K2Job* djobs;
+    float2 *dWc, *dtwP, *dtwPp, *dH, *dtwM; float *dwin, *dtaps, *datab; int* dnof; SegDesc* dsegs; K2Job* djobs;
     double *dra, *dva, *dang, *dkl;
-    if ((rc = p->upload(&dWc, Wc)) || (rc = p->upload(&dtwP, twP)) || (rc = p->upload(&dtwPp, twPp)) || (rc = p->upload(&dwin, win)) ||
+    if ((rc = p->upload(&dWc, Wc)) || (rc = p->upload(&datab, atab)) || (rc = p->upload(&dtwP, twP)) || (rc = p->upload(&dtwPp, twPp)) || (rc = p->upload(&dwin, win)) ||
         (rc = p->upload(&dnof, nof)) || (rc = p->upload(&dsegs, p->segs)) || (rc = p->upload(&djobs, p->jobs)) ||
         (rc = p->upload(&dtaps, taps)) || (rc = p->upload(&dH, H)) || (rc = p->upload(&dtwM, twM)) ||
         (rc = p->upload(&dra, ra)) || (rc = p->upload(&dva, va)) || (rc = p->upload(&dang, ang)) ||
         (rc = p->upload(&dkl, kl)))
         return bail(rc);
-    p->k = DevConsts{dWc, dwin, dtwP, dtwPp, dnof, dsegs, djobs, dtaps, dH, dtwM, dra, dva, dang, dkl, pre->deltaR, pre->deltaV};
+    p->k = DevConsts{dWc, datab, dwin, dtwP, dtwPp, dnof, dsegs, djobs, dtaps, dH, dtwM, dra, dva, dang, dkl, pre->deltaR, pre->deltaV};
     if (pre->tx_pulse) {
         std::vector<double> tx(pre->tx_pulse, pre->tx_pulse + 2 * (size_t)N);
         if ((rc = p->upload(&p->d_tx, tx))) return bail(rc);
@@ -679,6 +730,18 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     for (auto& L : p->lanes)
         if ((rc = setup_lane(p, L))) return bail(rc);
     *out = p;
+    return RSP_OK;
+}
+
+int32_t rsp_cluster_detections(const rsp_detection* dets, int32_t n, const rsp_cluster_params* cp,
+                               rsp_target* out, int32_t cap, int32_t* n_out) {
+    if ((!dets && n) || n < 0 || !cp || !n_out) return fail(RSP_ERR_INVALID, "bad argument");
+    std::vector<rsp_detection> d(dets, dets + n);
+    std::vector<rsp_target> t;
+    cluster_frame(*cp, d, t);
+    *n_out = (int32_t)t.size();
+    if (out) memcpy(out, t.data(), sizeof(rsp_target) * std::min<size_t>(cap, t.size()));
+    if ((int)t.size() > cap) return fail(RSP_ERR_OVERFLOW, "%d targets exceed cap %d", (int)t.size(), cap);
     return RSP_OK;
 }
 
@@ -821,26 +884,27 @@ int32_t rsp_process_stage2(rsp_plan* p, const void* iq, int32_t dtype, double* m
     return RSP_OK;
 }
 
-int32_t rsp_profile_stages(rsp_plan* p, const void* d_cube, int32_t iters, float* ms_out, int64_t* bytes_out,
-                           int32_t cap) {
-    if (!p || !d_cube || iters < 1) return fail(RSP_ERR_INVALID, "bad argument");
+int32_t rsp_profile_stages(rsp_plan* p, const void* const* d_cubes, int32_t n_cubes, int32_t iters, float* ms_out,
+                           int64_t* bytes_out, int32_t cap, int32_t* frames_out) {
+    if (!p || !d_cubes || n_cubes < 1 || iters < 1) return fail(RSP_ERR_INVALID, "bad argument");
     HIPCHK(hipSetDevice(p->device));
     int rc = drain_all(p);
     if (rc) return rc;
     Lane& L = p->lanes[0];
-    const float2* in[1] = {(const float2*)d_cube};
-    const FramePtrs fp = lane_ptrs(p, L, in, 1);
+    const int nf = std::min(n_cubes, p->F);
+    const float2* in[RSP_MAX_F];
+    for (int f = 0; f < nf; ++f) in[f] = (const float2*)d_cubes[f];
+    const FramePtrs fp = lane_ptrs(p, L, in, nf);
     const Geometry& g = p->g;
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
-    HIPCHK(hipMemsetAsync(L.count, 0, sizeof(int), L.stream));
     for (int s = 0; s < 3 && s < cap; ++s) {
         auto run = [&]() -> hipError_t {
-            if (s == 0) return launch_k1(g, p->k, fp, 1, 3, g.C, L.stream);
-            if (s == 1) return launch_k2(g, p->k, fp, 1, g.B * g.P, L.stream);
-            hipError_t e = hipMemsetAsync(L.count, 0, sizeof(int), L.stream);
-            return e != hipSuccess ? e : launch_k3(g, p->k, fp, 1, L.stream);
+            if (s == 0) return launch_k1(g, p->k, fp, nf, 3, g.C, L.stream);
+            if (s == 1) return launch_k2(g, p->k, fp, nf, g.B * g.P, L.stream);
+            hipError_t e = hipMemsetAsync(L.count, 0, sizeof(int) * nf, L.stream);
+            return e != hipSuccess ? e : launch_k3(g, p->k, fp, nf, L.stream);
         };
         HIPCHK(run());
         HIPCHK(hipEventRecord(e0, L.stream));
@@ -851,14 +915,42 @@ int32_t rsp_profile_stages(rsp_plan* p, const void* d_cube, int32_t iters, float
         HIPCHK(hipEventElapsedTime(&ms, e0, e1));
         if (ms_out) ms_out[s] = ms / iters;
     }
+    if (frames_out) *frames_out = nf;
+    if (const char* tf = getenv("RSP_TRACE_FILE")) {   // diagnostic per-workgroup phase stamps
+        size_t nwg[3] = {(size_t)g.ntiles * nf, (size_t)g.nwg_k2 * nf,
+                         (size_t)((g.G - 2 * (g.refR + g.guardR) + g.cfar_RT - 1) / g.cfar_RT) * (g.B - 1) * nf};
+        size_t mx = std::max(nwg[0], std::max(nwg[1], nwg[2]));
+        unsigned long long* dt = nullptr;
+        HIPCHK(hipMalloc(&dt, mx * 4 * sizeof(unsigned long long)));
+        FramePtrs tp = fp;
+        tp.trace = dt;
+        FILE* fo = fopen(tf, "a");
+        std::vector<unsigned long long> h(mx * 4);
+        for (int s = 0; s < 3; ++s) {
+            HIPCHK(hipMemsetAsync(dt, 0, mx * 4 * sizeof(unsigned long long), L.stream));
+            HIPCHK(hipMemsetAsync(L.count, 0, sizeof(int), L.stream));
+            if (s == 0) HIPCHK(launch_k1(g, p->k, tp, nf, 3, g.C, L.stream));
+            if (s == 1) HIPCHK(launch_k2(g, p->k, tp, nf, g.B * g.P, L.stream));
+            if (s == 2) HIPCHK(launch_k3(g, p->k, tp, nf, L.stream));
+            HIPCHK(hipStreamSynchronize(L.stream));
+            HIPCHK(hipMemcpy(h.data(), dt, nwg[s] * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+            for (size_t w = 0; fo && w < nwg[s]; ++w)
+                fprintf(fo, "%s,%zu,%llu,%llu,%llu,%llu\n", kStageNames[s], w, h[4 * w], h[4 * w + 1], h[4 * w + 2],
+                        h[4 * w + 3]);
+        }
+        if (fo) fclose(fo);
+        (void)hipFree(dt);
+    }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
-    if (bytes_out) {   // algorithmic bytes per launch (one frame)
-        const int64_t cube = (int64_t)g.C * g.nU * g.P * 8, z = (int64_t)g.B * g.nU * g.P * 8;
-        const int64_t rdm = (int64_t)g.B * g.P * g.G * 8;
-        if (cap > 0) bytes_out[0] = cube + z;
-        if (cap > 1) bytes_out[1] = z + rdm;
-        if (cap > 2) bytes_out[2] = rdm;
+    if (bytes_out) {   // algorithmic bytes per launch (nf frames); DESIGN.md "Measurement"
+        const int64_t cube = (int64_t)g.C * g.nU * g.P * 8;        // used fast-time samples, complex64
+        const int64_t z = (int64_t)g.B * g.nU * g.P * 8;           // Doppler-domain rows
+        const int64_t rdm = (int64_t)g.B * g.P * g.G * 8;          // complex RD map
+        const int64_t mag = (int64_t)g.B * g.P * g.G * 4;          // |RD| map
+        if (cap > 0) bytes_out[0] = nf * (cube + z);
+        if (cap > 1) bytes_out[1] = nf * (z + rdm + mag);
+        if (cap > 2) bytes_out[2] = nf * mag;
     }
     return RSP_OK;
 }

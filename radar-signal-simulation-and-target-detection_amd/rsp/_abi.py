@@ -89,9 +89,11 @@ PROTOTYPES = {
                                      ct.POINTER(ct.c_int32), ct.POINTER(ct.c_int32)]),
     'rsp_results_clear': (ct.c_int32, [_P]),
     'rsp_process_stage2': (ct.c_int32, [_P, _P, ct.c_int32, _dp, _dp]),
-    'rsp_profile_stages': (ct.c_int32, [_P, _P, ct.c_int32, ct.POINTER(ct.c_float), ct.POINTER(ct.c_int64),
-                                        ct.c_int32]),
+    'rsp_profile_stages': (ct.c_int32, [_P, ct.POINTER(_P), ct.c_int32, ct.c_int32, ct.POINTER(ct.c_float),
+                                        ct.POINTER(ct.c_int64), ct.c_int32, ct.POINTER(ct.c_int32)]),
     'rsp_stage_name': (ct.c_char_p, [ct.c_int32]),
+    'rsp_cluster_detections': (ct.c_int32, [ct.POINTER(Detection), ct.c_int32, ct.POINTER(ClusterParams),
+                                            ct.POINTER(Target), ct.c_int32, ct.POINTER(ct.c_int32)]),
     'rsp_device_alloc': (ct.c_int32, [_P, ct.c_int64, ct.POINTER(_P)]),
     'rsp_device_free': (ct.c_int32, [_P, _P]),
     'rsp_device_upload': (ct.c_int32, [_P, _P, _P, ct.c_int64]),

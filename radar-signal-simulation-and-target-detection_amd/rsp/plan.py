@@ -211,9 +211,15 @@ class Plan:
             check(lib().rsp_results_clear(self.h))
         return out
 
-    def profile_stages(self, d_cube, iters=20):
+    def profile_stages(self, d_cubes, iters=20):
+        """Per-stage HIP-event timing; d_cubes = device pointer or list of pointers (batched)."""
+        if not isinstance(d_cubes, (list, tuple)):
+            d_cubes = [d_cubes]
         n = self.sizes.n_stages
         ms = (ct.c_float * n)()
         by = (ct.c_int64 * n)()
-        check(lib().rsp_profile_stages(self.h, ct.c_void_p(d_cube), int(iters), ms, by, n))
-        return [{'stage': lib().rsp_stage_name(i).decode(), 'ms': ms[i], 'bytes': by[i]} for i in range(n)]
+        arr = (ct.c_void_p * len(d_cubes))(*d_cubes)
+        nf = ct.c_int32()
+        check(lib().rsp_profile_stages(self.h, arr, len(d_cubes), int(iters), ms, by, n, ct.byref(nf)))
+        return [{'stage': lib().rsp_stage_name(i).decode(), 'ms': ms[i], 'bytes': by[i], 'frames': nf.value}
+                for i in range(n)]

@@ -98,3 +98,43 @@ def test_plan_without_gpu_fails_loudly():
     else:   # a GPU is present (GPU box): the plan must be real
         assert p.sizes.G == s['pre_p']['N_total_gate']
         p.close()
+
+
+def _host_cluster(dets, cp):
+    lib = _abi.lib()
+    arr = (_abi.Detection * max(len(dets), 1))()
+    for i, d in enumerate(dets):
+        arr[i] = _abi.Detection(d['v_idx'], d['r_idx'], d['pair_idx'], 0, d['Power'], d['Range'], d['Velocity'],
+                                d['Angle'])
+    out = (_abi.Target * 4096)()
+    n = ct.c_int32()
+    c = _abi.ClusterParams(cp['max_range_sep'], cp['max_vel_sep'], cp['max_angle_sep'])
+    _abi.check(lib.rsp_cluster_detections(arr, len(dets), ct.byref(c), out, 4096, ct.byref(n)))
+    return [dict(Range=out[i].Range, Velocity=out[i].Velocity, Angle=out[i].Angle, Power=out[i].Power)
+            for i in range(n.value)]
+
+
+@pytest.mark.parametrize('seed', range(6))
+def test_native_clustering_equals_oracle_bfs(seed):
+    """librsp's S10/S11 (union-find over a range sweep) == the oracle's literal BFS (fsf:302-407)."""
+    import numpy as np
+    from oracle import chain
+    from rsp import config as C
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(1, 400))
+    # clumpy detections: a few targets smeared over range/Doppler/pairs plus stragglers
+    dets = []
+    for i in range(n):
+        c = rng.integers(0, 6)
+        dets.append(dict(v_idx=int(rng.integers(16, 100)), r_idx=int(rng.integers(16, 2000)),
+                         pair_idx=int(rng.integers(1, 8)),
+                         Range=1000.0 * c + rng.normal(0, 25), Velocity=5.0 + 0.5 * c + rng.normal(0, 0.3),
+                         Angle=3.0 * c + rng.normal(0, 3), Power=float(rng.uniform(1, 100))))
+    cp = C.default_cluster_params()
+    got = _host_cluster(dets, cp)
+    order = sorted(range(n), key=lambda i: (dets[i]['pair_idx'], dets[i]['r_idx'], dets[i]['v_idx']))
+    want = chain.cluster_stage2(chain.cluster_stage1([dets[i] for i in order], cp), cp)
+    assert len(got) == len(want)
+    for a, b in zip(got, want):
+        for key in ('Range', 'Velocity', 'Angle', 'Power'):
+            assert a[key] == pytest.approx(b[key], rel=1e-12, abs=1e-9)

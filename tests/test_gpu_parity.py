@@ -187,7 +187,7 @@ def test_profile_stages_reports_three_kernels():
     plan = Plan(s['cfg'], s['cfar'], s['clus'], s['pre_p'])
     ptr = plan.device_alloc(plan.sizes.cube_elems * 8)
     plan.synthesize_device(ptr, targets_for('small'), 1)
-    st = plan.profile_stages(ptr, iters=3)
+    st = plan.profile_stages([ptr], iters=3)
     plan.device_free(ptr)
     plan.close()
     assert [x['stage'] for x in st] == ['k1_dbf_mtd', 'k2_pc', 'k3_cfar']

@@ -18,14 +18,19 @@ from rsp.plan import Plan  # noqa: E402
 def main():
     name = sys.argv[1] if len(sys.argv) > 1 else 'x2'
     iters = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    nf = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     cfg, cfar, clus, W, ang, k = C.named_config(name)
     pre = precompute(cfg, W, ang, k, C.V8_FIR)
-    plan = Plan(cfg, cfar, clus, pre)
-    p = plan.device_alloc(plan.sizes.cube_elems * 8)
-    plan.synthesize_device(p, C.v8_2_targets(), 1)
-    st = plan.profile_stages(p, iters=iters)
+    plan = Plan(cfg, cfar, clus, pre, frames_per_launch=nf)
+    cubes = [plan.device_alloc(plan.sizes.cube_elems * 8) for _ in range(nf)]
+    tg = C.v8_2_targets()
+    for i, p in enumerate(cubes):
+        plan.synthesize_device(p, tg, 1 + i)
+        tg = C.evolve_targets(tg, cfg)
+    st = plan.profile_stages(cubes, iters=iters)
     print(json.dumps(st))
-    plan.device_free(p)
+    for p in cubes:
+        plan.device_free(p)
     plan.close()
 
 
