@@ -9,11 +9,22 @@ is idle-fast.  With the gloo backend the same code runs on CPU tensors (tests).
 import numpy as np
 
 
+def shard_frames(n_frames, rank, world):
+    """Contiguous block of frame indices (1-based, as v8:164) owned by ``rank``:
+    frames are independent (v8:164-190), so each GPU takes n_frames/world of them."""
+    per, extra = divmod(n_frames, world)
+    lo = rank * per + min(rank, extra)
+    hi = lo + per + (1 if rank < extra else 0)
+    return list(range(lo + 1, hi + 1))
+
+
 def _pack(results):
     rows = []
     for r in results:
         for t in r['final_targets']:
             rows.append((r['frame_idx'], t['Range'], t['Velocity'], t['Angle'], t['Power']))
+        if not r['final_targets']:      # keep empty frames visible: one NaN marker row
+            rows.append((r['frame_idx'], np.nan, np.nan, np.nan, np.nan))
     return np.asarray(rows, np.float64).reshape(-1, 5)
 
 
@@ -41,7 +52,9 @@ def gather_targets(results, rank, world, device=None):
         rows = b[:c].cpu().numpy()
         frames = {}
         for f, R, V, A, P in rows:
-            frames.setdefault(int(f), []).append({'Range': R, 'Velocity': V, 'Angle': A, 'Power': P})
-        for f in sorted(frames):
+            lst = frames.setdefault(int(f), [])
+            if not np.isnan(R):
+                lst.append({'Range': R, 'Velocity': V, 'Angle': A, 'Power': P})
+        for f in frames:                 # insertion order = the rank's processing order
             out.append({'rank': r, 'frame_idx': f, 'final_targets': frames[f]})
     return out

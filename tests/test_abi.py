@@ -138,3 +138,39 @@ def test_native_clustering_equals_oracle_bfs(seed):
     for a, b in zip(got, want):
         for key in ('Range', 'Velocity', 'Angle', 'Power'):
             assert a[key] == pytest.approx(b[key], rel=1e-12, abs=1e-9)
+
+
+C_HOST = r'''
+#include <stdio.h>
+#include "rsp.h"
+int main(void) {
+    rsp_detection d[3] = {{10, 100, 1, 0, 5.0, 1000.0, 5.0, 1.0},
+                          {10, 101, 2, 0, 7.0, 1010.0, 5.1, 2.0},
+                          {40, 900, 1, 0, 3.0, 5000.0, -3.0, 0.5}};
+    rsp_cluster_params cp = {30.0, 0.4, 5.0};
+    rsp_target out[8];
+    int32_t n = -1;
+    rsp_plan* plan = 0;
+    if (rsp_abi_version() != RSP_ABI_VERSION) return 2;
+    if (rsp_plan_create(0, 0, 0, 0, 0, 1, &plan) != RSP_ERR_INVALID) return 3;
+    if (rsp_cluster_detections(d, 3, &cp, out, 8, &n) != RSP_OK) return 4;
+    printf("%d %.6f %.6f\n", n, out[0].Range, out[0].Power);
+    return 0;
+}
+'''
+
+
+def test_plain_c_host_links_and_calls():
+    """A plain C program (what a MEX gateway is) compiles against include/rsp.h, links
+    librsp.so and gets status codes + host-side S10/S11 results without a GPU."""
+    libdir = os.path.dirname(_abi.lib()._name)
+    with tempfile.TemporaryDirectory() as d:
+        src, exe = os.path.join(d, 'host.c'), os.path.join(d, 'host')
+        open(src, 'w').write(C_HOST)
+        subprocess.run(['gcc', '-std=c99', '-Wall', '-Werror', '-I', os.path.dirname(HEADER), src, '-o', exe,
+                        '-L', libdir, '-lrsp', '-Wl,-rpath,' + libdir], check=True)
+        out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout.split()
+    # stage 1 merges the two (power-weighted), stage 2 keeps both groups
+    assert int(out[0]) == 2
+    assert float(out[1]) == pytest.approx((5 * 1000.0 + 7 * 1010.0) / 12, abs=1e-6)
+    assert float(out[2]) == pytest.approx(12.0)

@@ -1,0 +1,90 @@
+"""Multi-process (gloo, world_size 2, CPU) test of the frame-sharded path.
+
+Each rank takes its contiguous shard of frames (rsp.dist.shard_frames), produces
+final_targets for them, and the detection lists are gathered with the same code the
+bench runs over RCCL (rsp.dist.gather_targets).  Without a GPU the per-frame work is
+done by the oracle; the thing under test is the sharding + gather, which must give
+every rank the single-process result for all frames, in frame order.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from rsp.dist import shard_frames
+
+N_FRAMES = 5
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _frame_results(frames):
+    """Per-frame final_targets of the 'small' scene (targets evolved per frame, v8:170-173) via the oracle."""
+    from oracle import chain
+    from _scen import scenario, targets_for, noisy_cube
+    from rsp import config as C
+    s = scenario('small')
+    tg = targets_for('small')
+    out = []
+    for f in range(1, max(frames) + 1 if frames else 1):
+        if f in frames:
+            cube = noisy_cube(s, tg, frame_idx=f)
+            fin = chain.process_cube(cube.astype(np.complex128), s['cfg'], s['cfar'], s['clus'], s['pre_o'])
+            out.append({'frame_idx': f, 'final_targets': fin})
+        tg = C.evolve_targets(tg, s['cfg'])
+    return out
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    from rsp.dist import gather_targets
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        mine = shard_frames(N_FRAMES, rank, world)
+        res = _frame_results(mine)
+        got = gather_targets(res, rank, world)
+        q.put((rank, [(g['rank'], g['frame_idx'], [(t['Range'], t['Velocity'], t['Angle'], t['Power'])
+                                                   for t in g['final_targets']]) for g in got]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_frames_partition():
+    for n in (0, 1, 5, 64, 512):
+        for w in (1, 2, 3, 8):
+            parts = [shard_frames(n, r, w) for r in range(w)]
+            assert sum(parts, []) == list(range(1, n + 1))
+            assert max(map(len, parts)) - min(map(len, parts)) <= 1
+
+
+def test_gather_two_ranks_equals_single_process():
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert outs[0] == outs[1]                       # every rank holds the same gathered list
+    want = _frame_results(list(range(1, N_FRAMES + 1)))
+    got = outs[0]
+    assert [f for _, f, _ in got] == list(range(1, N_FRAMES + 1))
+    assert [r for r, _, _ in got] == [0, 0, 0, 1, 1]
+    for (_, f, tl), w in zip(got, want):
+        assert len(tl) == len(w['final_targets'])
+        for t, u in zip(tl, w['final_targets']):
+            assert t == pytest.approx((u['Range'], u['Velocity'], u['Angle'], u['Power']), rel=1e-12)
+    assert sum(len(tl) for _, _, tl in got) > 0
