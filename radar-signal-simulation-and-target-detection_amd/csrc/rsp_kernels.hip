@@ -96,11 +96,7 @@ template <bool INV> struct Dft<16, INV> {
     }
 };
 
-template <int R> struct Log2R;
-template <> struct Log2R<2> { static constexpr int v = 1; };
-template <> struct Log2R<4> { static constexpr int v = 2; };
-template <> struct Log2R<8> { static constexpr int v = 3; };
-template <> struct Log2R<16> { static constexpr int v = 4; };
+constexpr int clog2(int x) { return x <= 1 ? 0 : 1 + clog2(x >> 1); }
 
 // LDS index inside a row: SH > 0 inserts one complex every 2^SH to break power-of-two
 // strides (tools/lds_conflicts.py models the gfx950 bank rules for each pass).
@@ -124,65 +120,30 @@ struct StoreLdsH {
     __device__ __forceinline__ void put(int idx, int, int, int loff, float2 x) const { buf[loff] = cmul(x, h[idx]); }
 };
 
-// One Stockham radix-R pass (Govindaraju et al. formulation) over `nrows` rows of
-// length L = 2^LGL held in LDS (row stride rs).  Ns = 2^LGNS = product of the earlier
-// radices.  Reads stride L/R, twiddle W_{Ns R}^{(j mod Ns) r} from this pass's table
-// tw[k][r-1] (LDS; built by build_pass_twiddles() in rsp_plan.cpp),
-// radix-R DFT, writes positions expand(j, Ns, R) + r Ns.  In place: all reads, barrier,
-// all writes, barrier.  Every size is a compile-time constant, so a pass is straight-line
-// code and no address math is carried across passes.
-template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, class St>
-__device__ __forceinline__ void sh_pass(float2* buf, int rs, int nrows, const float2* tw, const St& st) {
-    constexpr int lgR = Log2R<R>::v;
-    constexpr int lgnb = LGL - lgR;
-    constexpr int nb = 1 << lgnb;
-    constexpr int Ns = 1 << LGNS;
-    const int total = nb * nrows;
-    const int tid = threadIdx.x;
-    // With power-of-two nb, Ns and pads every 2^SH, lidx(j + r nb) = lidx(j) + r nb + ((r nb) >> SH)
-    // and lidx(idxD + r Ns) = lidx(idxD) + r Ns + ((r Ns) >> SH): every LDS address of a butterfly
-    // is a per-thread base plus a compile-time offset (ds_read/ds_write immediate offsets).
-    float2 v[NB][R];
+// Twiddles w[r] = W^r, r = 1..R-1, of one butterfly from its lgR table entries
+// W^(2^i) (per-pass table [k][i]); the others are products of at most lgR - 1 of them
+// (a 16-point butterfly reads 4 table entries instead of 15).
+template <int R, bool INV>
+__device__ __forceinline__ void expand_tw(const float2* twk, float2 (&w)[R]) {
+    constexpr int lgR = clog2(R);
+    float2 b[lgR];
 #pragma unroll
-    for (int t = 0; t < NB; ++t) {
-        const int beta = tid + t * NTHR;
-        if (beta < total) {
-            const int row = beta >> lgnb, j = beta & (nb - 1);
-            const int k = j & (Ns - 1);
-            const float2* src = buf + row * rs + lidx<SH>(j);
-            const float2* twk = tw + k * (R - 1) - 1;   // per-pass table [k][r-1]
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                float2 x = src[r * nb + (SH ? (r * nb) >> SH : 0)];
-                if (r > 0 && LGNS > 0) {
-                    float2 w = twk[r];
-                    if (INV) w.y = -w.y;
-                    x = cmul(x, w);
-                }
-                v[t][r] = x;
-            }
-        }
+    for (int i = 0; i < lgR; ++i) {
+        b[i] = twk[i];
+        if (INV) b[i].y = -b[i].y;
     }
-    __syncthreads();
+    w[0] = make_float2(1.f, 0.f);
 #pragma unroll
-    for (int t = 0; t < NB; ++t) {
-        const int beta = tid + t * NTHR;
-        if (beta < total) {
-            const int row = beta >> lgnb, j = beta & (nb - 1);
-            const int k = j & (Ns - 1);
-            Dft<R, INV>::run(v[t]);
-            const int idxD = ((j >> LGNS) << (LGNS + lgR)) + k;
-            const int wbase = row * rs + lidx<SH>(idxD);
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-                st.put(t * R + r, row, idxD + r * Ns, wbase + r * Ns + (SH ? (r * Ns) >> SH : 0), v[t][r]);
-        }
+    for (int r = 1; r < R; ++r) {
+        const int hb = 1 << clog2(r);
+        w[r] = (hb == r) ? b[clog2(r)] : cmul(w[hb], w[r - hb]);
     }
-    __syncthreads();
 }
 
 // Radix plan of a 2^m-point FFT: radix-16 passes, remainder as 8/4 (m = 5 -> 8 x 4);
-// must match radix_plan() in rsp_plan.cpp.
+// must match radix_plan() in rsp_plan.cpp.  REV = the same radices in reverse order (the
+// inverse FFT of the overlap-save block, so that its first pass consumes exactly the
+// elements the forward FFT's last pass leaves in each thread's registers).
 constexpr int rad_bits(int m, int q) {
     for (int i = 0; i < q; ++i) m -= (m == 5) ? 3 : (m >= 4 ? 4 : m);
     return (m == 5) ? 3 : (m >= 4 ? 4 : m);
@@ -195,37 +156,115 @@ constexpr int n_passes(int m) {
     }
     return n;
 }
+constexpr int rad_bits_p(int m, int q, bool rev) { return rev ? rad_bits(m, n_passes(m) - 1 - q) : rad_bits(m, q); }
 
 // Offset of pass q's twiddle table inside the concatenated per-pass tables of a 2^LG FFT:
-// pass i >= 1 owns Ns_i * (R_i - 1) entries (pass 0 has Ns = 1, no twiddles).
-constexpr int tw_pass_off(int LG, int q) {
+// pass i >= 1 owns Ns_i * log2(R_i) entries T[k][i'] = W_{Ns R}^{k 2^i'} (pass 0: Ns = 1,
+// no twiddles).  Must match build_pass_twiddles() in rsp_plan.cpp.
+constexpr int tw_pass_off(int LG, int q, bool rev = false) {
     int off = 0, lgns = 0;
     for (int i = 0; i < q; ++i) {
-        const int rb = rad_bits(LG, i);
-        if (i > 0) off += (1 << lgns) * ((1 << rb) - 1);
+        const int rb = rad_bits_p(LG, i, rev);
+        if (i > 0) off += (1 << lgns) * rb;
         lgns += rb;
     }
     return off;
 }
-constexpr int tw_total(int LG) { return tw_pass_off(LG, n_passes(LG)); }
+constexpr int tw_total(int LG, bool rev = false) { return tw_pass_off(LG, n_passes(LG), rev); }
 
-// All passes of a 2^LG-point FFT over `nrows` rows; the last pass stores through `last`.
-// PTS = complex points per thread (nrows * L / NTHR).
-template <int LG, int Q, int LGNS, int PTS, bool INV, int SH, int NTHR, class StMid, class StLast>
-__device__ __forceinline__ void fft_passes(float2* buf, int rs, int nrows, const float2* tw, const StMid& mid,
-                                           const StLast& last) {
+// One Stockham radix-R pass (Govindaraju et al. formulation) over `nrows` rows of
+// length L = 2^LGL held in LDS (row stride rs).  Ns = 2^LGNS = product of the earlier
+// radices.  Reads stride L/R, twiddle W_{Ns R}^{(j mod Ns) r} (from this pass's table),
+// radix-R DFT, writes positions expand(j, Ns, R) + r Ns.  In place: all reads, barrier,
+// all writes, barrier.  Every size is a compile-time constant, so a pass is straight-line
+// code and no address math is carried across passes.
+// With power-of-two nb, Ns and pads every 2^SH, lidx(j + r nb) = lidx(j) + r nb + ((r nb) >> SH)
+// and lidx(idxD + r Ns) = lidx(idxD) + r Ns + ((r Ns) >> SH): every LDS address of a butterfly
+// is a per-thread base plus a compile-time offset (ds_read/ds_write immediate offsets).
+template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS>
+__device__ __forceinline__ void sh_load(const float2* buf, int rs, int nrows, const float2* tw, float2 (&v)[NB][R]) {
+    constexpr int lgR = clog2(R);
+    constexpr int lgnb = LGL - lgR;
+    constexpr int nb = 1 << lgnb;
+    constexpr int Ns = 1 << LGNS;
+    const int total = nb * nrows;
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+        const int beta = threadIdx.x + t * NTHR;
+        if (beta < total) {
+            const int row = beta >> lgnb, j = beta & (nb - 1);
+            const int k = j & (Ns - 1);
+            const float2* src = buf + row * rs + lidx<SH>(j);
+            float2 w[R];
+            if (LGNS > 0) expand_tw<R, INV>(tw + k * lgR, w);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                float2 x = src[r * nb + (SH ? (r * nb) >> SH : 0)];
+                if (r > 0 && LGNS > 0) x = cmul(x, w[r]);
+                v[t][r] = x;
+            }
+        }
+    }
+}
+
+// Radix-R DFT of the loaded butterflies and the Stockham store (through policy st).
+template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, class St>
+__device__ __forceinline__ void sh_store(float2 (&v)[NB][R], int rs, int nrows, const St& st) {
+    constexpr int lgR = clog2(R);
+    constexpr int lgnb = LGL - lgR;
+    constexpr int nb = 1 << lgnb;
+    constexpr int Ns = 1 << LGNS;
+    const int total = nb * nrows;
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+        const int beta = threadIdx.x + t * NTHR;
+        if (beta < total) {
+            const int row = beta >> lgnb, j = beta & (nb - 1);
+            const int k = j & (Ns - 1);
+            Dft<R, INV>::run(v[t]);
+            const int idxD = ((j >> LGNS) << (LGNS + lgR)) + k;
+            const int wbase = row * rs + lidx<SH>(idxD);
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                st.put(t * R + r, row, idxD + r * Ns, wbase + r * Ns + (SH ? (r * Ns) >> SH : 0), v[t][r]);
+        }
+    }
+}
+
+template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, class St>
+__device__ __forceinline__ void sh_pass(float2* buf, int rs, int nrows, const float2* tw, const St& st) {
+    float2 v[NB][R];
+    sh_load<R, INV, NB, SH, NTHR, LGL, LGNS>(buf, rs, nrows, tw, v);
+    __syncthreads();
+    sh_store<R, INV, NB, SH, NTHR, LGL, LGNS>(v, rs, nrows, st);
+    __syncthreads();
+}
+
+// Passes Q..QEND-1 of a 2^LG-point FFT (radix order reversed if REV) over `nrows` rows;
+// pass n_passes - 1 stores through `last`, the others through `mid`.  tw = this plan's
+// concatenated tables.  PTS = complex points per thread (nrows * L / NTHR).
+template <int LG, int Q, int QEND, int LGNS, int PTS, bool INV, bool REV, int SH, int NTHR, class StMid, class StLast>
+__device__ __forceinline__ void fft_range(float2* buf, int rs, int nrows, const float2* tw, const StMid& mid,
+                                          const StLast& last) {
     constexpr int NP = n_passes(LG);
-    if constexpr (Q < NP) {
-        constexpr int RB = rad_bits(LG, Q);
+    if constexpr (Q < QEND) {
+        constexpr int RB = rad_bits_p(LG, Q, REV);
         constexpr int R = 1 << RB;
         constexpr int NB = (PTS + R - 1) / R;
-        const float2* twq = tw + tw_pass_off(LG, Q);
+        const float2* twq = tw + tw_pass_off(LG, Q, REV);
         if constexpr (Q == NP - 1)
             sh_pass<R, INV, NB, SH, NTHR, LG, LGNS>(buf, rs, nrows, twq, last);
         else
             sh_pass<R, INV, NB, SH, NTHR, LG, LGNS>(buf, rs, nrows, twq, mid);
-        fft_passes<LG, Q + 1, LGNS + RB, PTS, INV, SH, NTHR>(buf, rs, nrows, tw, mid, last);
+        fft_range<LG, Q + 1, QEND, LGNS + RB, PTS, INV, REV, SH, NTHR>(buf, rs, nrows, tw, mid, last);
     }
+}
+
+// All passes of a 2^LG-point FFT over `nrows` rows; the last pass stores through `last`.
+template <int LG, int Q, int LGNS, int PTS, bool INV, int SH, int NTHR, class StMid, class StLast>
+__device__ __forceinline__ void fft_passes(float2* buf, int rs, int nrows, const float2* tw, const StMid& mid,
+                                           const StLast& last) {
+    fft_range<LG, Q, n_passes(LG), LGNS, PTS, INV, false, SH, NTHR>(buf, rs, nrows, tw, mid, last);
 }
 
 __device__ __forceinline__ int ilog2(int x) { return 31 - __clz(x); }
@@ -276,6 +315,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
     const int f = blockIdx.y, tile = blockIdx.x;
     const int B = g.B, C = g.C, P = g.P, NT = g.NT, Ppad = g.Ppad;
     trace_stamp(fp, 0);
+    if (tile == 0 && threadIdx.x == 0 && fp.count[f]) *fp.count[f] = 0;   // K3's detection counter
     float2* twl = Y + B * NT * Ppad;
     const bool fft = (mode & 2) && g.pow2P;
     const int sh = fft ? K1_SH : 0;
@@ -477,10 +517,15 @@ struct StoreRdm {   // last inverse pass: keep outputs i in [Lh-1, Lh-1+V) that 
 
 #define K2_SH 5   // one pad complex per 32 (tools/lds_conflicts.py)
 #define K2_LDS_DATA (RSP_K2_POINTS + (RSP_K2_POINTS >> K2_SH))
-#define K2_LDS_TW 2048   // >= tw_total(log2 M) for M <= 2048
+#define K2_LDS_TW 1408   // >= tw_total(log2 M) + tw_total(log2 M, reversed) for M <= 2048
 #define K2_MAXM 2048
 
 // One overlap-save block of one FFT segment for RSP_K2_POINTS / 2^LGM adjacent rows.
+// LDS round trips: forward pass 0 runs on the samples as loaded from z; the forward FFT's
+// last pass, the filter-spectrum product and the inverse FFT's first pass (radices in
+// reverse order, so that pass has the same butterflies) run in registers back to back;
+// the inverse FFT's last pass stores the kept gates to HBM.  2 (log2 M / 4) round trips
+// instead of 2 (log2 M / 4) + 3.
 template <int LGM>
 __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k, const SegDesc& sd, const K2Job& job,
                                            const float2* __restrict__ z, float2* __restrict__ rdm,
@@ -490,8 +535,9 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     constexpr int rows = RSP_K2_POINTS / M;
     constexpr int rs = M + (M >> K2_SH);
     constexpr int NP = n_passes(LGM);
-    constexpr int RL = 1 << rad_bits(LGM, NP - 1);   // radix of the last forward pass
-    constexpr int NBL = 16 / RL;                     // its butterflies per thread
+    static_assert(NP >= 2, "overlap-save block needs >= 2 FFT passes");
+    constexpr int RB0 = rad_bits(LGM, 0), R0 = 1 << RB0, NB0 = 16 / R0, nb0 = M / R0;
+    constexpr int RBL = rad_bits(LGM, NP - 1), RL = 1 << RBL, NBL = 16 / RL;   // last forward pass
     const int P = g.P, G = g.G;
     const int lo = sd.lo, hi = sd.hi, off = sd.off;
     const int tid = threadIdx.x;
@@ -499,20 +545,21 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     const int g0 = sd.ga + job.blk * sd.V;
     const int a = sd.seg_lo + g0 - Lh1;           // sample index of u[0]
     float2* twl = L + K2_LDS_DATA;
-    // issue every global load of the workgroup before the first LDS store: 16 samples,
-    // the pass twiddles and this thread's 16 filter-spectrum values (kept in registers
-    // for the last forward pass) in flight together
-    float2 val[16];
+    // every global load of the workgroup in flight together: the 16 samples of this thread's
+    // pass-0 butterflies, its 16 filter-spectrum values (for the fused middle pass) and the
+    // twiddle tables
+    float2 v0[NB0][R0];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        const int e = tid + u * RSP_THREADS;
-        const int rl = e >> LGM, i = e & (M - 1);
+    for (int t = 0; t < NB0; ++t) {
+        const int beta = tid + t * RSP_THREADS;
+        const int rl = beta / nb0, j = beta & (nb0 - 1);
         const int rho = row0 + rl;
-        const int n = a + i;
-        val[u] = make_float2(0.f, 0.f);
-        if (rho < rows_total && n >= lo && n <= hi) {
-            const int b = rho / P, v = rho - b * P;
-            val[u] = z[zaddr(g, b, v, n - lo + off)];
+        const int b = rho / P, v = rho - b * P;
+#pragma unroll
+        for (int r = 0; r < R0; ++r) {
+            const int n = a + j + r * nb0;
+            v0[t][r] = make_float2(0.f, 0.f);
+            if (rho < rows_total && n >= lo && n <= hi) v0[t][r] = z[zaddr(g, b, v, n - lo + off)];
         }
     }
     float2 hreg[16];
@@ -522,7 +569,9 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
 #pragma unroll
         for (int r = 0; r < RL; ++r) hreg[t * RL + r] = k.H[sd.H_off + j + r * (M / RL)];
     }
-    constexpr int NTW = tw_total(LGM);
+    constexpr int NTWF = tw_total(LGM, false);
+    constexpr int NTW = NTWF + tw_total(LGM, true);
+    static_assert(NTW <= K2_LDS_TW, "K2 twiddle tables exceed their LDS slot");
     constexpr int NT_TAB = (NTW + RSP_THREADS - 1) / RSP_THREADS;
     float2 tv[NT_TAB];
 #pragma unroll
@@ -530,11 +579,8 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
         const int i = tid + u * RSP_THREADS;
         if (i < NTW) tv[u] = k.twM[sd.tw_off + i];
     }
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        const int e = tid + u * RSP_THREADS;
-        L[(e >> LGM) * rs + lidx<K2_SH>(e & (M - 1))] = val[u];
-    }
+    // forward pass 0 (Ns = 1, no twiddles) straight from the loaded samples
+    sh_store<R0, false, NB0, K2_SH, RSP_THREADS, LGM, 0>(v0, rs, rows, StoreLds{L});
 #pragma unroll
     for (int u = 0; u < NT_TAB; ++u) {
         const int i = tid + u * RSP_THREADS;
@@ -542,14 +588,29 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     }
     __syncthreads();
     trace_stamp(fp, 1);
-    // forward FFT; the last pass multiplies by the block filter spectrum H (1/M folded in)
-    fft_passes<LGM, 0, 0, 16, false, K2_SH, RSP_THREADS>(L, rs, rows, twl, StoreLds{L},
-                                                        StoreLdsH<16>{L, hreg});
+    // forward passes 1 .. NP-2
+    fft_range<LGM, 1, NP - 1, RB0, 16, false, false, K2_SH, RSP_THREADS>(L, rs, rows, twl, StoreLds{L},
+                                                                          StoreLds{L});
+    // fused: forward last pass, x H (1/M folded in), inverse pass 0 of the reversed plan
+    {
+        float2 v[NBL][RL];
+        sh_load<RL, false, NBL, K2_SH, RSP_THREADS, LGM, LGM - RBL>(L, rs, rows, twl + tw_pass_off(LGM, NP - 1), v);
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < NBL; ++t) {
+            Dft<RL, false>::run(v[t]);
+#pragma unroll
+            for (int r = 0; r < RL; ++r) v[t][r] = cmul(v[t][r], hreg[t * RL + r]);
+        }
+        sh_store<RL, true, NBL, K2_SH, RSP_THREADS, LGM, 0>(v, rs, rows, StoreLds{L});
+        __syncthreads();
+    }
     trace_stamp(fp, 2);
-    // inverse FFT; the last pass keeps the valid overlap-save outputs = stitched gates
+    // inverse passes 1 .. NP-1 (reversed radices); the last keeps the valid overlap-save
+    // outputs = stitched gates
     const int gend = min(sd.gb, g0 + sd.V);
-    fft_passes<LGM, 0, 0, 16, true, K2_SH, RSP_THREADS>(L, rs, rows, twl, StoreLds{L},
-                                                       StoreRdm{rdm, mag, G, g.Gp, row0, rows_total, Lh1, g0, gend});
+    fft_range<LGM, 1, NP, RBL, 16, true, true, K2_SH, RSP_THREADS>(
+        L, rs, rows, twl + NTWF, StoreLds{L}, StoreRdm{rdm, mag, G, g.Gp, row0, rows_total, Lh1, g0, gend});
     trace_stamp(fp, 3);
 }
 
@@ -734,7 +795,17 @@ __device__ __forceinline__ void s9_estimate(const DevConsts& k, const float* S, 
 template <int RR, int RV>
 __global__ __launch_bounds__(RSP_THREADS) void k3_cfar(Geometry g, DevConsts k, FramePtrs fp) {
     extern __shared__ __attribute__((aligned(16))) float S[];   // [P][W] | queue[K3_QCAP] | qn, base
-    const int f = blockIdx.z, pair = blockIdx.y, tile = blockIdx.x;
+    // XCD-aware order (bijective swizzle, cdna_hip_programming.md T1): the workgroups that
+    // share an XCD take consecutive (tile, pair) ids with pairs fastest, so beam b's tile --
+    // read by pairs b-1 and b -- and the range halos of neighbouring tiles are L2 hits
+    const int npair = g.B - 1, ntile = (g.G - 2 * (g.refR + g.guardR) + g.cfar_RT - 1) / g.cfar_RT;
+    int wg = blockIdx.x;
+    {
+        const int nwg = gridDim.x, xcd = wg & 7, q = nwg >> 3, rm = nwg & 7;
+        wg = (xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q) + (wg >> 3);
+    }
+    const int pair = wg % npair, col = wg / npair;
+    const int tile = col % ntile, f = col / ntile;
     const int P = g.P, G = g.G, W = g.cfar_W, hR = g.cfar_hR;
     const int rR = RR ? RR : g.refR, gR = g.guardR, rV = RV ? RV : g.refV, gV = g.guardV;
     const int r_begin = rR + gR + tile * g.cfar_RT;
@@ -1015,7 +1086,7 @@ hipError_t launch_k3(const Geometry& g, const DevConsts& k, const FramePtrs& fp,
     if (g.B < 2 || ncut_r <= 0) return hipSuccess;
     const int tiles = (ncut_r + g.cfar_RT - 1) / g.cfar_RT;
     const size_t lds = (size_t)g.P * g.cfar_W * sizeof(float) + (K3_QCAP + 4) * sizeof(int);
-    const dim3 grid(tiles, g.B - 1, nf);
+    const dim3 grid(tiles * (g.B - 1) * nf);   // 1-D; k3_cfar remaps it XCD-aware
     hipError_t e;
     if (g.refR == 5 && g.refV == 5) {   // the reference's cfar_params (v8:45-46)
         if ((e = allow_lds(k3_cfar<5, 5>, lds)) != hipSuccess) return e;

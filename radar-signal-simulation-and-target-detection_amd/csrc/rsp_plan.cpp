@@ -84,19 +84,21 @@ void radix_plan(int m, int* nrad, int* rad) {
     }
 }
 
-// Per-pass Stockham twiddle tables of a 2^m-point FFT, concatenated: pass q >= 1 owns
-// Ns_q x (R_q - 1) entries T[k][r-1] = exp(-2 pi i k r / (Ns_q R_q)) (must match
-// tw_pass_off() in rsp_kernels.hip).
-void build_pass_twiddles(int m, std::vector<float2>& out) {
+// Per-pass Stockham twiddle tables of a 2^m-point FFT (radix order reversed if rev),
+// concatenated: pass q >= 1 owns Ns_q x log2(R_q) entries T[k][i] = exp(-2 pi i k 2^i / (Ns_q R_q));
+// the kernels form the other powers by products (expand_tw, tw_pass_off in rsp_kernels.hip).
+void build_pass_twiddles(int m, std::vector<float2>& out, bool rev = false) {
     int nrad, rad[8];
     radix_plan(m, &nrad, rad);
+    if (rev) std::reverse(rad, rad + nrad);
     int Ns = 1;
     for (int q = 0; q < nrad; ++q) {
         const int R = rad[q];
+        const int lgR = ilog2i(R);
         if (q > 0)
             for (int k = 0; k < Ns; ++k)
-                for (int r = 1; r < R; ++r) {
-                    const double a = -2.0 * M_PI * (double)k * r / ((double)Ns * R);
+                for (int i = 0; i < lgR; ++i) {
+                    const double a = -2.0 * M_PI * (double)k * (1 << i) / ((double)Ns * R);
                     out.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
                 }
         Ns *= R;
@@ -111,10 +113,8 @@ struct Lane {
     float2* z = nullptr;        // F frames
     float2* rdm = nullptr;      // F frames
     float* mag = nullptr;       // F frames
-    DevDet* dets = nullptr;     // F x max_dets
-    int* count = nullptr;       // F
-    DevDet* h_dets = nullptr;   // pinned F x async_cap
-    int* h_count = nullptr;     // pinned F
+    DevDet* dets = nullptr;     // F x (1 + max_dets): record 0 of each frame holds its count
+    DevDet* h_dets = nullptr;   // pinned F x (1 + async_cap), same layout
     int nf = 0;
     int frame_ids[RSP_MAX_F];
     bool busy = false;
@@ -148,7 +148,7 @@ struct rsp_plan {
     float2* d_aux = nullptr;      // second map for the stage-2 path
     float2* h_stage = nullptr;    // pinned staging for uploads
     size_t h_stage_bytes = 0;
-    Lane lanes[2];
+    Lane lanes[RSP_LANES];
     int next_lane = 0;
     // pending batch of the queue
     const float2* pend_in[RSP_MAX_F];
@@ -181,7 +181,6 @@ rsp_plan::~rsp_plan() {
     for (auto& L : lanes) {
         if (L.stream) (void)hipStreamSynchronize(L.stream);
         if (L.h_dets) (void)hipHostFree(L.h_dets);
-        if (L.h_count) (void)hipHostFree(L.h_count);
         if (L.done) (void)hipEventDestroy(L.done);
         if (L.stream) (void)hipStreamDestroy(L.stream);
     }
@@ -324,7 +323,8 @@ int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga,
     if (ti < 0) {
         tw_sizes.push_back(M);
         tw_offs.push_back((int)twM.size());
-        build_pass_twiddles(s.logM, twM);
+        build_pass_twiddles(s.logM, twM, false);   // forward FFT
+        build_pass_twiddles(s.logM, twM, true);    // inverse FFT (reversed radices)
         ti = (int)tw_sizes.size() - 1;
     }
     s.tw_off = tw_offs[ti];
@@ -338,10 +338,8 @@ int setup_lane(rsp_plan* p, Lane& L) {
     if ((rc = p->dalloc(&L.z, p->z_elems * p->F))) return rc;
     if ((rc = p->dalloc(&L.rdm, p->rdm_elems * p->F))) return rc;
     if ((rc = p->dalloc(&L.mag, p->mag_elems * p->F))) return rc;
-    if ((rc = p->dalloc(&L.dets, (size_t)p->g.max_dets * p->F))) return rc;
-    if ((rc = p->dalloc(&L.count, (size_t)p->F))) return rc;
-    HIPCHK(hipHostMalloc((void**)&L.h_dets, sizeof(DevDet) * p->async_cap * p->F, hipHostMallocDefault));
-    HIPCHK(hipHostMalloc((void**)&L.h_count, sizeof(int) * p->F, hipHostMallocDefault));
+    if ((rc = p->dalloc(&L.dets, (size_t)(p->g.max_dets + 1) * p->F))) return rc;
+    HIPCHK(hipHostMalloc((void**)&L.h_dets, sizeof(DevDet) * (p->async_cap + 1) * p->F, hipHostMallocDefault));
     return RSP_OK;
 }
 
@@ -352,8 +350,9 @@ FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const float2* const* in, i
         fp.z[f] = L.z + p->z_elems * f;
         fp.rdm[f] = L.rdm + p->rdm_elems * f;
         fp.mag[f] = L.mag + p->mag_elems * f;
-        fp.dets[f] = L.dets + (size_t)p->g.max_dets * f;
-        fp.count[f] = L.count + f;
+        DevDet* rec = L.dets + (size_t)(p->g.max_dets + 1) * f;
+        fp.count[f] = reinterpret_cast<int*>(rec);   // zeroed by K1, bumped by K3
+        fp.dets[f] = rec + 1;
     }
     return fp;
 }
@@ -361,13 +360,13 @@ FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const float2* const* in, i
 // Enqueue K1 -> K2 -> K3 for nf frames on lane L, plus the async detection read-back.
 int launch_batch(rsp_plan* p, Lane& L, const float2* const* in, const int* ids, int nf) {
     const FramePtrs fp = lane_ptrs(p, L, in, nf);
-    HIPCHK(hipMemsetAsync(L.count, 0, sizeof(int) * nf, L.stream));
     HIPCHK(launch_k1(p->g, p->k, fp, nf, 3, p->g.C, L.stream));
     HIPCHK(launch_k2(p->g, p->k, fp, nf, p->g.B * p->g.P, L.stream));
     HIPCHK(launch_k3(p->g, p->k, fp, nf, L.stream));
-    HIPCHK(hipMemcpyAsync(L.h_count, L.count, sizeof(int) * nf, hipMemcpyDeviceToHost, L.stream));
-    HIPCHK(hipMemcpy2DAsync(L.h_dets, sizeof(DevDet) * p->async_cap, L.dets, sizeof(DevDet) * p->g.max_dets,
-                            sizeof(DevDet) * p->async_cap, nf, hipMemcpyDeviceToHost, L.stream));
+    // one copy: count record + the first async_cap detections of every frame
+    HIPCHK(hipMemcpy2DAsync(L.h_dets, sizeof(DevDet) * (p->async_cap + 1), L.dets,
+                            sizeof(DevDet) * (p->g.max_dets + 1), sizeof(DevDet) * (p->async_cap + 1), nf,
+                            hipMemcpyDeviceToHost, L.stream));
     HIPCHK(hipEventRecord(L.done, L.stream));
     L.nf = nf;
     for (int f = 0; f < nf; ++f) L.frame_ids[f] = ids[f];
@@ -382,7 +381,8 @@ int harvest(rsp_plan* p, Lane& L, std::vector<std::vector<rsp_detection>>* keep_
     L.busy = false;
     if (keep_dets) keep_dets->assign(L.nf, {});
     for (int f = 0; f < L.nf; ++f) {
-        const int cnt = L.h_count[f];
+        const DevDet* hrec = L.h_dets + (size_t)f * (p->async_cap + 1);
+        const int cnt = *reinterpret_cast<const int*>(hrec);
         FrameResult fr;
         fr.frame_idx = L.frame_ids[f];
         fr.overflow = cnt > p->g.max_dets;
@@ -391,10 +391,10 @@ int harvest(rsp_plan* p, Lane& L, std::vector<std::vector<rsp_detection>>* keep_
         std::vector<rsp_detection> dets(n);
         const int na = std::min(n, p->async_cap);
         static_assert(sizeof(DevDet) == sizeof(rsp_detection), "layout");
-        if (na) memcpy(dets.data(), L.h_dets + (size_t)f * p->async_cap, sizeof(DevDet) * na);
+        if (na) memcpy(dets.data(), hrec + 1, sizeof(DevDet) * na);
         if (n > na)
-            HIPCHK(hipMemcpy(dets.data() + na, L.dets + (size_t)p->g.max_dets * f + na, sizeof(DevDet) * (n - na),
-                             hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(dets.data() + na, L.dets + (size_t)(p->g.max_dets + 1) * f + 1 + na,
+                             sizeof(DevDet) * (n - na), hipMemcpyDeviceToHost));
         cluster_frame(p->cl, dets, fr.targets);
         if (fr.overflow) p->overflow_seen = true;
         if (keep_dets) (*keep_dets)[f] = dets;
@@ -410,7 +410,7 @@ int flush_pending(rsp_plan* p) {
     if (rc) return rc;
     rc = launch_batch(p, L, p->pend_in, p->pend_ids, p->npend);
     p->npend = 0;
-    p->next_lane ^= 1;
+    p->next_lane = (p->next_lane + 1) % RSP_LANES;
     return rc;
 }
 
@@ -418,8 +418,8 @@ int drain_all(rsp_plan* p) {
     int rc = flush_pending(p);
     if (rc) return rc;
     // harvest in launch order: the lane launched first is next_lane
-    for (int q = 0; q < 2; ++q) {
-        rc = harvest(p, p->lanes[(p->next_lane + q) & 1]);
+    for (int q = 0; q < RSP_LANES; ++q) {
+        rc = harvest(p, p->lanes[(p->next_lane + q) % RSP_LANES]);
         if (rc) return rc;
     }
     return RSP_OK;
@@ -903,7 +903,8 @@ int32_t rsp_profile_stages(rsp_plan* p, const void* const* d_cubes, int32_t n_cu
         auto run = [&]() -> hipError_t {
             if (s == 0) return launch_k1(g, p->k, fp, nf, 3, g.C, L.stream);
             if (s == 1) return launch_k2(g, p->k, fp, nf, g.B * g.P, L.stream);
-            hipError_t e = hipMemsetAsync(L.count, 0, sizeof(int) * nf, L.stream);
+            // counts are zeroed by K1 in the pipeline; here by a tiny 2-D memset per launch
+            hipError_t e = hipMemset2DAsync(L.dets, sizeof(DevDet) * (g.max_dets + 1), 0, sizeof(int), nf, L.stream);
             return e != hipSuccess ? e : launch_k3(g, p->k, fp, nf, L.stream);
         };
         HIPCHK(run());
@@ -928,7 +929,7 @@ int32_t rsp_profile_stages(rsp_plan* p, const void* const* d_cubes, int32_t n_cu
         std::vector<unsigned long long> h(mx * 4);
         for (int s = 0; s < 3; ++s) {
             HIPCHK(hipMemsetAsync(dt, 0, mx * 4 * sizeof(unsigned long long), L.stream));
-            HIPCHK(hipMemsetAsync(L.count, 0, sizeof(int), L.stream));
+            HIPCHK(hipMemset2DAsync(L.dets, sizeof(DevDet) * (g.max_dets + 1), 0, sizeof(int), nf, L.stream));
             if (s == 0) HIPCHK(launch_k1(g, p->k, tp, nf, 3, g.C, L.stream));
             if (s == 1) HIPCHK(launch_k2(g, p->k, tp, nf, g.B * g.P, L.stream));
             if (s == 2) HIPCHK(launch_k3(g, p->k, tp, nf, L.stream));
