@@ -25,54 +25,61 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
 }
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+
+// ---- complex values as 2-wide float vectors ---------------------------------------------
+// The FFT core keeps every complex value in one ext_vector pair, so complex adds are single
+// v_pk_add_f32 and complex products two packed ops, without the register shuffles the
+// compiler's SLP packing of struct float2 code produces.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 tof2(float2 a) { return f2{a.x, a.y}; }
+__device__ __forceinline__ float2 fromf2(f2 a) { return make_float2(a.x, a.y); }
+__device__ __forceinline__ f2 vmul(f2 a, f2 b) { return a.xx * b + a.yy * f2{-b.y, b.x}; }
 template <bool INV>
-__device__ __forceinline__ float2 rot_mi(float2 a) {   // * (-i) forward, * (+i) inverse
-    return INV ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x);
+__device__ __forceinline__ f2 vrot(f2 a) {   // * (-i) forward, * (+i) inverse
+    return INV ? a.yx * f2{-1.f, 1.f} : a.yx * f2{1.f, -1.f};
 }
 template <bool INV>
-__device__ __forceinline__ float2 twc(float c, float s) {  // exp(-+ i theta) with (c, s) = (cos, sin)
-    return make_float2(c, INV ? s : -s);
-}
+__device__ __forceinline__ f2 vtw(float c, float s) { return f2{c, INV ? s : -s}; }   // exp(-+ i theta)
 
 // ---- radix-R DFT kernels in registers -------------------------------------------------
 template <int R, bool INV> struct Dft;
 template <bool INV> struct Dft<2, INV> {
-    static __device__ __forceinline__ void run(float2* a) {
-        float2 t = a[0];
-        a[0] = cadd(t, a[1]);
-        a[1] = csub(t, a[1]);
+    static __device__ __forceinline__ void run(f2* a) {
+        const f2 t = a[0];
+        a[0] = t + a[1];
+        a[1] = t - a[1];
     }
 };
 template <bool INV> struct Dft<4, INV> {
-    static __device__ __forceinline__ void run(float2* a) {
-        float2 t0 = cadd(a[0], a[2]), t1 = csub(a[0], a[2]);
-        float2 t2 = cadd(a[1], a[3]), t3 = rot_mi<INV>(csub(a[1], a[3]));
-        a[0] = cadd(t0, t2);
-        a[2] = csub(t0, t2);
-        a[1] = cadd(t1, t3);
-        a[3] = csub(t1, t3);
+    static __device__ __forceinline__ void run(f2* a) {
+        const f2 t0 = a[0] + a[2], t1 = a[0] - a[2];
+        const f2 t2 = a[1] + a[3], t3 = vrot<INV>(a[1] - a[3]);
+        a[0] = t0 + t2;
+        a[2] = t0 - t2;
+        a[1] = t1 + t3;
+        a[3] = t1 - t3;
     }
 };
 template <bool INV> struct Dft<8, INV> {
-    static __device__ __forceinline__ void run(float2* a) {
-        float2 e[4] = {a[0], a[2], a[4], a[6]};
-        float2 o[4] = {a[1], a[3], a[5], a[7]};
+    static __device__ __forceinline__ void run(f2* a) {
+        f2 e[4] = {a[0], a[2], a[4], a[6]};
+        f2 o[4] = {a[1], a[3], a[5], a[7]};
         Dft<4, INV>::run(e);
         Dft<4, INV>::run(o);
         const float r = 0.70710678118654752f;
-        o[1] = cmul(o[1], twc<INV>(r, r));
-        o[2] = rot_mi<INV>(o[2]);
-        o[3] = cmul(o[3], twc<INV>(-r, r));
+        o[1] = vmul(o[1], vtw<INV>(r, r));
+        o[2] = vrot<INV>(o[2]);
+        o[3] = vmul(o[3], vtw<INV>(-r, r));
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            a[k] = cadd(e[k], o[k]);
-            a[k + 4] = csub(e[k], o[k]);
+            a[k] = e[k] + o[k];
+            a[k + 4] = e[k] - o[k];
         }
     }
 };
 template <bool INV> struct Dft<16, INV> {
-    static __device__ __forceinline__ void run(float2* a) {
-        float2 e[8], o[8];
+    static __device__ __forceinline__ void run(f2* a) {
+        f2 e[8], o[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             e[k] = a[2 * k];
@@ -81,17 +88,17 @@ template <bool INV> struct Dft<16, INV> {
         Dft<8, INV>::run(e);
         Dft<8, INV>::run(o);
         const float c1 = 0.92387953251128674f, s1 = 0.38268343236508977f, r = 0.70710678118654752f;
-        o[1] = cmul(o[1], twc<INV>(c1, s1));
-        o[2] = cmul(o[2], twc<INV>(r, r));
-        o[3] = cmul(o[3], twc<INV>(s1, c1));
-        o[4] = rot_mi<INV>(o[4]);
-        o[5] = cmul(o[5], twc<INV>(-s1, c1));
-        o[6] = cmul(o[6], twc<INV>(-r, r));
-        o[7] = cmul(o[7], twc<INV>(-c1, s1));
+        o[1] = vmul(o[1], vtw<INV>(c1, s1));
+        o[2] = vmul(o[2], vtw<INV>(r, r));
+        o[3] = vmul(o[3], vtw<INV>(s1, c1));
+        o[4] = vrot<INV>(o[4]);
+        o[5] = vmul(o[5], vtw<INV>(-s1, c1));
+        o[6] = vmul(o[6], vtw<INV>(-r, r));
+        o[7] = vmul(o[7], vtw<INV>(-c1, s1));
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            a[k] = cadd(e[k], o[k]);
-            a[k + 8] = csub(e[k], o[k]);
+            a[k] = e[k] + o[k];
+            a[k + 8] = e[k] - o[k];
         }
     }
 };
@@ -108,7 +115,7 @@ __device__ __forceinline__ int lidx(int i) { return SH ? i + (i >> SH) : i; }
 // o, and the padded LDS offset loff of (row, o).
 struct StoreLds {
     float2* buf;
-    __device__ __forceinline__ void put(int, int, int, int loff, float2 x) const { buf[loff] = x; }
+    __device__ __forceinline__ void put(int, int, int, int loff, f2 x) const { buf[loff] = fromf2(x); }
 };
 
 // Last forward pass of the overlap-save FFT: multiply by the block filter spectrum H (1/M
@@ -116,29 +123,38 @@ struct StoreLds {
 template <int NH>
 struct StoreLdsH {
     float2* buf;
-    const float2 (&h)[NH];
-    __device__ __forceinline__ void put(int idx, int, int, int loff, float2 x) const { buf[loff] = cmul(x, h[idx]); }
+    const f2 (&h)[NH];
+    __device__ __forceinline__ void put(int idx, int, int, int loff, f2 x) const { buf[loff] = fromf2(vmul(x, h[idx])); }
 };
 
-// Twiddles w[r] = W^r, r = 1..R-1, of one butterfly from its lgR table entries
-// W^(2^i) (per-pass table [k][i]); the others are products of at most lgR - 1 of them
-// (a 16-point butterfly reads 4 table entries instead of 15).
-template <int R, bool INV>
-__device__ __forceinline__ void expand_tw(const float2* twk, float2 (&w)[R]) {
-    constexpr int lgR = clog2(R);
-    float2 b[lgR];
+// Twiddles w[r] = W_{Ns R}^{k r}, r = 1..R-1, of one butterfly (conjugated for the inverse)
+// from this pass's table row k: CMP = false: full rows [k][r-1] (R-1 loads); CMP = true:
+// compact rows [k][i] = W^(k 2^i) (lgR loads), the other powers formed as products of at
+// most lgR - 1 of them.
+template <int R, bool INV, bool CMP>
+__device__ __forceinline__ void load_tw(const float2* twk, f2 (&w)[R]) {
+    if constexpr (!CMP) {
 #pragma unroll
-    for (int i = 0; i < lgR; ++i) {
-        b[i] = twk[i];
-        if (INV) b[i].y = -b[i].y;
-    }
-    w[0] = make_float2(1.f, 0.f);
+        for (int r = 1; r < R; ++r) {
+            const float2 t = twk[r - 1];
+            w[r] = f2{t.x, INV ? -t.y : t.y};
+        }
+    } else {
+        constexpr int lgR = clog2(R);
+        f2 b[lgR];
 #pragma unroll
-    for (int r = 1; r < R; ++r) {
-        const int hb = 1 << clog2(r);
-        w[r] = (hb == r) ? b[clog2(r)] : cmul(w[hb], w[r - hb]);
+        for (int i = 0; i < lgR; ++i) {
+            const float2 t = twk[i];
+            b[i] = f2{t.x, INV ? -t.y : t.y};
+        }
+#pragma unroll
+        for (int r = 1; r < R; ++r) {
+            const int hb = 1 << clog2(r);
+            w[r] = (hb == r) ? b[clog2(r)] : vmul(w[hb], w[r - hb]);
+        }
     }
 }
+constexpr int tw_row(int R, bool cmp) { return cmp ? clog2(R) : R - 1; }
 
 // Radix plan of a 2^m-point FFT: radix-16 passes, remainder as 8/4 (m = 5 -> 8 x 4);
 // must match radix_plan() in rsp_plan.cpp.  REV = the same radices in reverse order (the
@@ -159,18 +175,18 @@ constexpr int n_passes(int m) {
 constexpr int rad_bits_p(int m, int q, bool rev) { return rev ? rad_bits(m, n_passes(m) - 1 - q) : rad_bits(m, q); }
 
 // Offset of pass q's twiddle table inside the concatenated per-pass tables of a 2^LG FFT:
-// pass i >= 1 owns Ns_i * log2(R_i) entries T[k][i'] = W_{Ns R}^{k 2^i'} (pass 0: Ns = 1,
-// no twiddles).  Must match build_pass_twiddles() in rsp_plan.cpp.
-constexpr int tw_pass_off(int LG, int q, bool rev = false) {
+// pass i >= 1 owns Ns_i rows of tw_row(R_i) entries (pass 0: Ns = 1, no twiddles).  Must
+// match build_pass_twiddles() in rsp_plan.cpp.
+constexpr int tw_pass_off(int LG, int q, bool rev = false, bool cmp = false) {
     int off = 0, lgns = 0;
     for (int i = 0; i < q; ++i) {
         const int rb = rad_bits_p(LG, i, rev);
-        if (i > 0) off += (1 << lgns) * rb;
+        if (i > 0) off += (1 << lgns) * tw_row(1 << rb, cmp);
         lgns += rb;
     }
     return off;
 }
-constexpr int tw_total(int LG, bool rev = false) { return tw_pass_off(LG, n_passes(LG), rev); }
+constexpr int tw_total(int LG, bool rev = false, bool cmp = false) { return tw_pass_off(LG, n_passes(LG), rev, cmp); }
 
 // One Stockham radix-R pass (Govindaraju et al. formulation) over `nrows` rows of
 // length L = 2^LGL held in LDS (row stride rs).  Ns = 2^LGNS = product of the earlier
@@ -181,8 +197,8 @@ constexpr int tw_total(int LG, bool rev = false) { return tw_pass_off(LG, n_pass
 // With power-of-two nb, Ns and pads every 2^SH, lidx(j + r nb) = lidx(j) + r nb + ((r nb) >> SH)
 // and lidx(idxD + r Ns) = lidx(idxD) + r Ns + ((r Ns) >> SH): every LDS address of a butterfly
 // is a per-thread base plus a compile-time offset (ds_read/ds_write immediate offsets).
-template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS>
-__device__ __forceinline__ void sh_load(const float2* buf, int rs, int nrows, const float2* tw, float2 (&v)[NB][R]) {
+template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP = false>
+__device__ __forceinline__ void sh_load(const float2* buf, int rs, int nrows, const float2* tw, f2 (&v)[NB][R]) {
     constexpr int lgR = clog2(R);
     constexpr int lgnb = LGL - lgR;
     constexpr int nb = 1 << lgnb;
@@ -195,12 +211,12 @@ __device__ __forceinline__ void sh_load(const float2* buf, int rs, int nrows, co
             const int row = beta >> lgnb, j = beta & (nb - 1);
             const int k = j & (Ns - 1);
             const float2* src = buf + row * rs + lidx<SH>(j);
-            float2 w[R];
-            if (LGNS > 0) expand_tw<R, INV>(tw + k * lgR, w);
+            f2 w[R];
+            if (LGNS > 0) load_tw<R, INV, CMP>(tw + k * tw_row(R, CMP), w);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                float2 x = src[r * nb + (SH ? (r * nb) >> SH : 0)];
-                if (r > 0 && LGNS > 0) x = cmul(x, w[r]);
+                f2 x = tof2(src[r * nb + (SH ? (r * nb) >> SH : 0)]);
+                if (r > 0 && LGNS > 0) x = vmul(x, w[r]);
                 v[t][r] = x;
             }
         }
@@ -209,7 +225,7 @@ __device__ __forceinline__ void sh_load(const float2* buf, int rs, int nrows, co
 
 // Radix-R DFT of the loaded butterflies and the Stockham store (through policy st).
 template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, class St>
-__device__ __forceinline__ void sh_store(float2 (&v)[NB][R], int rs, int nrows, const St& st) {
+__device__ __forceinline__ void sh_store(f2 (&v)[NB][R], int rs, int nrows, const St& st) {
     constexpr int lgR = clog2(R);
     constexpr int lgnb = LGL - lgR;
     constexpr int nb = 1 << lgnb;
@@ -231,10 +247,10 @@ __device__ __forceinline__ void sh_store(float2 (&v)[NB][R], int rs, int nrows, 
     }
 }
 
-template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, class St>
+template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP, class St>
 __device__ __forceinline__ void sh_pass(float2* buf, int rs, int nrows, const float2* tw, const St& st) {
-    float2 v[NB][R];
-    sh_load<R, INV, NB, SH, NTHR, LGL, LGNS>(buf, rs, nrows, tw, v);
+    f2 v[NB][R];
+    sh_load<R, INV, NB, SH, NTHR, LGL, LGNS, CMP>(buf, rs, nrows, tw, v);
     __syncthreads();
     sh_store<R, INV, NB, SH, NTHR, LGL, LGNS>(v, rs, nrows, st);
     __syncthreads();
@@ -243,7 +259,8 @@ __device__ __forceinline__ void sh_pass(float2* buf, int rs, int nrows, const fl
 // Passes Q..QEND-1 of a 2^LG-point FFT (radix order reversed if REV) over `nrows` rows;
 // pass n_passes - 1 stores through `last`, the others through `mid`.  tw = this plan's
 // concatenated tables.  PTS = complex points per thread (nrows * L / NTHR).
-template <int LG, int Q, int QEND, int LGNS, int PTS, bool INV, bool REV, int SH, int NTHR, class StMid, class StLast>
+template <int LG, int Q, int QEND, int LGNS, int PTS, bool INV, bool REV, int SH, int NTHR, bool CMP, class StMid,
+          class StLast>
 __device__ __forceinline__ void fft_range(float2* buf, int rs, int nrows, const float2* tw, const StMid& mid,
                                           const StLast& last) {
     constexpr int NP = n_passes(LG);
@@ -251,12 +268,12 @@ __device__ __forceinline__ void fft_range(float2* buf, int rs, int nrows, const 
         constexpr int RB = rad_bits_p(LG, Q, REV);
         constexpr int R = 1 << RB;
         constexpr int NB = (PTS + R - 1) / R;
-        const float2* twq = tw + tw_pass_off(LG, Q, REV);
+        const float2* twq = tw + tw_pass_off(LG, Q, REV, CMP);
         if constexpr (Q == NP - 1)
-            sh_pass<R, INV, NB, SH, NTHR, LG, LGNS>(buf, rs, nrows, twq, last);
+            sh_pass<R, INV, NB, SH, NTHR, LG, LGNS, CMP>(buf, rs, nrows, twq, last);
         else
-            sh_pass<R, INV, NB, SH, NTHR, LG, LGNS>(buf, rs, nrows, twq, mid);
-        fft_range<LG, Q + 1, QEND, LGNS + RB, PTS, INV, REV, SH, NTHR>(buf, rs, nrows, tw, mid, last);
+            sh_pass<R, INV, NB, SH, NTHR, LG, LGNS, CMP>(buf, rs, nrows, twq, mid);
+        fft_range<LG, Q + 1, QEND, LGNS + RB, PTS, INV, REV, SH, NTHR, CMP>(buf, rs, nrows, tw, mid, last);
     }
 }
 
@@ -264,7 +281,7 @@ __device__ __forceinline__ void fft_range(float2* buf, int rs, int nrows, const 
 template <int LG, int Q, int LGNS, int PTS, bool INV, int SH, int NTHR, class StMid, class StLast>
 __device__ __forceinline__ void fft_passes(float2* buf, int rs, int nrows, const float2* tw, const StMid& mid,
                                            const StLast& last) {
-    fft_range<LG, Q, n_passes(LG), LGNS, PTS, INV, false, SH, NTHR>(buf, rs, nrows, tw, mid, last);
+    fft_range<LG, Q, n_passes(LG), LGNS, PTS, INV, false, SH, NTHR, false>(buf, rs, nrows, tw, mid, last);
 }
 
 __device__ __forceinline__ int ilog2(int x) { return 31 - __clz(x); }
@@ -505,19 +522,20 @@ __device__ __forceinline__ float cabsf(float2 a) { return sqrtf(a.x * a.x + a.y 
 struct StoreRdm {   // last inverse pass: keep outputs i in [Lh-1, Lh-1+V) that map to gates < gend;
                     // also writes |x| (the CFAR input, fsf:184-185) into the magnitude map
     float2* rdm; float* mag; int G; int Gp; int row0; int rows_total; int Lh1; int g0; int gend;
-    __device__ __forceinline__ void put(int, int row, int o, int, float2 x) const {
+    __device__ __forceinline__ void put(int, int row, int o, int, f2 x) const {
         const int gg = g0 + o - Lh1;
         const int rho = row0 + row;
-        if (o >= Lh1 && gg < gend && rho < rows_total) {
-            rdm[(size_t)rho * G + gg] = x;
-            mag[(size_t)rho * Gp + gg] = cabsf(x);
+        if (o >= Lh1 && gg < gend && rho < rows_total) {   // 32-bit offsets: saddr + voffset stores
+            rdm[(unsigned)(rho * G + gg)] = fromf2(x);
+            mag[(unsigned)(rho * Gp + gg)] = sqrtf(x.x * x.x + x.y * x.y);
         }
     }
 };
 
 #define K2_SH 5   // one pad complex per 32 (tools/lds_conflicts.py)
 #define K2_LDS_DATA (RSP_K2_POINTS + (RSP_K2_POINTS >> K2_SH))
-#define K2_LDS_TW 1408   // >= tw_total(log2 M) + tw_total(log2 M, reversed) for M <= 2048
+#define K2_LDS_TW 4096       // >= tw_total(log2 M) + tw_total(log2 M, reversed) for M <= 2048
+#define K2_LDS_TW_CMP 1408   // the same for compact tables
 #define K2_MAXM 2048
 
 // One overlap-save block of one FFT segment for RSP_K2_POINTS / 2^LGM adjacent rows.
@@ -526,7 +544,7 @@ struct StoreRdm {   // last inverse pass: keep outputs i in [Lh-1, Lh-1+V) that 
 // reverse order, so that pass has the same butterflies) run in registers back to back;
 // the inverse FFT's last pass stores the kept gates to HBM.  2 (log2 M / 4) round trips
 // instead of 2 (log2 M / 4) + 3.
-template <int LGM>
+template <int LGM, bool TWG, bool CMP>
 __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k, const SegDesc& sd, const K2Job& job,
                                            const float2* __restrict__ z, float2* __restrict__ rdm,
                                            float* __restrict__ mag, int row0, int rows_total, float2* L,
@@ -544,36 +562,57 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     const int Lh1 = sd.Lh - 1;
     const int g0 = sd.ga + job.blk * sd.V;
     const int a = sd.seg_lo + g0 - Lh1;           // sample index of u[0]
-    float2* twl = L + K2_LDS_DATA;
+    // twiddle tables: LDS copy, or (TWG) read in place from global memory (L1/L2 resident)
+    float2* twl = TWG ? const_cast<float2*>(k.twM + sd.tw_off) : L + K2_LDS_DATA;
     // every global load of the workgroup in flight together: the 16 samples of this thread's
     // pass-0 butterflies, its 16 filter-spectrum values (for the fused middle pass) and the
     // twiddle tables
-    float2 v0[NB0][R0];
+    f2 v0[NB0][R0];
+    const int lgNT = ilog2(g.NT);
 #pragma unroll
     for (int t = 0; t < NB0; ++t) {
         const int beta = tid + t * RSP_THREADS;
         const int rl = beta / nb0, j = beta & (nb0 - 1);
         const int rho = row0 + rl;
         const int b = rho / P, v = rho - b * P;
+        // z index of sample n0 + r nb0: when NT | nb0 the tile advances by nb0/NT per r and the
+        // in-tile slot is fixed, so element r sits at zb + r (nb0 P) (one multiply per thread)
+        const int np0 = a + j - lo + off;
+        const int zb = ((b * g.ntiles + (np0 >> lgNT)) * P + v) * g.NT + (np0 & (g.NT - 1));
+        // branch-free: every lane loads (a valid address when masked) and selects
+        if ((nb0 & (g.NT - 1)) == 0) {   // uniform
 #pragma unroll
-        for (int r = 0; r < R0; ++r) {
-            const int n = a + j + r * nb0;
-            v0[t][r] = make_float2(0.f, 0.f);
-            if (rho < rows_total && n >= lo && n <= hi) v0[t][r] = z[zaddr(g, b, v, n - lo + off)];
+            for (int r = 0; r < R0; ++r) {
+                const int n = a + j + r * nb0;
+                const bool ok = rho < rows_total && n >= lo && n <= hi;
+                const f2 x = tof2(z[ok ? (unsigned)(zb + r * nb0 * P) : 0u]);
+                v0[t][r] = ok ? x : f2{0.f, 0.f};
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < R0; ++r) {
+                const int n = a + j + r * nb0;
+                const bool ok = rho < rows_total && n >= lo && n <= hi;
+                const f2 x = tof2(z[ok ? (unsigned)zaddr(g, b, v, n - lo + off) : 0u]);
+                v0[t][r] = ok ? x : f2{0.f, 0.f};
+            }
         }
     }
-    float2 hreg[16];
+    // H for the last forward pass's outputs j + r M/RL; butterflies t and t + (M/RL)/NTHR of a
+    // thread have the same j (different rows), so only the distinct ones are loaded
+    constexpr int NHT = (M / RL) / RSP_THREADS >= NBL ? NBL : ((M / RL) / RSP_THREADS > 0 ? (M / RL) / RSP_THREADS : 1);
+    f2 hreg[NHT * RL];
 #pragma unroll
-    for (int t = 0; t < NBL; ++t) {
+    for (int t = 0; t < NHT; ++t) {
         const int j = (tid + t * RSP_THREADS) & (M / RL - 1);   // last pass: Ns = nb = M / RL, idxD = j
 #pragma unroll
-        for (int r = 0; r < RL; ++r) hreg[t * RL + r] = k.H[sd.H_off + j + r * (M / RL)];
+        for (int r = 0; r < RL; ++r) hreg[t * RL + r] = tof2(k.H[sd.H_off + j + r * (M / RL)]);
     }
-    constexpr int NTWF = tw_total(LGM, false);
-    constexpr int NTW = NTWF + tw_total(LGM, true);
-    static_assert(NTW <= K2_LDS_TW, "K2 twiddle tables exceed their LDS slot");
-    constexpr int NT_TAB = (NTW + RSP_THREADS - 1) / RSP_THREADS;
-    float2 tv[NT_TAB];
+    constexpr int NTWF = tw_total(LGM, false, CMP);
+    constexpr int NTW = NTWF + tw_total(LGM, true, CMP);
+    static_assert(NTW <= (CMP ? K2_LDS_TW_CMP : K2_LDS_TW), "K2 twiddle tables exceed their LDS slot");
+    constexpr int NT_TAB = TWG ? 0 : (NTW + RSP_THREADS - 1) / RSP_THREADS;
+    float2 tv[NT_TAB > 0 ? NT_TAB : 1];
 #pragma unroll
     for (int u = 0; u < NT_TAB; ++u) {
         const int i = tid + u * RSP_THREADS;
@@ -589,18 +628,19 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     __syncthreads();
     trace_stamp(fp, 1);
     // forward passes 1 .. NP-2
-    fft_range<LGM, 1, NP - 1, RB0, 16, false, false, K2_SH, RSP_THREADS>(L, rs, rows, twl, StoreLds{L},
-                                                                          StoreLds{L});
+    fft_range<LGM, 1, NP - 1, RB0, 16, false, false, K2_SH, RSP_THREADS, CMP>(L, rs, rows, twl, StoreLds{L},
+                                                                               StoreLds{L});
     // fused: forward last pass, x H (1/M folded in), inverse pass 0 of the reversed plan
     {
-        float2 v[NBL][RL];
-        sh_load<RL, false, NBL, K2_SH, RSP_THREADS, LGM, LGM - RBL>(L, rs, rows, twl + tw_pass_off(LGM, NP - 1), v);
+        f2 v[NBL][RL];
+        sh_load<RL, false, NBL, K2_SH, RSP_THREADS, LGM, LGM - RBL, CMP>(L, rs, rows,
+                                                                       twl + tw_pass_off(LGM, NP - 1, false, CMP), v);
         __syncthreads();
 #pragma unroll
         for (int t = 0; t < NBL; ++t) {
             Dft<RL, false>::run(v[t]);
 #pragma unroll
-            for (int r = 0; r < RL; ++r) v[t][r] = cmul(v[t][r], hreg[t * RL + r]);
+            for (int r = 0; r < RL; ++r) v[t][r] = vmul(v[t][r], hreg[(t % NHT) * RL + r]);
         }
         sh_store<RL, true, NBL, K2_SH, RSP_THREADS, LGM, 0>(v, rs, rows, StoreLds{L});
         __syncthreads();
@@ -609,11 +649,12 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     // inverse passes 1 .. NP-1 (reversed radices); the last keeps the valid overlap-save
     // outputs = stitched gates
     const int gend = min(sd.gb, g0 + sd.V);
-    fft_range<LGM, 1, NP, RBL, 16, true, true, K2_SH, RSP_THREADS>(
+    fft_range<LGM, 1, NP, RBL, 16, true, true, K2_SH, RSP_THREADS, CMP>(
         L, rs, rows, twl + NTWF, StoreLds{L}, StoreRdm{rdm, mag, G, g.Gp, row0, rows_total, Lh1, g0, gend});
     trace_stamp(fp, 3);
 }
 
+template <bool TWG, bool CMP>
 __global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k, FramePtrs fp, int rows_total) {
     extern __shared__ __attribute__((aligned(16))) float2 L[];   // data | twiddles (M) | H (M)
     const int f = blockIdx.y;
@@ -634,12 +675,12 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k,
 
     if (sd.type == 1) {
         switch (sd.logM) {
-            case 6: k2_fft_job<6>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
-            case 7: k2_fft_job<7>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
-            case 8: k2_fft_job<8>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
-            case 9: k2_fft_job<9>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
-            case 10: k2_fft_job<10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
-            default: k2_fft_job<11>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
+            case 6: k2_fft_job<6, TWG, CMP>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
+            case 7: k2_fft_job<7, TWG, CMP>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
+            case 8: k2_fft_job<8, TWG, CMP>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
+            case 9: k2_fft_job<9, TWG, CMP>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
+            case 10: k2_fft_job<10, TWG, CMP>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
+            default: k2_fft_job<11, TWG, CMP>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
         }
     } else {
         // direct FIR (narrow segment): filter() + circshift(-fir_delay) (fsf:111-112)
@@ -1074,10 +1115,24 @@ hipError_t launch_k1(const Geometry& g, const DevConsts& k, const FramePtrs& fp,
 
 hipError_t launch_k2(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int rows,
                      hipStream_t s) {
-    const size_t lds = (size_t)(K2_LDS_DATA + K2_LDS_TW) * sizeof(float2);
-    hipError_t e = allow_lds(k2_pc, lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k2_pc, dim3(g.nwg_k2, nf), dim3(RSP_THREADS), lds, s, g, k, fp, rows);
+    hipError_t e;
+    const size_t lds_g = (size_t)(RSP_K2_POINTS + RSP_K2_POINTS / 16) * sizeof(float2);
+    const size_t lds_l = (size_t)(K2_LDS_DATA + ((g.dbg & 256) ? K2_LDS_TW : K2_LDS_TW_CMP)) * sizeof(float2);
+    // twiddles read in place from global memory (L1/L2), or (dbg 64) copied to LDS; tables in
+    // compact rows, or (dbg 256, built so by the plan) full rows.  Default = the fastest
+    // measured (profiles/).
+#define K2_LAUNCH(TWG, CMP, LDS)                                                                     \
+    do {                                                                                             \
+        if ((e = allow_lds(k2_pc<TWG, CMP>, LDS)) != hipSuccess) return e;                           \
+        hipLaunchKernelGGL((k2_pc<TWG, CMP>), dim3(g.nwg_k2, nf), dim3(RSP_THREADS), LDS, s, g, k, fp, rows); \
+    } while (0)
+    switch (g.dbg & (64 | 256)) {
+        case 0: K2_LAUNCH(true, true, lds_g); break;
+        case 64: K2_LAUNCH(false, true, lds_l); break;
+        case 256: K2_LAUNCH(true, false, lds_g); break;
+        default: K2_LAUNCH(false, false, lds_l); break;
+    }
+#undef K2_LAUNCH
     return hipGetLastError();
 }
 

@@ -85,20 +85,19 @@ void radix_plan(int m, int* nrad, int* rad) {
 }
 
 // Per-pass Stockham twiddle tables of a 2^m-point FFT (radix order reversed if rev),
-// concatenated: pass q >= 1 owns Ns_q x log2(R_q) entries T[k][i] = exp(-2 pi i k 2^i / (Ns_q R_q));
-// the kernels form the other powers by products (expand_tw, tw_pass_off in rsp_kernels.hip).
-void build_pass_twiddles(int m, std::vector<float2>& out, bool rev = false) {
+// concatenated: pass q >= 1 owns Ns_q x (R_q - 1) entries T[k][r-1] = exp(-2 pi i k r / (Ns_q R_q))
+// (must match tw_pass_off() in rsp_kernels.hip).
+void build_pass_twiddles(int m, std::vector<float2>& out, bool rev = false, bool cmp = false) {
     int nrad, rad[8];
     radix_plan(m, &nrad, rad);
     if (rev) std::reverse(rad, rad + nrad);
     int Ns = 1;
     for (int q = 0; q < nrad; ++q) {
         const int R = rad[q];
-        const int lgR = ilog2i(R);
         if (q > 0)
             for (int k = 0; k < Ns; ++k)
-                for (int i = 0; i < lgR; ++i) {
-                    const double a = -2.0 * M_PI * (double)k * (1 << i) / ((double)Ns * R);
+                for (int r = 1; r < R; r = cmp ? 2 * r : r + 1) {   // compact rows: r = 1, 2, 4, 8
+                    const double a = -2.0 * M_PI * (double)k * r / ((double)Ns * R);
                     out.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
                 }
         Ns *= R;
@@ -276,7 +275,7 @@ struct Interval { int lo, hi; };
 
 int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga, int gb, int seg_lo,
                       std::vector<float2>& H, std::vector<float2>& twM, std::vector<int>& tw_sizes,
-                      std::vector<int>& tw_offs, const char* name) {
+                      std::vector<int>& tw_offs, const char* name, bool cmp) {
     std::vector<cd> h(Nfft);
     for (int i = 0; i < Nfft; ++i) h[i] = cd(mf_fft[2 * i], mf_fft[2 * i + 1]);
     fft_d(h, +1);
@@ -323,8 +322,8 @@ int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga,
     if (ti < 0) {
         tw_sizes.push_back(M);
         tw_offs.push_back((int)twM.size());
-        build_pass_twiddles(s.logM, twM, false);   // forward FFT
-        build_pass_twiddles(s.logM, twM, true);    // inverse FFT (reversed radices)
+        build_pass_twiddles(s.logM, twM, false, cmp);   // forward FFT
+        build_pass_twiddles(s.logM, twM, true, cmp);    // inverse FFT (reversed radices)
         ti = (int)tw_sizes.size() - 1;
     }
     s.tw_off = tw_offs[ti];
@@ -589,14 +588,14 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     if (g2 > 0) {
         SegDesc s{};
         int rc = build_fft_segment(s, pre->MF_medium_fft, pre->N_fft_med, N, g1, g1 + g2, pre->seg_start_medium - 1, H,
-                                   twM, tw_sizes, tw_offs, "medium");
+                                   twM, tw_sizes, tw_offs, "medium", (g.dbg & 256) == 0);
         if (rc) return bail(rc);
         p->segs.push_back(s);
     }
     if (g3 > 0) {
         SegDesc s{};
         int rc = build_fft_segment(s, pre->MF_long_fft, pre->N_fft_long, N, g1 + g2, G, pre->seg_start_long - 1, H, twM,
-                                   tw_sizes, tw_offs, "long");
+                                   tw_sizes, tw_offs, "long", (g.dbg & 256) == 0);
         if (rc) return bail(rc);
         p->segs.push_back(s);
     }
