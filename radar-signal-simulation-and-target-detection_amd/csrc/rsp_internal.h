@@ -62,6 +62,13 @@ struct Geometry {
     K2Job jobs[RSP_MAX_JOBS];
 };
 
+// K3 tiles: range cells from the first cell under test rounded down to 4, cfar_RT per tile
+// (k3_cfar, launch_k3, rsp_profile_stages).
+__host__ __device__ inline int k3_ntiles(const Geometry& g) {
+    const int rc0 = g.refR + g.guardR;
+    return (g.G - rc0 - (rc0 & ~3) + g.cfar_RT - 1) / g.cfar_RT;
+}
+
 struct FramePtrs {
     const float2* in[RSP_MAX_F];   // K1 input cube (PNC) or beam cube
     float2* z[RSP_MAX_F];          // compacted Doppler-domain rows

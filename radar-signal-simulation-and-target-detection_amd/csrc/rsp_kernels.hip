@@ -774,16 +774,28 @@ __device__ double spline_peak(const double* y, int n) {
             c3[i] = (1.0 / 6.0) * d3;
         }
     }
-    const int nq = (n - 1) * INTERP + 1;
+    // samples q = 0 .. (n-1) INTERP in order (first argmax wins); sample q lies on interval
+    // min(q / INTERP, n - 2) like ppval -- every array index is a compile-time constant
     double best = -INFINITY, bx = 0.0;
-    for (int q = 0; q < nq; ++q) {
-        int i = q / INTERP;
-        if (i > n - 2) i = n - 2;
-        const double t = (q - i * INTERP) * dx;
-        const double val = ((c3[i] * t + c2[i]) * t + c1[i]) * t + c0[i];
-        if (val > best) {
-            best = val;
-            bx = q * dx;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (i < n - 1) {
+#pragma unroll
+            for (int t = 0; t < INTERP; ++t) {
+                const double tt = t * dx;
+                const double val = ((c3[i] * tt + c2[i]) * tt + c1[i]) * tt + c0[i];
+                if (val > best) {
+                    best = val;
+                    bx = (i * INTERP + t) * dx;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {   // the last sample: end of the last interval
+        if (i == n - 2) {
+            const double val = ((c3[i] + c2[i]) + c1[i]) + c0[i];
+            if (val > best) bx = (n - 1);
         }
     }
     return bx;
@@ -794,22 +806,14 @@ __device__ __forceinline__ void s9_estimate(const DevConsts& k, const float* S, 
                                             int v, int r, int pair, const float* __restrict__ MA,
                                             const float* __restrict__ MB, DevDet* out) {
     const int c = r - c0;
+    // the 5-cell windows clipped to the map (fsf:241-250): cells first .. first + n - 1
+    const int rfirst = max(r - 2, 0), nrc = min(r + 2, G - 1) - rfirst + 1;
+    const int vfirst = max(v - 2, 0), nvc = min(v + 2, P - 1) - vfirst + 1;
     double yr[5], yv[5];
-    int nrc = 0, rfirst = -1;
-    for (int q = -2; q <= 2; ++q) {
-        const int rr = r + q;
-        if (rr >= 0 && rr < G) {
-            if (rfirst < 0) rfirst = rr;
-            yr[nrc++] = (double)S[v * W + c + q];
-        }
-    }
-    int nvc = 0, vfirst = -1;
-    for (int q = -2; q <= 2; ++q) {
-        const int vv = v + q;
-        if (vv >= 0 && vv < P) {
-            if (vfirst < 0) vfirst = vv;
-            yv[nvc++] = (double)S[vv * W + c];
-        }
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        yr[j] = j < nrc ? (double)S[v * W + (rfirst - c0) + j] : 0.0;
+        yv[j] = j < nvc ? (double)S[(vfirst + j) * W + c] : 0.0;
     }
     const double rmax = (nrc < 3) ? (double)r : rfirst + spline_peak<8>(yr, nrc);
     const double vmax = (nvc < 3) ? (double)v : vfirst + spline_peak<4>(yv, nvc);
@@ -829,17 +833,30 @@ __device__ __forceinline__ void s9_estimate(const DevConsts& k, const float* S, 
     *out = d;
 }
 
+// Out-of-line copy for the queue-overflow path (pathological detection densities), so the
+// CFAR loops do not carry an inlined S9 body.
+__device__ __attribute__((noinline)) void s9_estimate_ool(const DevConsts& k, const float* S, int W, int c0, int P,
+                                                          int G, int Gp, int v, int r, int pair, const float* MA,
+                                                          const float* MB, DevDet* out) {
+    s9_estimate(k, S, W, c0, P, G, Gp, v, r, pair, MA, MB, out);
+}
+
 #define K3_QCAP 1024
 #define K3_VEC 12   // float4 loads per beam per thread in flight
 
-// RR/RV = reference-cell counts when known at compile time (the reference's 5/5), 0 = runtime.
-template <int RR, int RV>
-__global__ __launch_bounds__(RSP_THREADS) void k3_cfar(Geometry g, DevConsts k, FramePtrs fp) {
+constexpr int floor4(int x) { return x >= 0 ? (x & ~3) : -((-x + 3) & ~3); }
+
+// RR/RV/GR/GV = reference/guard cell counts when known at compile time (the reference's
+// 5/5/10/10, v8:45-46), 0 = runtime.  Tiles: RT range cells x all P Doppler cells of one beam
+// pair, tile starts aligned to 4 cells so that the magnitude rows load as float4.
+template <int RR, int RV, int GR, int GV>
+__global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts k, FramePtrs fp) {
     extern __shared__ __attribute__((aligned(16))) float S[];   // [P][W] | queue[K3_QCAP] | qn, base
+    constexpr bool FAST = RR > 0 && RV > 0 && GR > 0 && GV > 0;
     // XCD-aware order (bijective swizzle, cdna_hip_programming.md T1): the workgroups that
     // share an XCD take consecutive (tile, pair) ids with pairs fastest, so beam b's tile --
     // read by pairs b-1 and b -- and the range halos of neighbouring tiles are L2 hits
-    const int npair = g.B - 1, ntile = (g.G - 2 * (g.refR + g.guardR) + g.cfar_RT - 1) / g.cfar_RT;
+    const int npair = g.B - 1, ntile = k3_ntiles(g);
     int wg = blockIdx.x;
     {
         const int nwg = gridDim.x, xcd = wg & 7, q = nwg >> 3, rm = nwg & 7;
@@ -847,22 +864,22 @@ __global__ __launch_bounds__(RSP_THREADS) void k3_cfar(Geometry g, DevConsts k, 
     }
     const int pair = wg % npair, col = wg / npair;
     const int tile = col % ntile, f = col / ntile;
-    const int P = g.P, G = g.G, W = g.cfar_W, hR = g.cfar_hR;
-    const int rR = RR ? RR : g.refR, gR = g.guardR, rV = RV ? RV : g.refV, gV = g.guardV;
-    const int r_begin = rR + gR + tile * g.cfar_RT;
-    const int r_end = min(r_begin + g.cfar_RT, G - rR - gR);
-    const int c0 = r_begin - hR;
+    const int P = g.P, G = g.G, W = g.cfar_W, hR = g.cfar_hR, RT = g.cfar_RT;
+    const int rR = RR ? RR : g.refR, gR = GR ? GR : g.guardR, rV = RV ? RV : g.refV, gV = GV ? GV : g.guardV;
+    const int rc0 = rR + gR;                           // first cell under test (0-based)
+    const int tstart = (rc0 & ~3) + tile * RT;         // multiple of 4
+    const int c0 = tstart - hR;                        // tile column 0 (multiple of 4; may be < 0)
+    const int cut_lo = max(tstart, rc0), cut_hi = min(tstart + RT, G - rc0);
     int* queue = reinterpret_cast<int*>(S + P * W);
     int* qn = queue + K3_QCAP;
     const int Gp = g.Gp;
     const float* __restrict__ MA = fp.mag[f] + (size_t)pair * P * Gp;   // |RDM| of beams pair, pair+1
     const float* __restrict__ MB = MA + (size_t)P * Gp;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;   // 4 waves
     trace_stamp(fp, 0);
     if (threadIdx.x == 0) qn[0] = 0;
     // ---- load S = |A| + |B| (fsf:184-187) from the magnitude maps: 16 B per lane,
     //      K3_VEC float4 of each beam in flight per thread
-    if ((c0 & 3) == 0 && (W & 3) == 0) {
+    {
         const int W4 = W >> 2, n4 = P * W4;
         for (int e0 = 0; e0 < n4; e0 += K3_VEC * RSP_THREADS) {
             float4 xa[K3_VEC], xb[K3_VEC];
@@ -873,7 +890,7 @@ __global__ __launch_bounds__(RSP_THREADS) void k3_cfar(Geometry g, DevConsts k, 
                 xb[u] = xa[u];
                 if (e < n4) {
                     const int v = e / W4, r = c0 + 4 * (e - v * W4);
-                    if (r < G) {   // rows are padded to Gp (multiple of 4): r + 3 < Gp
+                    if (r >= 0 && r < G) {   // rows are padded to Gp (multiple of 4): r + 3 < Gp
                         xa[u] = *reinterpret_cast<const float4*>(MA + (size_t)v * Gp + r);
                         xb[u] = *reinterpret_cast<const float4*>(MB + (size_t)v * Gp + r);
                         if (r + 1 >= G) { xa[u].y = 0.f; xb[u].y = 0.f; }
@@ -890,58 +907,109 @@ __global__ __launch_bounds__(RSP_THREADS) void k3_cfar(Geometry g, DevConsts k, 
                         make_float4(xa[u].x + xb[u].x, xa[u].y + xb[u].y, xa[u].z + xb[u].z, xa[u].w + xb[u].w);
             }
         }
-    } else {
-        for (int e = threadIdx.x; e < P * W; e += RSP_THREADS) {
-            const int v = e / W, r = c0 + (e - v * W);
-            S[e] = (r >= 0 && r < G) ? MA[(size_t)v * Gp + r] + MB[(size_t)v * Gp + r] : 0.f;
-        }
     }
     __syncthreads();
     trace_stamp(fp, 1);
     const int v0 = rV + gV, v1 = P - rV - gV;
-    const int nr = r_end - r_begin;
-    if (v1 <= v0 || nr <= 0) return;
+    if (v1 <= v0 || cut_hi <= cut_lo) return;
     const float fR = (float)rR, fV = (float)rV;
+    // mean() = sum / n over the slices of fsf:197-203 (max(a/n, b/n) = max(a, b)/n); the
+    // division is a multiply by 1/n (<= 1 ulp from the quotient: only cells within that of the
+    // threshold can decide differently, the fp32-vs-fp64 band the parity tests allow)
+    const float iR = 1.0f / fR, iV = 1.0f / fV;
+#define K3_HIT(V, C, CUT, LR, TR, LV, TV)                                                               \
+    do {                                                                                                \
+        const float nR_ = fmaxf(LR, TR) * iR, nV_ = fmaxf(LV, TV) * iV;                                 \
+        if ((CUT) > g.T * fmaxf(nR_, nV_)) {                                                            \
+            const int qi = atomicAdd(qn, 1);                                                            \
+            if (qi < K3_QCAP) {                                                                         \
+                queue[qi] = ((V) << 16) | (C);                                                          \
+            } else { /* queue overflow (pathological): estimate in place */                             \
+                const int idx = atomicAdd(fp.count[f], 1);                                              \
+                if (idx < g.max_dets)                                                                   \
+                    s9_estimate_ool(k, S, W, c0, P, G, Gp, V, c0 + (C), pair, MA, MB, &fp.dets[f][idx]); \
+            }                                                                                           \
+        }                                                                                               \
+    } while (0)
     // ---- cross GOCA-CFAR (fsf:192-213); hits go to an LDS queue so that the S9 work is
     //      spread over the whole workgroup instead of serialising in the lane that owns a range cell
-    for (int rb = 0; rb < nr; rb += 64) {
-        const int ri = rb + lane;
-        if (ri >= nr) continue;
-        const int r = r_begin + ri;
-        const int c = r - c0;
-        for (int v = v0 + wv; v < v1; v += 4) {
-            const float* rowp = S + v * W;
-            // window sums left to right like mean() over the slices of fsf:197-203; with RR/RV
-            // known the 2*(RR+RV) LDS reads are independent and issue back to back
-            float lr = 0.f, tr = 0.f, lv = 0.f, tv = 0.f;
-            const float* lrp = rowp + c - gR - rR;
-            const float* trp = rowp + c + gR + 1;
-            const float* lvp = S + (v - gV - rV) * W + c;
-            const float* tvp = S + (v + gV + 1) * W + c;
+    if (FAST && RT == 64) {
+        // a thread takes 4 adjacent range cells of one Doppler row: every window value comes
+        // from float4 LDS reads (17 per 4 cells instead of 20 scalar reads per cell); sums run
+        // left to right over each slice like mean()
+        constexpr int DL = -(GR + RR), DR = GR + 1;              // window starts rel. to the cell
+        constexpr int BL = floor4(DL), BR = floor4(DR);
+        constexpr int NL = (DL + 3 + RR - BL + 3) / 4, NR = (DR + 3 + RR - BR + 3) / 4;
+        const int q = threadIdx.x & 15;
+        const int c = hR + 4 * q;                                 // first tile column of the group
+        const int r = c0 + c;
+#pragma unroll 1
+        for (int v = v0 + (threadIdx.x >> 4); v < v1; v += RSP_THREADS / 16) {
+            const float* row = S + v * W + c;
+            float xl[4 * NL], xr[4 * NR], cv[4];
+            f2 lv01 = {0.f, 0.f}, lv23 = {0.f, 0.f}, tv01 = {0.f, 0.f}, tv23 = {0.f, 0.f};   // packed column sums
 #pragma unroll
-            for (int q = 0; q < (RR ? RR : rR); ++q) {
-                lr += lrp[q];
-                tr += trp[q];
+            for (int j = 0; j < NL; ++j) {
+                const float4 t = *reinterpret_cast<const float4*>(row + BL + 4 * j);
+                xl[4 * j] = t.x; xl[4 * j + 1] = t.y; xl[4 * j + 2] = t.z; xl[4 * j + 3] = t.w;
             }
 #pragma unroll
-            for (int q = 0; q < (RV ? RV : rV); ++q) {
-                lv += lvp[q * W];
-                tv += tvp[q * W];
+            for (int j = 0; j < NR; ++j) {
+                const float4 t = *reinterpret_cast<const float4*>(row + BR + 4 * j);
+                xr[4 * j] = t.x; xr[4 * j + 1] = t.y; xr[4 * j + 2] = t.z; xr[4 * j + 3] = t.w;
             }
-            const float nR = fmaxf(lr / fR, tr / fR);   // mean() = sum / n
-            const float nV = fmaxf(lv / fV, tv / fV);
-            const float thr = g.T * fmaxf(nR, nV);
-            if (rowp[c] > thr) {
-                const int qi = atomicAdd(qn, 1);
-                if (qi < K3_QCAP) {
-                    queue[qi] = (v << 16) | c;
-                } else {   // queue overflow (pathological): estimate in place
-                    const int idx = atomicAdd(fp.count[f], 1);
-                    if (idx < g.max_dets) s9_estimate(k, S, W, c0, P, G, Gp, v, r, pair, MA, MB, &fp.dets[f][idx]);
+            {
+                const float4 t = *reinterpret_cast<const float4*>(row);
+                cv[0] = t.x; cv[1] = t.y; cv[2] = t.z; cv[3] = t.w;
+            }
+#pragma unroll
+            for (int qq = 0; qq < RV; ++qq) {
+                const float4 a = *reinterpret_cast<const float4*>(row + (qq - GV - RV) * W);
+                const float4 b = *reinterpret_cast<const float4*>(row + (qq + GV + 1) * W);
+                lv01 += f2{a.x, a.y};
+                lv23 += f2{a.z, a.w};
+                tv01 += f2{b.x, b.y};
+                tv23 += f2{b.z, b.w};
+            }
+            const float lv[4] = {lv01.x, lv01.y, lv23.x, lv23.y}, tv[4] = {tv01.x, tv01.y, tv23.x, tv23.y};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float lr = 0.f, tr = 0.f;
+#pragma unroll
+                for (int qq = 0; qq < RR; ++qq) {
+                    lr += xl[i + DL - BL + qq];
+                    tr += xr[i + DR - BR + qq];
                 }
+                const int ri = r + i;
+                if (ri >= cut_lo && ri < cut_hi) K3_HIT(v, c + i, cv[i], lr, tr, lv[i], tv[i]);
+            }
+        }
+    } else {
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;   // 4 waves
+        for (int rb = cut_lo; rb < cut_hi; rb += 64) {
+            const int r = rb + lane;
+            if (r >= cut_hi) continue;
+            const int c = r - c0;
+            for (int v = v0 + wv; v < v1; v += 4) {
+                const float* rowp = S + v * W;
+                float lr = 0.f, tr = 0.f, lv = 0.f, tv = 0.f;
+                const float* lrp = rowp + c - gR - rR;
+                const float* trp = rowp + c + gR + 1;
+                const float* lvp = S + (v - gV - rV) * W + c;
+                const float* tvp = S + (v + gV + 1) * W + c;
+                for (int qq = 0; qq < rR; ++qq) {
+                    lr += lrp[qq];
+                    tr += trp[qq];
+                }
+                for (int qq = 0; qq < rV; ++qq) {
+                    lv += lvp[qq * W];
+                    tv += tvp[qq * W];
+                }
+                K3_HIT(v, c, rowp[c], lr, tr, lv, tv);
             }
         }
     }
+#undef K3_HIT
     __syncthreads();
     trace_stamp(fp, 2);
     const int n = min(qn[0], K3_QCAP);
@@ -1137,18 +1205,16 @@ hipError_t launch_k2(const Geometry& g, const DevConsts& k, const FramePtrs& fp,
 }
 
 hipError_t launch_k3(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, hipStream_t s) {
-    const int ncut_r = g.G - 2 * (g.refR + g.guardR);
-    if (g.B < 2 || ncut_r <= 0) return hipSuccess;
-    const int tiles = (ncut_r + g.cfar_RT - 1) / g.cfar_RT;
+    if (g.B < 2 || g.G - 2 * (g.refR + g.guardR) <= 0) return hipSuccess;
     const size_t lds = (size_t)g.P * g.cfar_W * sizeof(float) + (K3_QCAP + 4) * sizeof(int);
-    const dim3 grid(tiles * (g.B - 1) * nf);   // 1-D; k3_cfar remaps it XCD-aware
+    const dim3 grid(k3_ntiles(g) * (g.B - 1) * nf);   // 1-D; k3_cfar remaps it XCD-aware
     hipError_t e;
-    if (g.refR == 5 && g.refV == 5) {   // the reference's cfar_params (v8:45-46)
-        if ((e = allow_lds(k3_cfar<5, 5>, lds)) != hipSuccess) return e;
-        hipLaunchKernelGGL((k3_cfar<5, 5>), grid, dim3(RSP_THREADS), lds, s, g, k, fp);
+    if (g.refR == 5 && g.refV == 5 && g.guardR == 10 && g.guardV == 10) {   // the reference's cfar_params (v8:45-46)
+        if ((e = allow_lds(k3_cfar<5, 5, 10, 10>, lds)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k3_cfar<5, 5, 10, 10>), grid, dim3(RSP_THREADS), lds, s, g, k, fp);
     } else {
-        if ((e = allow_lds(k3_cfar<0, 0>, lds)) != hipSuccess) return e;
-        hipLaunchKernelGGL((k3_cfar<0, 0>), grid, dim3(RSP_THREADS), lds, s, g, k, fp);
+        if ((e = allow_lds(k3_cfar<0, 0, 0, 0>, lds)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k3_cfar<0, 0, 0, 0>), grid, dim3(RSP_THREADS), lds, s, g, k, fp);
     }
     return hipGetLastError();
 }

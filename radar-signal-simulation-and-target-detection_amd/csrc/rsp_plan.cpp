@@ -660,7 +660,7 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     for (int q = 0; q < g.njobs; ++q) g.jobs[q] = p->jobs[q];
     g.nwg_k2 = wg;
     // K3 tile
-    g.cfar_hR = std::max(g.refR + g.guardR, 2);
+    g.cfar_hR = (std::max(g.refR + g.guardR, 2) + 3) & ~3;   // halo, multiple of 4 (float4 tile loads)
     g.cfar_RT = 64;
     while (g.cfar_RT > 8 && (size_t)P * (g.cfar_RT + 2 * g.cfar_hR) * 4 > 96 * 1024) g.cfar_RT >>= 1;
     g.cfar_W = (g.cfar_RT + 2 * g.cfar_hR + 3) & ~3;   // LDS row stride, float4 aligned
@@ -917,8 +917,7 @@ int32_t rsp_profile_stages(rsp_plan* p, const void* const* d_cubes, int32_t n_cu
     }
     if (frames_out) *frames_out = nf;
     if (const char* tf = getenv("RSP_TRACE_FILE")) {   // diagnostic per-workgroup phase stamps
-        size_t nwg[3] = {(size_t)g.ntiles * nf, (size_t)g.nwg_k2 * nf,
-                         (size_t)((g.G - 2 * (g.refR + g.guardR) + g.cfar_RT - 1) / g.cfar_RT) * (g.B - 1) * nf};
+        size_t nwg[3] = {(size_t)g.ntiles * nf, (size_t)g.nwg_k2 * nf, (size_t)k3_ntiles(g) * (g.B - 1) * nf};
         size_t mx = std::max(nwg[0], std::max(nwg[1], nwg[2]));
         unsigned long long* dt = nullptr;
         HIPCHK(hipMalloc(&dt, mx * 4 * sizeof(unsigned long long)));
