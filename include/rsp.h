@@ -216,6 +216,66 @@ int32_t rsp_device_upload(rsp_plan* plan, void* d_dst, const void* h_src, int64_
 int32_t rsp_device_download(rsp_plan* plan, void* h_dst, const void* d_src, int64_t bytes);
 int32_t rsp_device_sync(rsp_plan* plan);
 
+/* ---- MAT-file frame I/O (host only, no GPU) ----
+ * The reference moves frames as `frame_sim_array_%d.mat` written by MATLAB's default
+ * `save` (-v7: Level-5 format, zlib-compressed elements):
+ * main_simulate_echoes_with_array.m:226-229 (`raw_iq_data`),
+ * main_simulate_echoes_with_array_v2.m:256-289 (`raw_iq_data_noise_sample`, `servo_angle`),
+ * read back by `load` in debug_simulated_data_processing_v3.m:17-22 and
+ * main_test_with_simulated_data.m:195,208,215.  These functions replace that MATLAB
+ * `save`/`load` pair for hosts without MATLAB.  Level-5 files of either byte order,
+ * compressed or not, are read; v7.3 (HDF5) returns RSP_ERR_UNSUPPORTED. */
+#define RSP_MAT_MAXDIMS 8
+typedef enum rsp_mat_class {    /* MATLAB mxClassID values */
+    RSP_MAT_CHAR = 4, RSP_MAT_DOUBLE = 6, RSP_MAT_SINGLE = 7, RSP_MAT_INT8 = 8, RSP_MAT_UINT8 = 9,
+    RSP_MAT_INT16 = 10, RSP_MAT_UINT16 = 11, RSP_MAT_INT32 = 12, RSP_MAT_UINT32 = 13,
+    RSP_MAT_INT64 = 14, RSP_MAT_UINT64 = 15
+} rsp_mat_class;
+typedef enum rsp_mat_out {
+    RSP_MAT_OUT_F64 = 1,   /* numeric -> double; complex interleaved (mxGetComplexDoubles) */
+    RSP_MAT_OUT_F32 = 2,   /* numeric -> float;  complex interleaved                       */
+    RSP_MAT_OUT_CHAR = 3   /* char array -> NUL-terminated UTF-8                           */
+} rsp_mat_out;
+
+/* One variable of a MAT file as `whos -file` lists it. */
+typedef struct rsp_mat_var {
+    char name[64];
+    int32_t cls;           /* rsp_mat_class (1 cell, 2 struct, 5 sparse, ... listed, not read) */
+    int32_t is_complex;
+    int32_t ndims;
+    int32_t reserved;
+    int64_t dims[RSP_MAT_MAXDIMS];
+    int64_t numel;
+} rsp_mat_var;
+
+/* A variable to write: column-major data, complex interleaved (re, im); cls is
+ * RSP_MAT_DOUBLE (data = double*), RSP_MAT_SINGLE (float*) or RSP_MAT_CHAR (bytes). */
+typedef struct rsp_mat_wvar {
+    const char* name;
+    int32_t cls;
+    int32_t is_complex;
+    int32_t ndims;
+    const int64_t* dims;
+    const void* data;
+} rsp_mat_wvar;
+
+/* List up to `cap` variables (*n_vars = how many the file holds). */
+int32_t rsp_mat_list(const char* path, rsp_mat_var* vars, int32_t cap, int32_t* n_vars);
+/* Read variable `name` into `out` (cap = entries of out; a complex value counts 2). */
+int32_t rsp_mat_read(const char* path, const char* name, int32_t dtype, void* out, int64_t cap);
+/* Write a MAT file (Level 5; compress != 0 -> zlib elements like MATLAB -v7). */
+int32_t rsp_mat_write(const char* path, const rsp_mat_wvar* vars, int32_t n, int32_t compress);
+/* load(frame_sim_array_%d.mat): the [P x N x C] cube (raw_iq_data_noise_sample, else
+ * raw_iq_data) into `cube` as dtype RSP_C64/RSP_C128 (NULL: only dims_out), and
+ * servo_angle (may be NULL; *n_angle = its length, 0 if absent).  One pass over the file. */
+int32_t rsp_mat_load_frame(const char* path, int32_t dtype, void* cube, int64_t cap_elems, int32_t dims_out[3],
+                           double* servo_angle, int32_t angle_cap, int32_t* n_angle);
+/* save(frame_sim_array_%d.mat, ...): generation 1 -> `raw_iq_data`, 2 ->
+ * `raw_iq_data_noise_sample`; complex double cube [P x N x C] interleaved; servo_angle
+ * 1 x n_angle (omitted if NULL or n_angle == 0). */
+int32_t rsp_mat_save_frame(const char* path, const double* cube, int32_t P, int32_t N, int32_t C,
+                           const double* servo_angle, int32_t n_angle, int32_t generation, int32_t compress);
+
 #ifdef __cplusplus
 }
 #endif

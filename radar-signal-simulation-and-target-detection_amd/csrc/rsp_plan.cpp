@@ -19,15 +19,33 @@ namespace {
 
 thread_local std::string g_err;
 
-int fail(int code, const char* fmt, ...) {
+int vfail(int code, const char* fmt, va_list ap) {
     char buf[1024];
-    va_list ap;
-    va_start(ap, fmt);
     vsnprintf(buf, sizeof buf, fmt, ap);
-    va_end(ap);
     g_err = buf;
     return code;
 }
+
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vfail(code, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+}  // namespace
+
+// Error sink shared with the other host translation units (not exported).
+__attribute__((visibility("hidden"))) int rsp_set_error(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vfail(code, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+namespace {
 
 #define HIPCHK(expr)                                                                            \
     do {                                                                                        \

@@ -7,6 +7,8 @@ Drop-in for the MATLAB reference's per-frame chain
   precomputed_data, frame_idx)``  -- fun_process_single_frame.m:13
 * ``process_stage2_mtd(iq_data, angle, config)``  -- process_stage2_mtd.m:1
 * ``precompute(...)`` -- the driver's "%% 3" section (v8:79-155)
+* ``load_frame`` / ``save_frame`` -- the ``frame_sim_array_%d.mat`` load/save pair
+  (main_simulate_echoes_with_array_v2.m:285, debug_simulated_data_processing_v3.m:20-22)
 
 All compute runs in librsp.so (HIP kernels for gfx950 behind the C-ABI in
 include/rsp.h).  There is no CPU fallback.
@@ -16,6 +18,8 @@ from .config import (named_config, make_config, default_cfar_params, default_clu
 from .precompute import precompute
 from .plan import Plan
 from ._abi import RspError
+from .matio import load_frame, save_frame
+from . import matio
 
 _PLANS = {}
 

@@ -69,6 +69,21 @@ class Sizes(ct.Structure):
                 ('used_samples', ct.c_int32), ('max_detections', ct.c_int32), ('n_stages', ct.c_int32)]
 
 
+RSP_MAT_CHAR, RSP_MAT_DOUBLE, RSP_MAT_SINGLE = 4, 6, 7
+RSP_MAT_OUT_F64, RSP_MAT_OUT_F32, RSP_MAT_OUT_CHAR = 1, 2, 3
+RSP_MAT_MAXDIMS = 8
+
+
+class MatVar(ct.Structure):
+    _fields_ = [('name', ct.c_char * 64), ('cls', ct.c_int32), ('is_complex', ct.c_int32), ('ndims', ct.c_int32),
+                ('reserved', ct.c_int32), ('dims', ct.c_int64 * RSP_MAT_MAXDIMS), ('numel', ct.c_int64)]
+
+
+class MatWVar(ct.Structure):
+    _fields_ = [('name', ct.c_char_p), ('cls', ct.c_int32), ('is_complex', ct.c_int32), ('ndims', ct.c_int32),
+                ('dims', ct.POINTER(ct.c_int64)), ('data', ct.c_void_p)]
+
+
 _P = ct.c_void_p
 PROTOTYPES = {
     'rsp_abi_version': (ct.c_int32, []),
@@ -99,6 +114,13 @@ PROTOTYPES = {
     'rsp_device_upload': (ct.c_int32, [_P, _P, _P, ct.c_int64]),
     'rsp_device_download': (ct.c_int32, [_P, _P, _P, ct.c_int64]),
     'rsp_device_sync': (ct.c_int32, [_P]),
+    'rsp_mat_list': (ct.c_int32, [ct.c_char_p, ct.POINTER(MatVar), ct.c_int32, ct.POINTER(ct.c_int32)]),
+    'rsp_mat_read': (ct.c_int32, [ct.c_char_p, ct.c_char_p, ct.c_int32, _P, ct.c_int64]),
+    'rsp_mat_write': (ct.c_int32, [ct.c_char_p, ct.POINTER(MatWVar), ct.c_int32, ct.c_int32]),
+    'rsp_mat_load_frame': (ct.c_int32, [ct.c_char_p, ct.c_int32, _P, ct.c_int64, ct.POINTER(ct.c_int32), _dp,
+                                        ct.c_int32, ct.POINTER(ct.c_int32)]),
+    'rsp_mat_save_frame': (ct.c_int32, [ct.c_char_p, _dp, ct.c_int32, ct.c_int32, ct.c_int32, _dp, ct.c_int32,
+                                        ct.c_int32, ct.c_int32]),
 }
 
 _lib = None
