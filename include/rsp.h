@@ -197,12 +197,19 @@ int32_t rsp_process_stage2(rsp_plan* plan, const void* iq_beams, int32_t dtype,
 /* ---- measurement ----
  * Time each device stage `iters` times on the plan's stream with HIP events.  Each launch
  * batches nf = min(n_cubes, frames_per_launch) frames taken from the device-resident
- * complex64 cubes d_cubes[0..nf-1].  ms_out[i] = average ms per launch of stage i,
+ * complex64 cubes d_cubes[]; launch j takes cubes (j nf + f) mod n_cubes, f < nf.  ms_out[i] = average ms per launch of stage i,
  * bytes_out[i] = algorithmic HBM bytes per launch (nf frames), *frames_out = nf.
  * Stage names via rsp_stage_name. */
 int32_t rsp_profile_stages(rsp_plan* plan, const void* const* d_cubes, int32_t n_cubes, int32_t iters,
                            float* ms_out, int64_t* bytes_out, int32_t cap, int32_t* frames_out);
 const char* rsp_stage_name(int32_t stage);
+
+/* Live stage timing of the throughput queue (rsp_enqueue_device): with timing on, every batch
+ * records HIP events around K1, K2 and K3 on the stream the kernels run on, and harvest adds the
+ * elapsed times.  rsp_set_stage_timing resets the sums.  rsp_stage_times: ms_sum[i] = total ms
+ * of stage i over *launches batched launches holding *frames frames. */
+int32_t rsp_set_stage_timing(rsp_plan* plan, int32_t on);
+int32_t rsp_stage_times(const rsp_plan* plan, double* ms_sum, int32_t cap, int64_t* launches, int64_t* frames);
 
 /* Host-only S10 + S11 (fun_cluster_stage1_10 / fun_cluster_stage2_11, fsf:302-407) on a
  * detection list (any order; sorted into the reference's find() order first).  No GPU. */

@@ -4,7 +4,7 @@
 #include <stdint.h>
 
 #define RSP_MAX_F 8          // frames batched per launch
-#define RSP_LANES 3          // streams of the throughput queue (batches in flight)
+#define RSP_LANES 4          // max streams of the throughput queue (batches in flight)
 #define RSP_K2_POINTS 4096   // complex points per pulse-compression workgroup
 #define RSP_THREADS 256
 

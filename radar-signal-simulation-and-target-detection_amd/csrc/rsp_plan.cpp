@@ -125,7 +125,12 @@ void build_pass_twiddles(int m, std::vector<float2>& out, bool rev = false, bool
 double mround(double x) { return x < 0 ? -std::floor(-x + 0.5) : std::floor(x + 0.5); }
 
 struct Lane {
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;   // the lane's own stream: detection read-back, synchronous paths
+    hipStream_t ks = nullptr;       // where the lane's K1-K3 run: the plan's shared kernel stream, or `stream`
+    hipEvent_t kdone = nullptr;     // K3 of the lane's batch done (on ks)
+    hipEvent_t ready = nullptr;     // work queued on `stream` before the batch (uploads), awaited by ks
+    hipEvent_t tev[4] = {};         // live stage timing: before K1, after K1, K2, K3 (on ks)
+    bool timed = false;
     hipEvent_t done = nullptr;
     float2* z = nullptr;        // F frames
     float2* rdm = nullptr;      // F frames
@@ -166,7 +171,19 @@ struct rsp_plan {
     float2* h_stage = nullptr;    // pinned staging for uploads
     size_t h_stage_bytes = 0;
     Lane lanes[RSP_LANES];
+    int nlanes = 3;   // lanes in use (RSP_NLANES, 1..RSP_LANES)
     int next_lane = 0;
+    // Throughput queue.  Default: each lane runs its batch (K1-K3 + read-back) on its own
+    // stream, so consecutive batches overlap on the device (one batch's kernel tail fills with
+    // the next batch's workgroups: 52 vs 59 us/frame at x2, F = 4, measured).  RSP_QUEUE=serial:
+    // all batches run back to back on ONE kernel stream (every kernel has the chip to itself)
+    // while the lanes' streams carry the read-back.
+    hipStream_t kstream = nullptr;
+    // live stage timing of the queue (rsp_set_stage_timing): HIP events around K1/K2/K3 of
+    // every batch, summed at harvest
+    bool time_stages = false;
+    double stage_ms[3] = {0, 0, 0};
+    int64_t stage_launches = 0, stage_frames = 0;
     // pending batch of the queue
     const float2* pend_in[RSP_MAX_F];
     int pend_ids[RSP_MAX_F];
@@ -195,12 +212,18 @@ struct rsp_plan {
 
 rsp_plan::~rsp_plan() {
     (void)hipSetDevice(device);
+    if (kstream) (void)hipStreamSynchronize(kstream);
     for (auto& L : lanes) {
         if (L.stream) (void)hipStreamSynchronize(L.stream);
         if (L.h_dets) (void)hipHostFree(L.h_dets);
         if (L.done) (void)hipEventDestroy(L.done);
+        if (L.kdone) (void)hipEventDestroy(L.kdone);
+        if (L.ready) (void)hipEventDestroy(L.ready);
+        for (auto& e : L.tev)
+            if (e) (void)hipEventDestroy(e);
         if (L.stream) (void)hipStreamDestroy(L.stream);
     }
+    if (kstream) (void)hipStreamDestroy(kstream);
     if (h_stage) (void)hipHostFree(h_stage);
     for (void* p : dev_allocs) (void)hipFree(p);
 }
@@ -351,6 +374,10 @@ int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga,
 int setup_lane(rsp_plan* p, Lane& L) {
     HIPCHK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&L.done, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&L.kdone, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&L.ready, hipEventDisableTiming));
+    for (auto& e : L.tev) HIPCHK(hipEventCreate(&e));
+    L.ks = p->kstream ? p->kstream : L.stream;
     int rc;
     if ((rc = p->dalloc(&L.z, p->z_elems * p->F))) return rc;
     if ((rc = p->dalloc(&L.rdm, p->rdm_elems * p->F))) return rc;
@@ -375,11 +402,24 @@ FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const float2* const* in, i
 }
 
 // Enqueue K1 -> K2 -> K3 for nf frames on lane L, plus the async detection read-back.
-int launch_batch(rsp_plan* p, Lane& L, const float2* const* in, const int* ids, int nf) {
+int launch_batch(rsp_plan* p, Lane& L, const float2* const* in, const int* ids, int nf, bool after_stream = false) {
     const FramePtrs fp = lane_ptrs(p, L, in, nf);
-    HIPCHK(launch_k1(p->g, p->k, fp, nf, 3, p->g.C, L.stream));
-    HIPCHK(launch_k2(p->g, p->k, fp, nf, p->g.B * p->g.P, L.stream));
-    HIPCHK(launch_k3(p->g, p->k, fp, nf, L.stream));
+    if (after_stream && L.ks != L.stream) {   // kernels follow whatever the caller queued on the lane's stream
+        HIPCHK(hipEventRecord(L.ready, L.stream));
+        HIPCHK(hipStreamWaitEvent(L.ks, L.ready, 0));
+    }
+    L.timed = p->time_stages;
+    if (L.timed) HIPCHK(hipEventRecord(L.tev[0], L.ks));
+    HIPCHK(launch_k1(p->g, p->k, fp, nf, 3, p->g.C, L.ks));
+    if (L.timed) HIPCHK(hipEventRecord(L.tev[1], L.ks));
+    HIPCHK(launch_k2(p->g, p->k, fp, nf, p->g.B * p->g.P, L.ks));
+    if (L.timed) HIPCHK(hipEventRecord(L.tev[2], L.ks));
+    HIPCHK(launch_k3(p->g, p->k, fp, nf, L.ks));
+    if (L.timed) HIPCHK(hipEventRecord(L.tev[3], L.ks));
+    if (L.ks != L.stream) {   // read-back on the lane's stream, off the kernel stream
+        HIPCHK(hipEventRecord(L.kdone, L.ks));
+        HIPCHK(hipStreamWaitEvent(L.stream, L.kdone, 0));
+    }
     // one copy: count record + the first async_cap detections of every frame
     HIPCHK(hipMemcpy2DAsync(L.h_dets, sizeof(DevDet) * (p->async_cap + 1), L.dets,
                             sizeof(DevDet) * (p->g.max_dets + 1), sizeof(DevDet) * (p->async_cap + 1), nf,
@@ -396,6 +436,15 @@ int harvest(rsp_plan* p, Lane& L, std::vector<std::vector<rsp_detection>>* keep_
     if (!L.busy) return RSP_OK;
     HIPCHK(hipEventSynchronize(L.done));
     L.busy = false;
+    if (L.timed) {
+        for (int i = 0; i < 3; ++i) {
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, L.tev[i], L.tev[i + 1]));
+            p->stage_ms[i] += ms;
+        }
+        p->stage_launches += 1;
+        p->stage_frames += L.nf;
+    }
     if (keep_dets) keep_dets->assign(L.nf, {});
     for (int f = 0; f < L.nf; ++f) {
         const DevDet* hrec = L.h_dets + (size_t)f * (p->async_cap + 1);
@@ -427,7 +476,7 @@ int flush_pending(rsp_plan* p) {
     if (rc) return rc;
     rc = launch_batch(p, L, p->pend_in, p->pend_ids, p->npend);
     p->npend = 0;
-    p->next_lane = (p->next_lane + 1) % RSP_LANES;
+    p->next_lane = (p->next_lane + 1) % p->nlanes;
     return rc;
 }
 
@@ -435,8 +484,8 @@ int drain_all(rsp_plan* p) {
     int rc = flush_pending(p);
     if (rc) return rc;
     // harvest in launch order: the lane launched first is next_lane
-    for (int q = 0; q < RSP_LANES; ++q) {
-        rc = harvest(p, p->lanes[(p->next_lane + q) % RSP_LANES]);
+    for (int q = 0; q < p->nlanes; ++q) {
+        rc = harvest(p, p->lanes[(p->next_lane + q) % p->nlanes]);
         if (rc) return rc;
     }
     return RSP_OK;
@@ -488,7 +537,7 @@ int run_sync_frame(rsp_plan* p, const float2* d_in, int frame_idx, rsp_frame_out
     const float2* in[1] = {d_in};
     int ids[1] = {frame_idx};
     std::vector<std::vector<rsp_detection>> dets;
-    if ((rc = launch_batch(p, L, in, ids, 1))) return rc;
+    if ((rc = launch_batch(p, L, in, ids, 1, true))) return rc;
     if ((rc = harvest(p, L, &dets))) return rc;
     FrameResult fr = p->results.back();
     p->results.resize(nres);   // synchronous frames do not enter the queue's result list
@@ -744,9 +793,32 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     g.Gp = (G + 3) & ~3;
     p->mag_elems = (size_t)B * P * g.Gp;
     if ((rc = p->dalloc(&p->d_cube, (size_t)std::max(C, B) * N * P))) return bail(rc);
+    {
+        const char* nl = getenv("RSP_NLANES");
+        if (nl) p->nlanes = std::max(1, std::min(RSP_LANES, atoi(nl)));
+        const char* q = getenv("RSP_QUEUE");
+        if (q && !strcmp(q, "serial") && hipStreamCreateWithFlags(&p->kstream, hipStreamNonBlocking) != hipSuccess)
+            return bail(fail(RSP_ERR_DEVICE, "hipStreamCreateWithFlags failed"));
+    }
     for (auto& L : p->lanes)
         if ((rc = setup_lane(p, L))) return bail(rc);
     *out = p;
+    return RSP_OK;
+}
+
+int32_t rsp_set_stage_timing(rsp_plan* p, int32_t on) {
+    if (!p) return fail(RSP_ERR_INVALID, "null plan");
+    p->time_stages = on != 0;
+    for (double& v : p->stage_ms) v = 0;
+    p->stage_launches = p->stage_frames = 0;
+    return RSP_OK;
+}
+
+int32_t rsp_stage_times(const rsp_plan* p, double* ms_sum, int32_t cap, int64_t* launches, int64_t* frames) {
+    if (!p || !ms_sum || cap < 0) return fail(RSP_ERR_INVALID, "bad argument");
+    for (int i = 0; i < std::min(cap, 3); ++i) ms_sum[i] = p->stage_ms[i];
+    if (launches) *launches = p->stage_launches;
+    if (frames) *frames = p->stage_frames;
     return RSP_OK;
 }
 
@@ -909,20 +981,29 @@ int32_t rsp_profile_stages(rsp_plan* p, const void* const* d_cubes, int32_t n_cu
     if (rc) return rc;
     Lane& L = p->lanes[0];
     const int nf = std::min(n_cubes, p->F);
-    const float2* in[RSP_MAX_F];
-    for (int f = 0; f < nf; ++f) in[f] = (const float2*)d_cubes[f];
-    const FramePtrs fp = lane_ptrs(p, L, in, nf);
+    // batches rotate over all n_cubes cubes (cube (j nf + f) mod n_cubes in batch j), so that a
+    // ring larger than the 256 MiB Infinity Cache makes K1 read its input from HBM as in the queue
+    const int nsets = (n_cubes + nf - 1) / nf;
+    std::vector<FramePtrs> fps(nsets);
+    for (int j = 0; j < nsets; ++j) {
+        const float2* in[RSP_MAX_F];
+        for (int f = 0; f < nf; ++f) in[f] = (const float2*)d_cubes[(j * nf + f) % n_cubes];
+        fps[j] = lane_ptrs(p, L, in, nf);
+    }
+    const FramePtrs& fp = fps[0];
     const Geometry& g = p->g;
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
     for (int s = 0; s < 3 && s < cap; ++s) {
+        int it = 0;
         auto run = [&]() -> hipError_t {
-            if (s == 0) return launch_k1(g, p->k, fp, nf, 3, g.C, L.stream);
-            if (s == 1) return launch_k2(g, p->k, fp, nf, g.B * g.P, L.stream);
+            const FramePtrs& fj = fps[it++ % nsets];
+            if (s == 0) return launch_k1(g, p->k, fj, nf, 3, g.C, L.stream);
+            if (s == 1) return launch_k2(g, p->k, fj, nf, g.B * g.P, L.stream);
             // counts are zeroed by K1 in the pipeline; here by a tiny 2-D memset per launch
             hipError_t e = hipMemset2DAsync(L.dets, sizeof(DevDet) * (g.max_dets + 1), 0, sizeof(int), nf, L.stream);
-            return e != hipSuccess ? e : launch_k3(g, p->k, fp, nf, L.stream);
+            return e != hipSuccess ? e : launch_k3(g, p->k, fj, nf, L.stream);
         };
         HIPCHK(run());
         HIPCHK(hipEventRecord(e0, L.stream));

@@ -107,6 +107,9 @@ PROTOTYPES = {
     'rsp_profile_stages': (ct.c_int32, [_P, ct.POINTER(_P), ct.c_int32, ct.c_int32, ct.POINTER(ct.c_float),
                                         ct.POINTER(ct.c_int64), ct.c_int32, ct.POINTER(ct.c_int32)]),
     'rsp_stage_name': (ct.c_char_p, [ct.c_int32]),
+    'rsp_set_stage_timing': (ct.c_int32, [_P, ct.c_int32]),
+    'rsp_stage_times': (ct.c_int32, [_P, ct.POINTER(ct.c_double), ct.c_int32, ct.POINTER(ct.c_int64),
+                                     ct.POINTER(ct.c_int64)]),
     'rsp_cluster_detections': (ct.c_int32, [ct.POINTER(Detection), ct.c_int32, ct.POINTER(ClusterParams),
                                             ct.POINTER(Target), ct.c_int32, ct.POINTER(ct.c_int32)]),
     'rsp_device_alloc': (ct.c_int32, [_P, ct.c_int64, ct.POINTER(_P)]),

@@ -211,6 +211,19 @@ class Plan:
             check(lib().rsp_results_clear(self.h))
         return out
 
+    def set_stage_timing(self, on=True):
+        """Live HIP-event timing of K1/K2/K3 of every queued batch (resets the sums)."""
+        check(lib().rsp_set_stage_timing(self.h, 1 if on else 0))
+
+    def stage_times(self):
+        """Sums of the live stage timing: [{'stage', 'ms_total', 'launches', 'frames'}]."""
+        n = self.sizes.n_stages
+        ms = (ct.c_double * n)()
+        nl, nf = ct.c_int64(), ct.c_int64()
+        check(lib().rsp_stage_times(self.h, ms, n, ct.byref(nl), ct.byref(nf)))
+        return [{'stage': lib().rsp_stage_name(i).decode(), 'ms_total': ms[i], 'launches': nl.value,
+                 'frames': nf.value} for i in range(n)]
+
     def profile_stages(self, d_cubes, iters=20):
         """Per-stage HIP-event timing; d_cubes = device pointer or list of pointers (batched)."""
         if not isinstance(d_cubes, (list, tuple)):

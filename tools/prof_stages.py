@@ -22,7 +22,8 @@ def main():
     cfg, cfar, clus, W, ang, k = C.named_config(name)
     pre = precompute(cfg, W, ang, k, C.V8_FIR)
     plan = Plan(cfg, cfar, clus, pre, frames_per_launch=nf)
-    cubes = [plan.device_alloc(plan.sizes.cube_elems * 8) for _ in range(nf)]
+    # a ring of >= 8 cubes (> the 256 MiB Infinity Cache at x2), rotated over by the launches
+    cubes = [plan.device_alloc(plan.sizes.cube_elems * 8) for _ in range(max(nf, 8))]
     tg = C.v8_2_targets()
     for i, p in enumerate(cubes):
         plan.synthesize_device(p, tg, 1 + i)
