@@ -283,6 +283,66 @@ int32_t rsp_mat_load_frame(const char* path, int32_t dtype, void* cube, int64_t 
 int32_t rsp_mat_save_frame(const char* path, const double* cube, int32_t P, int32_t N, int32_t C,
                            const double* servo_angle, int32_t n_angle, int32_t generation, int32_t compress);
 
+/* ---- MUSIC direction finding (BASELINE config #5) ----
+ * MUSIC_1D.m:21-48 and run_music_algorithm.m:22-69: per instance X [N x K] (complex,
+ * column-major, instances stacked as [N x K x I]):
+ *   R = X*X'/K (MUSIC_1D.m:28); [EV, D] = eig(R), sort 'descend' (:29-32);
+ *   Q_n = EV(:, M+1:N) (:33); P = 1./sum(abs(Q_n'*S1).^2) over the scan grid (:35-37);
+ *   P_dB = 10*log10(P/max(P)) (:39-41); findpeaks(P_dB), the M largest (:43-47).
+ * The reference scripts have no function signature; these entry points take the scripts'
+ * variables (N, K, M, d/lambda, phi_list) as the plan and X as the data.  fp32 on the device
+ * (MFMA covariance, Householder + bisection eigensolver); tolerance vs the fp64 oracle in tests/test_music.py. */
+typedef struct rsp_music_config {
+    int32_t channel_num;      /* N, 2..64 (MUSIC_1D.m:10; BASELINE #5: 64)                 */
+    int32_t num_snapshots;    /* K (MUSIC_1D.m:18; BASELINE #5: 1024)                      */
+    int32_t num_sources;      /* M = signal subspace dimension, 1..min(8, N-1) (:15)       */
+    int32_t n_scan;           /* scan grid length, 3..4096 (MUSIC_1D.m:35: 200)             */
+    double d_over_lambda;     /* element spacing / wavelength (MUSIC_1D.m:11: 0.5)         */
+    const double* scan_rad;   /* phi_list in radians, n_scan entries (borrowed for create) */
+    int32_t max_batch;        /* instances per call (device buffers sized for it)          */
+} rsp_music_config;
+
+/* Synthetic signal model of MUSIC_1D.m:14-24 / run_music_algorithm.m:14-39; MATLAB randn is
+ * replaced by the Philox streams documented in oracle/music.py. */
+typedef struct rsp_music_scene {
+    int32_t n_src;            /* sources, 1..8                                              */
+    int32_t complex_sources;  /* 0: Alpha = randn(M,K) (MUSIC_1D.m:22); 1: (randn+1j*randn)/sqrt(2)
+                                 (run_music_algorithm.m:30-32); both scaled by amplitudes[m] */
+    int32_t snr_measured;     /* 1: awgn(X, SNR, 'measured') (MUSIC_1D.m:24);
+                                 0: noise power 1/10^(SNR/10) (run_music_algorithm.m:35)    */
+    int32_t reserved;
+    double snr_db;
+    double angles_rad[8];     /* phi (MUSIC_1D.m:14)                                        */
+    double amplitudes[8];     /* source_amplitudes (run_music_algorithm.m:15); 1 for MUSIC_1D */
+} rsp_music_scene;
+
+/* Caller-owned outputs for n_inst instances; any pointer may be NULL (not produced). */
+typedef struct rsp_music_out {
+    float* spectrum_db;       /* [n_scan x I] P_MUSIC_dB (MUSIC_1D.m:41)                      */
+    float* eigenvalues;       /* [N x I] descending (MUSIC_1D.m:30-31)                         */
+    int32_t* peak_idx;        /* [M x I] 1-based scan indices of the M largest peaks (:43-47), 0 = none */
+    int32_t* n_peaks;         /* [I] number of findpeaks peaks                                 */
+    double* covariance;       /* complex [N x N x I] R (MUSIC_1D.m:28), column-major           */
+} rsp_music_out;
+
+typedef struct rsp_music_plan rsp_music_plan;
+
+int32_t rsp_music_create(const rsp_music_config* cfg, int32_t device, rsp_music_plan** out);
+int32_t rsp_music_destroy(rsp_music_plan* plan);
+/* Host snapshots X [N x K x n_inst] (RSP_C64 or RSP_C128), synchronous. */
+int32_t rsp_music_process(rsp_music_plan* plan, const void* X, int32_t dtype, int32_t n_inst, rsp_music_out* out);
+/* Device-resident complex64 snapshots; results copied to `out` (NULL: results stay on the device). */
+int32_t rsp_music_process_device(rsp_music_plan* plan, const void* d_X, int32_t n_inst, rsp_music_out* out);
+/* Synthesise n_inst instances (instance ids inst0..) into device memory d_X [N x K x n_inst]. */
+int32_t rsp_music_synthesize_device(rsp_music_plan* plan, const rsp_music_scene* scene, int32_t n_inst,
+                                    int32_t inst0, uint64_t seed, void* d_X);
+/* HIP-event timing of the two device stages (ms_out[0] covariance, ms_out[1] eig + spectrum)
+ * averaged over `iters` launches on the plan's stream. */
+int32_t rsp_music_profile(rsp_music_plan* plan, const void* d_X, int32_t n_inst, int32_t iters, float* ms_out);
+int32_t rsp_music_device_alloc(rsp_music_plan* plan, int64_t bytes, void** d_ptr);
+int32_t rsp_music_device_free(rsp_music_plan* plan, void* d_ptr);
+int32_t rsp_music_device_download(rsp_music_plan* plan, void* h_dst, const void* d_src, int64_t bytes);
+
 #ifdef __cplusplus
 }
 #endif

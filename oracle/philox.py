@@ -39,14 +39,17 @@ def philox4x32_10(c0, c1, c2, c3, k0, k1):
     return c0, c1, c2, c3
 
 
-def unit_normal_complex(n_samples, frame_idx, seed, start=0):
-    """Complex samples I + jQ (each I, Q ~ N(0,1)) for linear indices start..start+n-1."""
+def unit_normal_complex(n_samples, frame_idx, seed, start=0, tag=TAG):
+    """Complex samples I + jQ (each I, Q ~ N(0,1)) for linear indices start..start+n-1.
+
+    ``tag`` is counter word 3 (the stream id): TAG for the echo noise, the MUSIC
+    streams use their own tags (oracle/music.py)."""
     idx = np.arange(start, start + n_samples, dtype=np.uint64)
     pair = idx >> np.uint64(1)
     lo = (pair & MASK32).astype(np.uint32)
     hi = (pair >> np.uint64(32)).astype(np.uint32)
     fr = np.full(lo.shape, frame_idx & 0xFFFFFFFF, np.uint32)
-    tag = np.full(lo.shape, TAG, np.uint32)
+    tag = np.full(lo.shape, tag, np.uint32)
     x0, x1, x2, x3 = philox4x32_10(lo, hi, fr, tag, seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
     odd = (idx & np.uint64(1)).astype(bool)
     ua = np.where(odd, x2, x0).astype(np.float64)

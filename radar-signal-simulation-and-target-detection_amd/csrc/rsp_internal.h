@@ -8,6 +8,23 @@
 #define RSP_K2_POINTS 4096   // complex points per pulse-compression workgroup
 #define RSP_THREADS 256
 
+// Philox4x32-10 (Salmon et al., SC'11) in place on counter c with key (k0, k1); the streams
+// built on it are documented in oracle/philox.py (echo noise) and oracle/music.py (MUSIC).
+__device__ __forceinline__ void rsp_philox10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)M0 * c[0];
+        const uint64_t p1 = (uint64_t)M1 * c[2];
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+        c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
 // Device record of one CFAR detection + its S9 estimate; layout == rsp_detection.
 struct DevDet {
     int32_t v_idx, r_idx, pair_idx, reserved;   // 1-based like fsf:220

@@ -1090,21 +1090,6 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k_mtd_cols(Geometry g, DevCons
 // ======================================================================================
 // S4 + S4.1 on the device: echo synthesis + Philox noise (fsf:45-88)
 // ======================================================================================
-__device__ __forceinline__ void philox10(uint32_t c[4], uint32_t k0, uint32_t k1) {
-    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        const uint64_t p0 = (uint64_t)M0 * c[0];
-        const uint64_t p1 = (uint64_t)M1 * c[2];
-        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
-        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-        const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
-        c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
-        k0 += 0x9E3779B9u;
-        k1 += 0xBB67AE85u;
-    }
-}
-
 __global__ __launch_bounds__(RSP_THREADS) void k_synth(Geometry g, const double* __restrict__ tx,
                                                      const SynthTarget* __restrict__ tg, int nt, int frame_idx,
                                                      uint64_t seed, double nscale, float2* __restrict__ cube) {
@@ -1132,7 +1117,7 @@ __global__ __launch_bounds__(RSP_THREADS) void k_synth(Geometry g, const double*
     // Philox noise (oracle/philox.py documents the stream)
     const uint64_t pairi = (uint64_t)i >> 1;
     uint32_t ctr[4] = {(uint32_t)pairi, (uint32_t)(pairi >> 32), (uint32_t)frame_idx, 0x52535020u};
-    philox10(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+    rsp_philox10(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
     const uint32_t xa = (i & 1) ? ctr[2] : ctr[0];
     const uint32_t xb = (i & 1) ? ctr[3] : ctr[1];
     const double ua = ((double)xa + 0.5) * 2.3283064365386963e-10;

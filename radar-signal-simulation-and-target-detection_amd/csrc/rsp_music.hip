@@ -1,0 +1,798 @@
+// rsp_music.hip -- MUSIC direction finding on gfx950 (BASELINE config #5).
+//
+// Reference: MUSIC_1D.m:21-48 and run_music_algorithm.m:22-69.  Per instance (one snapshot
+// matrix X [N x K], N <= 64 channels):
+//   R = X X^H / K                          (MUSIC_1D.m:28)   k_music_cov   f32 MFMA
+//   [EV, D] = eig(R); sort descend          (MUSIC_1D.m:29-33) k_music_eig   Householder + bisection
+//   P = 1 ./ sum(|Q_n^H S1|.^2); dB          (MUSIC_1D.m:35-41) k_music_eig   (same workgroup)
+//   findpeaks + top M                       (MUSIC_1D.m:43-48) k_music_eig   (same workgroup)
+// plus the synthetic snapshot model of MUSIC_1D.m:21-24 / run_music_algorithm.m:27-39 with the
+// Philox streams documented in oracle/music.py (k_music_synth).
+//
+// Batching: one workgroup per instance in every kernel; BASELINE config #5 runs >= 1024
+// instances per launch so that the 256 CUs are full.
+#include "rsp.h"
+#include "rsp_internal.h"
+
+#include <cmath>
+#include <cstdarg>
+#include <cstring>
+#include <vector>
+
+int rsp_set_error(int code, const char* fmt, ...);   // rsp_plan.cpp
+
+#define MU_NMAX 64
+#define MU_MMAX 8
+#define MU_THREADS 256
+#define MU_LDA (MU_NMAX + 1)   // LDS row stride (complex) of A and V: column walks hit 2 banks apart
+#define MU_SCAN_MAX 4096
+#define MU_TAG_SRC 0x4D555341u     // 'MUSA' (oracle/music.py TAG_SRC)
+#define MU_TAG_NOISE 0x4D55534Eu   // 'MUSN' (oracle/music.py TAG_NOISE)
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Complex N(0,1) pair of linear index i of a Philox stream (oracle/philox.py unit_normal_complex).
+__device__ __forceinline__ double2 mu_normal(uint64_t i, uint32_t inst, uint64_t seed, uint32_t tag) {
+    const uint64_t pr = i >> 1;
+    uint32_t c[4] = {(uint32_t)pr, (uint32_t)(pr >> 32), inst, tag};
+    rsp_philox10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const uint32_t xa = (i & 1) ? c[2] : c[0];
+    const uint32_t xb = (i & 1) ? c[3] : c[1];
+    const double ua = ((double)xa + 0.5) * 2.3283064365386963e-10;
+    const double ub = ((double)xb + 0.5) * 2.3283064365386963e-10;
+    const double r = sqrt(-2.0 * log(ua));
+    double s, co;
+    sincos(2.0 * M_PI * ub, &s, &co);
+    return make_double2(r * co, r * s);
+}
+
+// ---------------------------------------------------------------------------------------
+// Synthetic snapshots (MUSIC_1D.m:21-24, run_music_algorithm.m:27-39), fp64 like MATLAB,
+// stored complex64 [inst][K][N] (MATLAB column-major N x K per instance).  Pass 0 measures
+// the signal power (awgn 'measured'), pass 1 adds the noise and stores.
+// ---------------------------------------------------------------------------------------
+#define MU_SYN_KC 128
+// snr_measured: awgn(X, SNR, 'measured') (MUSIC_1D.m:24), the noise scale follows from pass 0;
+// otherwise nsc_fixed = sqrt(noise_power / 2) (run_music_algorithm.m:35-36) and pass 0 is skipped.
+__global__ __launch_bounds__(MU_THREADS) void k_music_synth(int N, int K, int M, int inst0, uint64_t seed,
+                                                          const double2* __restrict__ Ssrc, const double* __restrict__ amp,
+                                                          int complex_src, int snr_measured, double snr_db,
+                                                          double nsc_fixed, float2* __restrict__ X) {
+    __shared__ double2 al[MU_MMAX][MU_SYN_KC];
+    __shared__ double2 Sl[MU_MMAX][MU_NMAX];
+    __shared__ double red[MU_THREADS];
+    const int tid = threadIdx.x;
+    const uint32_t inst = (uint32_t)(inst0 + blockIdx.x);
+    float2* __restrict__ Xi = X + (size_t)blockIdx.x * K * N;
+    for (int e = tid; e < M * N; e += MU_THREADS) Sl[e / N][e % N] = Ssrc[e];
+    double nsc = nsc_fixed;
+    for (int pass = snr_measured ? 0 : 1; pass < 2; ++pass) {
+        double psum = 0.0;
+        for (int k0 = 0; k0 < K; k0 += MU_SYN_KC) {
+            const int kc = min(MU_SYN_KC, K - k0);
+            __syncthreads();
+            for (int e = tid; e < M * kc; e += MU_THREADS) {   // Alpha(m, k): stream index m + M k
+                const int kk = e / M, m = e - kk * M;
+                const double2 z = mu_normal((uint64_t)m + (uint64_t)M * (k0 + kk), inst, seed, MU_TAG_SRC);
+                al[m][kk] = complex_src ? make_double2(z.x * M_SQRT1_2 * amp[m], z.y * M_SQRT1_2 * amp[m])
+                                        : make_double2(z.x * amp[m], 0.0);
+            }
+            __syncthreads();
+            for (int e = tid; e < N * kc; e += MU_THREADS) {
+                const int kk = e / N, c = e - kk * N;
+                double xr = 0.0, xi = 0.0;
+                for (int m = 0; m < M; ++m) {   // X = S * Alpha (MUSIC_1D.m:23)
+                    const double2 sv = Sl[m][c], a = al[m][kk];
+                    xr += sv.x * a.x - sv.y * a.y;
+                    xi += sv.x * a.y + sv.y * a.x;
+                }
+                if (pass == 0) {
+                    psum += xr * xr + xi * xi;
+                } else {   // noise: stream index c + N k
+                    const uint64_t lin = (uint64_t)c + (uint64_t)N * (k0 + kk);
+                    const double2 z = mu_normal(lin, inst, seed, MU_TAG_NOISE);
+                    Xi[lin] = make_float2((float)(xr + nsc * z.x), (float)(xi + nsc * z.y));
+                }
+            }
+        }
+        if (pass == 0) {   // noise power = mean|X|^2 / 10^(SNR/10)
+            red[tid] = psum;
+            __syncthreads();
+            for (int h = MU_THREADS / 2; h > 0; h >>= 1) {
+                if (tid < h) red[tid] += red[tid + h];
+                __syncthreads();
+            }
+            nsc = sqrt(red[0] / ((double)N * K) / pow(10.0, snr_db / 10.0) / 2.0);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// R = X X^H / K on the f32 matrix cores (MUSIC_1D.m:28).  One workgroup (4 waves) per
+// instance, split-K over the waves (4-snapshot steps interleaved, so the waves stream adjacent
+// 2 KB blocks).  Lane l loads the 4 consecutive channels 4(l&15)..+3 of snapshot 4s + (l>>4):
+// 32 B per lane, 512 B per snapshot.  Channel 4r + I is row r of "virtual block" I, so the
+// same register is the A operand (A[r][kk] = x_I) and the B operand (B[kk][r] = x_I) of
+// v_mfma_f32_16x16x4_f32, and tile (I, J) = sum_k x_I x_J^H holds R[4r+I][4s+J].
+// Hermitian: only the 10 tiles I <= J are accumulated (4 MFMAs each per step:
+// Re += xr xr' + xi xi', Im += xi xr' - xr xi'); the rest is mirrored at the store.
+// ---------------------------------------------------------------------------------------
+template <bool VEC4>
+__global__ __launch_bounds__(MU_THREADS) void k_music_cov(int N, int K, const float2* __restrict__ X,
+                                                        float2* __restrict__ R) {
+    __shared__ float red[10][2][256];   // per tile, Re/Im, D[i][j] row-major
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r = lane & 15, kk = lane >> 4;
+    const float2* __restrict__ Xi = X + (size_t)blockIdx.x * K * N;
+    f32x4 ar[10], ai[10];
+#pragma unroll
+    for (int t = 0; t < 10; ++t) {
+        ar[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        ai[t] = ar[t];
+    }
+    const int nsteps = (K + 3) >> 2;
+    auto load = [&](int s, float (&xr)[4], float (&xi)[4]) {
+        const int k = 4 * s + kk;
+        const int c0 = 4 * r;
+        if (VEC4) {
+            float4 u = make_float4(0.f, 0.f, 0.f, 0.f), v = u;
+            if (k < K && c0 < N) {
+                const float4* p = reinterpret_cast<const float4*>(Xi + (size_t)k * N + c0);
+                u = p[0];
+                v = p[1];
+            }
+            xr[0] = u.x; xi[0] = u.y; xr[1] = u.z; xi[1] = u.w;
+            xr[2] = v.x; xi[2] = v.y; xr[3] = v.z; xi[3] = v.w;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float2 x = make_float2(0.f, 0.f);
+                if (k < K && c0 + i < N) x = Xi[(size_t)k * N + c0 + i];
+                xr[i] = x.x;
+                xi[i] = x.y;
+            }
+        }
+    };
+    auto step = [&](const float (&xr)[4], const float (&xi)[4]) {
+        float nr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) nr[i] = -xr[i];
+        int t = 0;
+#pragma unroll
+        for (int I = 0; I < 4; ++I)
+#pragma unroll
+            for (int J = I; J < 4; ++J, ++t) {
+                ar[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[I], xr[J], ar[t], 0, 0, 0);
+                ar[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xi[I], xi[J], ar[t], 0, 0, 0);
+                ai[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xi[I], xr[J], ai[t], 0, 0, 0);
+                ai[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(nr[I], xi[J], ai[t], 0, 0, 0);
+            }
+    };
+    // software pipeline: the loads of step s + 8 are in flight while step s computes
+    float xr0[4], xi0[4], xr1[4], xi1[4];
+    int s = w;
+    if (s < nsteps) load(s, xr0, xi0);
+    if (s + 4 < nsteps) load(s + 4, xr1, xi1);
+    for (; s + 4 < nsteps; s += 8) {
+        step(xr0, xi0);
+        if (s + 8 < nsteps) load(s + 8, xr0, xi0);
+        step(xr1, xi1);
+        if (s + 12 < nsteps) load(s + 12, xr1, xi1);
+    }
+    if (s < nsteps) step(xr0, xi0);
+    // ordered cross-wave sum (deterministic): wave 0 stores, waves 1..3 add in turn
+    for (int ww = 0; ww < 4; ++ww) {
+        if (w == ww) {
+#pragma unroll
+            for (int t = 0; t < 10; ++t)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int e = (4 * kk + v) * 16 + r;   // D row 4(l>>4)+v, column l&15
+                    if (ww == 0) {
+                        red[t][0][e] = ar[t][v];
+                        red[t][1][e] = ai[t][v];
+                    } else {
+                        red[t][0][e] += ar[t][v];
+                        red[t][1][e] += ai[t][v];
+                    }
+                }
+        }
+        __syncthreads();
+    }
+    // R[inst] column-major with leading dimension 64: R(a, b) at a + 64 b
+    float2* __restrict__ Ri = R + (size_t)blockIdx.x * MU_NMAX * MU_NMAX;
+    const float invK = 1.0f / (float)K;
+    int t = 0;
+    for (int I = 0; I < 4; ++I)
+        for (int J = I; J < 4; ++J, ++t) {
+            const int i = tid >> 4, j = tid & 15;
+            const int a = 4 * i + I, b = 4 * j + J;
+            const float re = red[t][0][tid] * invK, im = red[t][1][tid] * invK;
+            if (a < N && b < N) {
+                Ri[a + MU_NMAX * b] = make_float2(re, im);
+                if (I != J) Ri[b + MU_NMAX * a] = make_float2(re, -im);
+            }
+        }
+}
+
+// ---------------------------------------------------------------------------------------
+// eig + MUSIC spectrum + findpeaks (MUSIC_1D.m:29-48), one workgroup per instance, fp32 in LDS.
+//  1. Householder reduction of the Hermitian R to a real symmetric tridiagonal T = Q^H R Q
+//     (the lower-triangle algorithm of LAPACK zhetd2: reflectors H_k = I - tau_k v_k v_k^H
+//     with real beta_k, so the subdiagonal is real; v_k is kept in column k of A).
+//  2. All N eigenvalues of T by Sturm-count bisection, one thread per eigenvalue index
+//     (EVA, MUSIC_1D.m:29-31, sorted descending).
+//  3. The M signal eigenvectors of T by block inverse iteration on T - lambda I (partial-pivot
+//     tridiagonal LU as LAPACK dlagtf/dlagts, 3 solves, Gram-Schmidt after each), then
+//     q_j = Q y_j by applying the reflectors in reverse order (one wave per vector).
+//  4. sum_j |Q_n^H a|^2 (MUSIC_1D.m:37) = a^H (I - Q_s Q_s^H) a for the unitary eigenvector
+//     matrix [Q_s Q_n]; it is evaluated as the squared norm of the residual a - Q_s (Q_s^H a),
+//     so nothing cancels against |a|^2 = N.
+//  5. P = 1 / den, P_dB = 10 log10(P / max P), findpeaks + the M largest (MUSIC_1D.m:37-47).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ float2 cm(float2 a, float2 b) { return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
+__device__ __forceinline__ float2 cadd2(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csc(float s, float2 a) { return make_float2(s * a.x, s * a.y); }
+__device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
+__device__ __forceinline__ float2 cmc(float2 a, float2 b) {   // conj(a) * b
+    return make_float2(a.x * b.x + a.y * b.y, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+#define MU_ITER 3   // inverse-iteration solves per signal vector
+
+__global__ __launch_bounds__(MU_THREADS) void k_music_eig(int N, int M, int S, const float2* __restrict__ R,
+                                                        const float2* __restrict__ S1T, int Spad,
+                                                        float* __restrict__ spec_db, float* __restrict__ eig_out,
+                                                        int* __restrict__ peaks_out) {
+    __shared__ float2 A[MU_NMAX * MU_LDA];   // R, then the reflectors; then den(s)
+    __shared__ float2 vv[MU_NMAX], pp[MU_NMAX], taus[MU_NMAX], Qs[MU_MMAX][MU_NMAX];
+    __shared__ float dd[MU_NMAX], ee[MU_NMAX], lam[MU_NMAX], Y[MU_MMAX][MU_NMAX];
+    __shared__ float fa[MU_MMAX][MU_NMAX], fb[MU_MMAX][MU_NMAX], fc[MU_MMAX][MU_NMAX], fd[MU_MMAX][MU_NMAX];
+    __shared__ float2 sc[2];
+    __shared__ __attribute__((aligned(8))) float red[MU_THREADS];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int n = N;
+    const float2* __restrict__ Ri = R + (size_t)blockIdx.x * MU_NMAX * MU_NMAX;
+    for (int e = tid; e < n * n; e += MU_THREADS) {   // A(i, j) = R(i, j); R column-major ld 64
+        const int j = e / n, i = e - j * n;
+        A[i * MU_LDA + j] = Ri[i + MU_NMAX * j];
+    }
+    __syncthreads();
+    // ---- 1. tridiagonalisation (zhetd2, lower)
+    const int row = tid >> 2, part = tid & 3;   // (row, column-phase) of the matvec / rank-2 update
+    for (int k = 0; k < n - 1; ++k) {
+        const int m = n - k - 1;   // length of x = A(k+1:n-1, k)
+        if (w == 0) {   // zlarfg: H^H x = beta e1, beta real
+            float xn2 = 0.f;
+            if (lane >= 1 && lane < m) {
+                const float2 x = A[(k + 1 + lane) * MU_LDA + k];
+                xn2 = x.x * x.x + x.y * x.y;
+            }
+            xn2 = wave_sum(xn2);
+            if (lane == 0) {
+                const float2 al = A[(k + 1) * MU_LDA + k];
+                float2 tau = make_float2(0.f, 0.f), scale = make_float2(0.f, 0.f);
+                float beta = al.x;
+                if (xn2 > 0.f || al.y != 0.f) {
+                    beta = -copysignf(sqrtf(al.x * al.x + al.y * al.y + xn2), al.x);
+                    tau = make_float2((beta - al.x) / beta, -al.y / beta);
+                    const float2 dn = make_float2(al.x - beta, al.y);   // 1 / (alpha - beta)
+                    const float q = 1.f / (dn.x * dn.x + dn.y * dn.y);
+                    scale = make_float2(dn.x * q, -dn.y * q);
+                }
+                sc[0] = tau;
+                sc[1] = scale;
+                taus[k] = tau;
+                ee[k] = beta;
+                dd[k] = A[k * MU_LDA + k].x;
+            }
+        }
+        __syncthreads();
+        const float2 tau = sc[0], scale = sc[1];
+        if (tid < m) {
+            float2 v = make_float2(1.f, 0.f);
+            if (tid > 0) {
+                v = cm(A[(k + 1 + tid) * MU_LDA + k], scale);
+                A[(k + 1 + tid) * MU_LDA + k] = v;
+            }
+            vv[tid] = v;
+        }
+        __syncthreads();
+        if (tau.x == 0.f && tau.y == 0.f) continue;   // H = I (uniform)
+        // p = tau A22 v (4 threads per row)
+        float2 acc = make_float2(0.f, 0.f);
+        if (row < m) {
+            const float2* ar = A + (k + 1 + row) * MU_LDA + k + 1;
+            for (int j = part; j < m; j += 4) acc = cadd2(acc, cm(ar[j], vv[j]));
+        }
+        acc.x += __shfl_xor(acc.x, 1);
+        acc.y += __shfl_xor(acc.y, 1);
+        acc.x += __shfl_xor(acc.x, 2);
+        acc.y += __shfl_xor(acc.y, 2);
+        if (part == 0 && row < m) pp[row] = cm(tau, acc);
+        __syncthreads();
+        // alpha = -1/2 tau (p^H v) (every wave computes it), w = p + alpha v
+        float2 t = lane < m ? cmc(pp[lane], vv[lane]) : make_float2(0.f, 0.f);
+        t.x = wave_sum(t.x);
+        t.y = wave_sum(t.y);
+        const float2 alpha = csc(-0.5f, cm(tau, t));
+        // A22 -= v w^H + w v^H
+        if (row < m) {
+            const float2 vi = vv[row], wi = cadd2(pp[row], cm(alpha, vi));
+            float2* ar = A + (k + 1 + row) * MU_LDA + k + 1;
+            for (int j = part; j < m; j += 4) {
+                const float2 vj = vv[j], wj = cadd2(pp[j], cm(alpha, vj));
+                const float2 u = cadd2(cm(vi, cconj(wj)), cm(wi, cconj(vj)));
+                ar[j] = make_float2(ar[j].x - u.x, ar[j].y - u.y);
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) dd[n - 1] = A[(n - 1) * MU_LDA + n - 1].x;
+    __syncthreads();
+    // ---- 2. eigenvalues of T by bisection: thread k -> k-th smallest
+    if (tid < n) {
+        float lo = dd[0], hi = dd[0], tn = 0.f;
+        for (int i = 0; i < n; ++i) {
+            const float r = (i > 0 ? fabsf(ee[i - 1]) : 0.f) + (i < n - 1 ? fabsf(ee[i]) : 0.f);
+            lo = fminf(lo, dd[i] - r);
+            hi = fmaxf(hi, dd[i] + r);
+        }
+        tn = fmaxf(fabsf(lo), fabsf(hi));
+        const float pivmin = 1e-30f * fmaxf(1.f, tn * tn);
+        lo -= 1e-6f * tn + pivmin;
+        hi += 1e-6f * tn + pivmin;
+        for (int it = 0; it < 64 && hi - lo > 2.4e-7f * fmaxf(fabsf(lo), fabsf(hi)) + pivmin; ++it) {
+            const float mid = 0.5f * (lo + hi);
+            int cnt = 0;
+            float q = dd[0] - mid;
+            if (fabsf(q) < pivmin) q = -pivmin;
+            cnt += q < 0.f;
+            for (int i = 1; i < n; ++i) {
+                q = (dd[i] - mid) - ee[i - 1] * ee[i - 1] / q;
+                if (fabsf(q) < pivmin) q = -pivmin;
+                cnt += q < 0.f;
+            }
+            if (cnt > tid) hi = mid; else lo = mid;
+        }
+        const float l = 0.5f * (lo + hi);
+        lam[tid] = l;
+        eig_out[(size_t)blockIdx.x * N + (n - 1 - tid)] = l;   // descending (MUSIC_1D.m:31)
+    }
+    __syncthreads();
+    // ---- 3. signal eigenvectors of T: block inverse iteration
+    float tnorm = 0.f;
+    for (int i = 0; i < n; ++i) tnorm = fmaxf(tnorm, fabsf(dd[i]) + (i > 0 ? fabsf(ee[i - 1]) : 0.f) + (i < n - 1 ? fabsf(ee[i]) : 0.f));
+    const float ptol = 1.2e-7f * tnorm + 1e-30f;
+    if (tid < M) {   // factor T - lambda_j I = P L U (dlagtf)
+        const int j = tid;
+        const float lj = lam[n - 1 - j];
+        float* a = fa[j];   // U diagonal
+        float* b = fb[j];   // U superdiagonal 1
+        float* c = fc[j];   // multipliers (bit 31 of fd = interchange flag kept separately)
+        float* d2 = fd[j];  // U superdiagonal 2
+        for (int i = 0; i < n; ++i) {
+            a[i] = dd[i] - lj;
+            b[i] = i < n - 1 ? ee[i] : 0.f;
+            c[i] = i < n - 1 ? ee[i] : 0.f;
+            d2[i] = 0.f;
+            Y[j][i] = 1.f + 0.0625f * (float)((i * 37 + j * 11) % 17);   // start vector
+        }
+        unsigned long long swp = 0ull;
+        for (int k = 0; k < n - 1; ++k) {
+            if (fabsf(a[k]) >= fabsf(c[k])) {
+                if (fabsf(a[k]) < ptol) a[k] = copysignf(ptol, a[k]);
+                c[k] = c[k] / a[k];
+                a[k + 1] -= c[k] * b[k];
+            } else {
+                swp |= 1ull << k;
+                const float mult = a[k] / c[k];
+                a[k] = c[k];
+                const float tmp = a[k + 1];
+                a[k + 1] = b[k] - mult * tmp;
+                if (k < n - 2) {
+                    d2[k] = b[k + 1];
+                    b[k + 1] = -mult * d2[k];
+                }
+                b[k] = tmp;
+                c[k] = mult;
+            }
+        }
+        if (fabsf(a[n - 1]) < ptol) a[n - 1] = copysignf(ptol, a[n - 1]);
+        reinterpret_cast<unsigned long long*>(red)[j] = swp;
+    }
+    __syncthreads();
+    for (int it = 0; it < MU_ITER; ++it) {
+        if (tid < M) {   // solve (dlagts): forward with the interchanges, then U back-substitution
+            const int j = tid;
+            const unsigned long long swp = reinterpret_cast<unsigned long long*>(red)[j];
+            float* y = Y[j];
+            for (int k = 0; k < n - 1; ++k) {
+                if (swp >> k & 1ull) {
+                    const float t0 = y[k];
+                    y[k] = y[k + 1];
+                    y[k + 1] = t0 - fc[j][k] * y[k];
+                } else {
+                    y[k + 1] -= fc[j][k] * y[k];
+                }
+            }
+            y[n - 1] /= fa[j][n - 1];
+            if (n > 1) y[n - 2] = (y[n - 2] - fb[j][n - 2] * y[n - 1]) / fa[j][n - 2];
+            for (int k = n - 3; k >= 0; --k) y[k] = (y[k] - fb[j][k] * y[k + 1] - fd[j][k] * y[k + 2]) / fa[j][k];
+        }
+        __syncthreads();
+        if (w == 0) {   // modified Gram-Schmidt over the M vectors (lane = component)
+            for (int j = 0; j < M; ++j) {
+                float yj = lane < n ? Y[j][lane] : 0.f;
+                for (int i = 0; i < j; ++i) {
+                    const float yi = lane < n ? Y[i][lane] : 0.f;
+                    const float dot = wave_sum(yi * yj);
+                    yj -= dot * yi;
+                }
+                const float nr = wave_sum(yj * yj);
+                yj *= rsqrtf(nr);
+                if (lane < n) Y[j][lane] = yj;
+            }
+        }
+        __syncthreads();
+    }
+    // q_j = H_0 H_1 ... H_{n-2} y_j (one wave per vector, lane = component)
+    for (int j = w; j < M; j += MU_THREADS / 64) {
+        float2 y = make_float2(lane < n ? Y[j][lane] : 0.f, 0.f);
+        for (int k = n - 2; k >= 0; --k) {
+            const float2 tau = taus[k];
+            const float2 v = lane == k + 1 ? make_float2(1.f, 0.f)
+                                           : (lane > k + 1 && lane < n ? A[lane * MU_LDA + k] : make_float2(0.f, 0.f));
+            float2 dot = cmc(v, y);
+            dot.x = wave_sum(dot.x);
+            dot.y = wave_sum(dot.y);
+            const float2 u = cm(tau, cm(v, dot));
+            y = make_float2(y.x - u.x, y.y - u.y);
+        }
+        if (lane < n) Qs[j][lane] = y;
+    }
+    __syncthreads();
+    // ---- 4. den(s) = |a(s) - Q_s Q_s^H a(s)|^2, one thread per angle (A's LDS holds den)
+    float* den = reinterpret_cast<float*>(A);
+    for (int s = tid; s < S; s += MU_THREADS) {
+        float2 cf[MU_MMAX];
+#pragma unroll
+        for (int m = 0; m < MU_MMAX; ++m) cf[m] = make_float2(0.f, 0.f);
+        for (int c = 0; c < n; ++c) {
+            const float2 a = S1T[(size_t)c * Spad + s];
+#pragma unroll
+            for (int m = 0; m < MU_MMAX; ++m)
+                if (m < M) cf[m] = cadd2(cf[m], cmc(Qs[m][c], a));
+        }
+        float r2 = 0.f;
+        for (int c = 0; c < n; ++c) {
+            float2 r = S1T[(size_t)c * Spad + s];
+#pragma unroll
+            for (int m = 0; m < MU_MMAX; ++m)
+                if (m < M) {
+                    const float2 u = cm(Qs[m][c], cf[m]);
+                    r = make_float2(r.x - u.x, r.y - u.y);
+                }
+            r2 += r.x * r.x + r.y * r.y;
+        }
+        den[s] = r2;
+    }
+    __syncthreads();
+    // P = 1 ./ den, P_dB = 10 log10(P / max P) (MUSIC_1D.m:37-41)
+    float pmax = 0.f;
+    for (int s = tid; s < S; s += MU_THREADS) pmax = fmaxf(pmax, 1.f / den[s]);
+    red[tid] = pmax;
+    __syncthreads();
+    for (int h = MU_THREADS / 2; h > 0; h >>= 1) {
+        if (tid < h) red[tid] = fmaxf(red[tid], red[tid + h]);
+        __syncthreads();
+    }
+    pmax = red[0];
+    float* __restrict__ out = spec_db + (size_t)blockIdx.x * S;
+    for (int s = tid; s < S; s += MU_THREADS) {
+        const float db = 10.f * log10f((1.f / den[s]) / pmax);
+        den[s] = db;
+        out[s] = db;
+    }
+    __syncthreads();
+    // findpeaks (first sample of a flat top, ends excluded) + the M largest, stable (MUSIC_1D.m:43-47)
+    if (tid == 0) {
+        int best[MU_MMAX];
+        float bval[MU_MMAX];
+        int nb = 0, npk = 0;
+        int prev = 0;   // index of the previous distinct value
+        int t = 1;
+        while (t < S && den[t] == den[0]) ++t;
+        while (t < S) {
+            int u = t + 1;
+            while (u < S && den[u] == den[t]) ++u;   // [t, u) run of equal values
+            if (u < S && den[t] > den[prev] && den[t] > den[u]) {
+                ++npk;
+                const float v = den[t];
+                int pos = nb;
+                while (pos > 0 && v > bval[pos - 1]) --pos;   // strict: earlier index wins ties
+                if (pos < M) {
+                    for (int i = min(nb, M - 1); i > pos; --i) {
+                        best[i] = best[i - 1];
+                        bval[i] = bval[i - 1];
+                    }
+                    best[pos] = t;
+                    bval[pos] = v;
+                    if (nb < M) ++nb;
+                }
+            }
+            prev = t;
+            t = u;
+        }
+        int* po = peaks_out + (size_t)blockIdx.x * (MU_MMAX + 1);
+        po[0] = npk;
+        for (int i = 0; i < MU_MMAX; ++i) po[1 + i] = i < nb ? best[i] + 1 : 0;
+    }
+}
+
+}  // namespace
+
+// =======================================================================================
+// Host side: plan + C-ABI (include/rsp.h, MUSIC section)
+// =======================================================================================
+struct rsp_music_plan {
+    int device = 0;
+    int N = 0, K = 0, M = 0, S = 0, Spad = 0, max_batch = 0;
+    double dl = 0.0;
+    hipStream_t stream = nullptr;
+    float2* d_S1T = nullptr;     // steering table [64][Spad], zero rows for c >= N
+    float2* d_R = nullptr;       // [max_batch][64][64]
+    float2* d_X = nullptr;       // host-path staging [max_batch][K][N] (lazy)
+    float* d_spec = nullptr;     // [max_batch][S]
+    float* d_eig = nullptr;      // [max_batch][N]
+    int* d_peaks = nullptr;      // [max_batch][MU_MMAX + 1]
+    double2* d_src = nullptr;    // synthesis: source steering [MU_MMAX][N]
+    double* d_amp = nullptr;     // [MU_MMAX]
+    hipEvent_t ev[4] = {};
+};
+
+namespace {
+
+#define MUCHK(expr)                                                                                    \
+    do {                                                                                               \
+        hipError_t e_ = (expr);                                                                        \
+        if (e_ != hipSuccess)                                                                          \
+            return rsp_set_error(RSP_ERR_DEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                                 __FILE__, __LINE__);                                                  \
+    } while (0)
+
+int music_run(rsp_music_plan* p, const float2* dX, int n_inst, bool timed, float* ms) {
+    if (n_inst < 1 || n_inst > p->max_batch)
+        return rsp_set_error(RSP_ERR_INVALID, "n_inst %d outside 1..max_batch %d", n_inst, p->max_batch);
+    MUCHK(hipSetDevice(p->device));
+    if (timed) MUCHK(hipEventRecord(p->ev[0], p->stream));
+    if (p->N % 4 == 0)
+        hipLaunchKernelGGL(k_music_cov<true>, dim3(n_inst), dim3(MU_THREADS), 0, p->stream, p->N, p->K, dX, p->d_R);
+    else
+        hipLaunchKernelGGL(k_music_cov<false>, dim3(n_inst), dim3(MU_THREADS), 0, p->stream, p->N, p->K, dX, p->d_R);
+    MUCHK(hipGetLastError());
+    if (timed) MUCHK(hipEventRecord(p->ev[1], p->stream));
+    hipLaunchKernelGGL(k_music_eig, dim3(n_inst), dim3(MU_THREADS), 0, p->stream, p->N, p->M, p->S, p->d_R, p->d_S1T,
+                       p->Spad, p->d_spec, p->d_eig, p->d_peaks);
+    MUCHK(hipGetLastError());
+    if (timed) {
+        MUCHK(hipEventRecord(p->ev[2], p->stream));
+        MUCHK(hipEventSynchronize(p->ev[2]));
+        MUCHK(hipEventElapsedTime(&ms[0], p->ev[0], p->ev[1]));
+        MUCHK(hipEventElapsedTime(&ms[1], p->ev[1], p->ev[2]));
+    }
+    return RSP_OK;
+}
+
+int music_fetch(rsp_music_plan* p, int n_inst, rsp_music_out* out) {
+    if (!out) return RSP_OK;
+    const int N = p->N, M = p->M, S = p->S;
+    if (out->spectrum_db)
+        MUCHK(hipMemcpyAsync(out->spectrum_db, p->d_spec, (size_t)n_inst * S * sizeof(float), hipMemcpyDeviceToHost, p->stream));
+    if (out->eigenvalues)
+        MUCHK(hipMemcpyAsync(out->eigenvalues, p->d_eig, (size_t)n_inst * N * sizeof(float), hipMemcpyDeviceToHost, p->stream));
+    std::vector<int> pk;
+    if (out->peak_idx || out->n_peaks) {
+        pk.resize((size_t)n_inst * (MU_MMAX + 1));
+        MUCHK(hipMemcpyAsync(pk.data(), p->d_peaks, pk.size() * sizeof(int), hipMemcpyDeviceToHost, p->stream));
+    }
+    std::vector<float2> rc;
+    if (out->covariance) {
+        rc.resize((size_t)n_inst * MU_NMAX * MU_NMAX);
+        MUCHK(hipMemcpyAsync(rc.data(), p->d_R, rc.size() * sizeof(float2), hipMemcpyDeviceToHost, p->stream));
+    }
+    MUCHK(hipStreamSynchronize(p->stream));
+    for (int i = 0; i < n_inst && !pk.empty(); ++i) {
+        if (out->n_peaks) out->n_peaks[i] = pk[(size_t)i * (MU_MMAX + 1)];
+        if (out->peak_idx)
+            for (int m = 0; m < M; ++m) out->peak_idx[(size_t)i * M + m] = pk[(size_t)i * (MU_MMAX + 1) + 1 + m];
+    }
+    if (out->covariance)   // N x N column-major complex double per instance
+        for (int i = 0; i < n_inst; ++i)
+            for (int b = 0; b < N; ++b)
+                for (int a = 0; a < N; ++a) {
+                    const float2 v = rc[(size_t)i * MU_NMAX * MU_NMAX + a + MU_NMAX * b];
+                    double* o = out->covariance + 2 * ((size_t)i * N * N + a + (size_t)N * b);
+                    o[0] = v.x;
+                    o[1] = v.y;
+                }
+    return RSP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t rsp_music_create(const rsp_music_config* cfg, int32_t device, rsp_music_plan** out) {
+    if (!cfg || !out || !cfg->scan_rad) return rsp_set_error(RSP_ERR_INVALID, "null argument");
+    *out = nullptr;
+    const int N = cfg->channel_num, K = cfg->num_snapshots, M = cfg->num_sources, S = cfg->n_scan;
+    if (N < 2 || N > MU_NMAX) return rsp_set_error(RSP_ERR_UNSUPPORTED, "channel_num %d outside 2..%d", N, MU_NMAX);
+    if (M < 1 || M >= N || M > MU_MMAX)
+        return rsp_set_error(RSP_ERR_UNSUPPORTED, "num_sources %d outside 1..min(%d, channel_num-1)", M, MU_MMAX);
+    if (K < 1) return rsp_set_error(RSP_ERR_INVALID, "num_snapshots %d < 1", K);
+    if (S < 3 || S > MU_SCAN_MAX) return rsp_set_error(RSP_ERR_UNSUPPORTED, "n_scan %d outside 3..%d", S, MU_SCAN_MAX);
+    if (cfg->max_batch < 1) return rsp_set_error(RSP_ERR_INVALID, "max_batch %d < 1", cfg->max_batch);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        return rsp_set_error(RSP_ERR_DEVICE, "HIP device %d not available (%d devices)", device, ndev);
+    rsp_music_plan* p = new rsp_music_plan();
+    p->device = device;
+    p->N = N; p->K = K; p->M = M; p->S = S; p->Spad = (S + 7) & ~3;
+    p->max_batch = cfg->max_batch;
+    p->dl = cfg->d_over_lambda;
+    auto bail = [&](int rc) { rsp_music_destroy(p); return rc; };
+    if (hipSetDevice(device) != hipSuccess) return bail(rsp_set_error(RSP_ERR_DEVICE, "hipSetDevice(%d)", device));
+    if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(rsp_set_error(RSP_ERR_DEVICE, "hipStreamCreate failed"));
+    for (auto& e : p->ev)
+        if (hipEventCreate(&e) != hipSuccess) return bail(rsp_set_error(RSP_ERR_DEVICE, "hipEventCreate failed"));
+    const size_t B = (size_t)p->max_batch;
+    struct { void** ptr; size_t bytes; } allocs[] = {
+        {(void**)&p->d_S1T, (size_t)MU_NMAX * p->Spad * sizeof(float2)},
+        {(void**)&p->d_R, B * MU_NMAX * MU_NMAX * sizeof(float2)},
+        {(void**)&p->d_spec, B * S * sizeof(float)},
+        {(void**)&p->d_eig, B * N * sizeof(float)},
+        {(void**)&p->d_peaks, B * (MU_MMAX + 1) * sizeof(int)},
+        {(void**)&p->d_src, (size_t)MU_MMAX * MU_NMAX * sizeof(double2)},
+        {(void**)&p->d_amp, (size_t)MU_MMAX * sizeof(double)},
+    };
+    for (auto& a : allocs)
+        if (hipMalloc(a.ptr, a.bytes) != hipSuccess)
+            return bail(rsp_set_error(RSP_ERR_NOMEM, "hipMalloc(%zu bytes) failed", a.bytes));
+    // S1 = exp(1j k z sin(phi_list')) (MUSIC_1D.m:36), fp64 then rounded; stored transposed
+    // [channel][angle] so a thread's 4 consecutive angles are one 32 B load
+    std::vector<float2> s1((size_t)MU_NMAX * p->Spad, make_float2(0.f, 0.f));
+    for (int c = 0; c < N; ++c)
+        for (int s = 0; s < S; ++s) {
+            const double ph = 2.0 * M_PI * p->dl * c * std::sin(cfg->scan_rad[s]);
+            s1[(size_t)c * p->Spad + s] = make_float2((float)std::cos(ph), (float)std::sin(ph));
+        }
+    if (hipMemcpy(p->d_S1T, s1.data(), s1.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess)
+        return bail(rsp_set_error(RSP_ERR_DEVICE, "steering upload failed"));
+    *out = p;
+    return RSP_OK;
+}
+
+int32_t rsp_music_destroy(rsp_music_plan* p) {
+    if (!p) return RSP_OK;
+    (void)hipSetDevice(p->device);
+    if (p->stream) (void)hipStreamSynchronize(p->stream);
+    void* bufs[] = {p->d_S1T, p->d_R, p->d_X, p->d_spec, p->d_eig, p->d_peaks, p->d_src, p->d_amp};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    for (auto& e : p->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (p->stream) (void)hipStreamDestroy(p->stream);
+    delete p;
+    return RSP_OK;
+}
+
+int32_t rsp_music_synthesize_device(rsp_music_plan* p, const rsp_music_scene* sc, int32_t n_inst, int32_t inst0,
+                                    uint64_t seed, void* d_X) {
+    if (!p || !sc || !d_X) return rsp_set_error(RSP_ERR_INVALID, "null argument");
+    if (sc->n_src < 1 || sc->n_src > MU_MMAX)
+        return rsp_set_error(RSP_ERR_UNSUPPORTED, "n_src %d outside 1..%d", sc->n_src, MU_MMAX);
+    if (n_inst < 1) return rsp_set_error(RSP_ERR_INVALID, "n_inst %d < 1", n_inst);
+    MUCHK(hipSetDevice(p->device));
+    const int N = p->N, Ms = sc->n_src;
+    std::vector<double2> src((size_t)Ms * N);
+    for (int m = 0; m < Ms; ++m)   // S = exp(1j k z sin(phi')) (MUSIC_1D.m:21)
+        for (int c = 0; c < N; ++c) {
+            const double ph = 2.0 * M_PI * p->dl * c * std::sin(sc->angles_rad[m]);
+            src[(size_t)m * N + c] = make_double2(std::cos(ph), std::sin(ph));
+        }
+    double amp[MU_MMAX];
+    for (int m = 0; m < MU_MMAX; ++m) amp[m] = m < Ms ? sc->amplitudes[m] : 0.0;
+    MUCHK(hipMemcpyAsync(p->d_src, src.data(), src.size() * sizeof(double2), hipMemcpyHostToDevice, p->stream));
+    MUCHK(hipMemcpyAsync(p->d_amp, amp, sizeof amp, hipMemcpyHostToDevice, p->stream));
+    const double nsc_fixed = std::sqrt(1.0 / std::pow(10.0, sc->snr_db / 10.0) / 2.0);
+    hipLaunchKernelGGL(k_music_synth, dim3(n_inst), dim3(MU_THREADS), 0, p->stream, N, p->K, Ms, inst0, seed,
+                       p->d_src, p->d_amp, sc->complex_sources, sc->snr_measured ? 1 : 0, sc->snr_db, nsc_fixed,
+                       (float2*)d_X);
+    MUCHK(hipGetLastError());
+    MUCHK(hipStreamSynchronize(p->stream));   // the host staging above is stack memory
+    return RSP_OK;
+}
+
+int32_t rsp_music_process_device(rsp_music_plan* p, const void* d_X, int32_t n_inst, rsp_music_out* out) {
+    if (!p || !d_X) return rsp_set_error(RSP_ERR_INVALID, "null argument");
+    int rc = music_run(p, (const float2*)d_X, n_inst, false, nullptr);
+    if (rc) return rc;
+    if (!out) {
+        MUCHK(hipStreamSynchronize(p->stream));
+        return RSP_OK;
+    }
+    return music_fetch(p, n_inst, out);
+}
+
+int32_t rsp_music_process(rsp_music_plan* p, const void* X, int32_t dtype, int32_t n_inst, rsp_music_out* out) {
+    if (!p || !X) return rsp_set_error(RSP_ERR_INVALID, "null argument");
+    if (n_inst < 1 || n_inst > p->max_batch)
+        return rsp_set_error(RSP_ERR_INVALID, "n_inst %d outside 1..max_batch %d", n_inst, p->max_batch);
+    if (dtype != RSP_C64 && dtype != RSP_C128) return rsp_set_error(RSP_ERR_INVALID, "unknown dtype %d", dtype);
+    MUCHK(hipSetDevice(p->device));
+    const size_t elems = (size_t)n_inst * p->K * p->N;
+    if (!p->d_X) {
+        const size_t bytes = (size_t)p->max_batch * p->K * p->N * sizeof(float2);
+        if (hipMalloc(&p->d_X, bytes) != hipSuccess)
+            return rsp_set_error(RSP_ERR_NOMEM, "hipMalloc(%zu bytes) failed", bytes);
+    }
+    if (dtype == RSP_C64) {
+        MUCHK(hipMemcpy(p->d_X, X, elems * sizeof(float2), hipMemcpyHostToDevice));
+    } else {
+        std::vector<float2> h(elems);
+        const double* x = (const double*)X;
+        for (size_t i = 0; i < elems; ++i) h[i] = make_float2((float)x[2 * i], (float)x[2 * i + 1]);
+        MUCHK(hipMemcpy(p->d_X, h.data(), elems * sizeof(float2), hipMemcpyHostToDevice));
+    }
+    return rsp_music_process_device(p, p->d_X, n_inst, out);
+}
+
+int32_t rsp_music_profile(rsp_music_plan* p, const void* d_X, int32_t n_inst, int32_t iters, float* ms_out) {
+    if (!p || !d_X || !ms_out || iters < 1) return rsp_set_error(RSP_ERR_INVALID, "bad argument");
+    double acc[2] = {0.0, 0.0};
+    for (int it = 0; it < iters; ++it) {
+        float ms[2];
+        int rc = music_run(p, (const float2*)d_X, n_inst, true, ms);
+        if (rc) return rc;
+        acc[0] += ms[0];
+        acc[1] += ms[1];
+    }
+    ms_out[0] = (float)(acc[0] / iters);
+    ms_out[1] = (float)(acc[1] / iters);
+    return RSP_OK;
+}
+
+int32_t rsp_music_device_alloc(rsp_music_plan* p, int64_t bytes, void** d_ptr) {
+    if (!p || !d_ptr || bytes <= 0) return rsp_set_error(RSP_ERR_INVALID, "bad argument");
+    MUCHK(hipSetDevice(p->device));
+    if (hipMalloc(d_ptr, (size_t)bytes) != hipSuccess)
+        return rsp_set_error(RSP_ERR_NOMEM, "hipMalloc(%lld bytes) failed", (long long)bytes);
+    return RSP_OK;
+}
+
+int32_t rsp_music_device_free(rsp_music_plan* p, void* d_ptr) {
+    if (!p) return rsp_set_error(RSP_ERR_INVALID, "null plan");
+    MUCHK(hipSetDevice(p->device));
+    MUCHK(hipStreamSynchronize(p->stream));
+    MUCHK(hipFree(d_ptr));
+    return RSP_OK;
+}
+
+int32_t rsp_music_device_download(rsp_music_plan* p, void* h_dst, const void* d_src, int64_t bytes) {
+    if (!p || !h_dst || !d_src || bytes < 0) return rsp_set_error(RSP_ERR_INVALID, "bad argument");
+    MUCHK(hipSetDevice(p->device));
+    MUCHK(hipStreamSynchronize(p->stream));
+    MUCHK(hipMemcpy(h_dst, d_src, (size_t)bytes, hipMemcpyDeviceToHost));
+    return RSP_OK;
+}
+
+}  // extern "C"

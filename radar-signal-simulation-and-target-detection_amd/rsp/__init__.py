@@ -19,6 +19,7 @@ from .precompute import precompute
 from .plan import Plan
 from ._abi import RspError
 from .matio import load_frame, save_frame
+from .music import MusicPlan, MUSIC_1D
 from . import matio
 
 _PLANS = {}

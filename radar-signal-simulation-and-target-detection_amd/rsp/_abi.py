@@ -84,6 +84,22 @@ class MatWVar(ct.Structure):
                 ('dims', ct.POINTER(ct.c_int64)), ('data', ct.c_void_p)]
 
 
+class MusicConfig(ct.Structure):
+    _fields_ = [('channel_num', ct.c_int32), ('num_snapshots', ct.c_int32), ('num_sources', ct.c_int32),
+                ('n_scan', ct.c_int32), ('d_over_lambda', ct.c_double), ('scan_rad', _dp), ('max_batch', ct.c_int32)]
+
+
+class MusicScene(ct.Structure):
+    _fields_ = [('n_src', ct.c_int32), ('complex_sources', ct.c_int32), ('snr_measured', ct.c_int32),
+                ('reserved', ct.c_int32), ('snr_db', ct.c_double), ('angles_rad', ct.c_double * 8),
+                ('amplitudes', ct.c_double * 8)]
+
+
+class MusicOut(ct.Structure):
+    _fields_ = [('spectrum_db', ct.POINTER(ct.c_float)), ('eigenvalues', ct.POINTER(ct.c_float)),
+                ('peak_idx', ct.POINTER(ct.c_int32)), ('n_peaks', ct.POINTER(ct.c_int32)), ('covariance', _dp)]
+
+
 _P = ct.c_void_p
 PROTOTYPES = {
     'rsp_abi_version': (ct.c_int32, []),
@@ -124,6 +140,15 @@ PROTOTYPES = {
                                         ct.c_int32, ct.POINTER(ct.c_int32)]),
     'rsp_mat_save_frame': (ct.c_int32, [ct.c_char_p, _dp, ct.c_int32, ct.c_int32, ct.c_int32, _dp, ct.c_int32,
                                         ct.c_int32, ct.c_int32]),
+    'rsp_music_create': (ct.c_int32, [ct.POINTER(MusicConfig), ct.c_int32, ct.POINTER(_P)]),
+    'rsp_music_destroy': (ct.c_int32, [_P]),
+    'rsp_music_process': (ct.c_int32, [_P, _P, ct.c_int32, ct.c_int32, ct.POINTER(MusicOut)]),
+    'rsp_music_process_device': (ct.c_int32, [_P, _P, ct.c_int32, ct.POINTER(MusicOut)]),
+    'rsp_music_synthesize_device': (ct.c_int32, [_P, ct.POINTER(MusicScene), ct.c_int32, ct.c_int32, ct.c_uint64, _P]),
+    'rsp_music_profile': (ct.c_int32, [_P, _P, ct.c_int32, ct.c_int32, ct.POINTER(ct.c_float)]),
+    'rsp_music_device_alloc': (ct.c_int32, [_P, ct.c_int64, ct.POINTER(_P)]),
+    'rsp_music_device_free': (ct.c_int32, [_P, _P]),
+    'rsp_music_device_download': (ct.c_int32, [_P, _P, _P, ct.c_int64]),
 }
 
 _lib = None

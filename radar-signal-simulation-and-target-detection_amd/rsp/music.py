@@ -1,0 +1,134 @@
+"""MUSIC direction finding on the device (MUSIC_1D.m:21-48, run_music_algorithm.m:22-69).
+
+``MusicPlan`` binds the ``rsp_music_*`` C-ABI (include/rsp.h): the scripts' parameters
+(N channels, K snapshots, M sources, element spacing / wavelength, scan grid phi_list) make the
+plan; ``process`` runs a batch of snapshot matrices X [N x K] through
+
+  R = X X^H / K -> eig, sort descend -> Q_n -> P(phi) = 1/sum|Q_n^H a(phi)|^2 -> P_dB -> findpeaks
+
+and returns what the scripts compute: ``P_MUSIC_dB``, the sorted eigenvalues ``EVA``, the M
+peak indices / angles ``phi_e`` (MUSIC_1D.m:48).  ``MUSIC_1D(X, ...)`` is the one-instance
+form of MUSIC_1D.m.  All compute runs in librsp.so; there is no CPU path.
+"""
+import ctypes as ct
+
+import numpy as np
+
+from . import _abi
+
+
+class MusicPlan:
+    def __init__(self, channel_num, num_snapshots, num_sources, scan_rad, d_over_lambda=0.5, max_batch=1,
+                 device=0):
+        self._lib = _abi.lib()
+        self.scan_rad = np.ascontiguousarray(scan_rad, np.float64)
+        self.N, self.K, self.M, self.S = int(channel_num), int(num_snapshots), int(num_sources), len(self.scan_rad)
+        self.max_batch = int(max_batch)
+        cfg = _abi.MusicConfig(self.N, self.K, self.M, self.S, float(d_over_lambda),
+                               self.scan_rad.ctypes.data_as(_abi._dp), self.max_batch)
+        h = ct.c_void_p()
+        _abi.check(self._lib.rsp_music_create(ct.byref(cfg), int(device), ct.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, '_h', None):
+            self._lib.rsp_music_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- outputs -------------------------------------------------------------------------
+    def _out(self, n, want_cov):
+        o = {'spectrum_db': np.zeros((n, self.S), np.float32), 'eig': np.zeros((n, self.N), np.float32),
+             'peaks': np.zeros((n, self.M), np.int32), 'n_peaks': np.zeros(n, np.int32)}
+        if want_cov:
+            o['R'] = np.zeros((n, self.N, self.N, 2), np.float64)   # per instance: [b][a] = R(a, b)
+        st = _abi.MusicOut(o['spectrum_db'].ctypes.data_as(ct.POINTER(ct.c_float)),
+                           o['eig'].ctypes.data_as(ct.POINTER(ct.c_float)),
+                           o['peaks'].ctypes.data_as(ct.POINTER(ct.c_int32)),
+                           o['n_peaks'].ctypes.data_as(ct.POINTER(ct.c_int32)),
+                           o['R'].ctypes.data_as(_abi._dp) if want_cov else None)
+        return o, st
+
+    def _finish(self, o):
+        if 'R' in o:
+            r = o.pop('R')
+            o['R'] = np.ascontiguousarray(np.transpose(r[..., 0] + 1j * r[..., 1], (0, 2, 1)))
+        pk = o['peaks']
+        o['angles_deg'] = np.where(pk > 0, self.scan_rad[np.maximum(pk - 1, 0)] * 180.0 / np.pi, np.nan)
+        return o
+
+    def process(self, X, want_cov=False):
+        """X: complex [n, N, K] (or [N, K]) host snapshots -> dict of per-instance outputs."""
+        X = np.asarray(X)
+        if X.ndim == 2:
+            X = X[None]
+        n = X.shape[0]
+        if X.shape[1:] != (self.N, self.K):
+            raise ValueError('X must be [n, %d, %d], got %s' % (self.N, self.K, X.shape))
+        # MATLAB column-major N x K per instance == C-order [n][K][N]
+        if X.dtype == np.complex64:
+            buf, dt = np.ascontiguousarray(np.transpose(X, (0, 2, 1))), _abi.RSP_C64
+        else:
+            buf, dt = np.ascontiguousarray(np.transpose(X.astype(np.complex128), (0, 2, 1))), _abi.RSP_C128
+        o, st = self._out(n, want_cov)
+        _abi.check(self._lib.rsp_music_process(self._h, buf.ctypes.data, dt, n, ct.byref(st)))
+        return self._finish(o)
+
+    # ---- device-resident path (bench) ------------------------------------------------------
+    def device_alloc(self, n_inst):
+        p = ct.c_void_p()
+        _abi.check(self._lib.rsp_music_device_alloc(self._h, n_inst * self.N * self.K * 8, ct.byref(p)))
+        return p.value
+
+    def device_free(self, p):
+        _abi.check(self._lib.rsp_music_device_free(self._h, ct.c_void_p(p)))
+
+    def download(self, d_X, n_inst):
+        h = np.zeros((n_inst, self.K, self.N), np.complex64)
+        _abi.check(self._lib.rsp_music_device_download(self._h, h.ctypes.data, ct.c_void_p(d_X), h.nbytes))
+        return np.ascontiguousarray(np.transpose(h, (0, 2, 1)))
+
+    def synthesize_device(self, d_X, scene, n_inst, inst0=0, seed=20250101):
+        ang = list(scene['angles_rad'])
+        amp = list(scene.get('amplitudes', [1.0] * len(ang)))
+        sc = _abi.MusicScene(len(ang), int(scene.get('complex_sources', 0)), int(scene.get('snr_measured', 1)), 0,
+                             float(scene['snr_db']), (ct.c_double * 8)(*ang), (ct.c_double * 8)(*amp))
+        _abi.check(self._lib.rsp_music_synthesize_device(self._h, ct.byref(sc), n_inst, inst0, ct.c_uint64(seed),
+                                                         ct.c_void_p(d_X)))
+
+    def process_device(self, d_X, n_inst, fetch=True, want_cov=False):
+        if not fetch:
+            _abi.check(self._lib.rsp_music_process_device(self._h, ct.c_void_p(d_X), n_inst, None))
+            return None
+        o, st = self._out(n_inst, want_cov)
+        _abi.check(self._lib.rsp_music_process_device(self._h, ct.c_void_p(d_X), n_inst, ct.byref(st)))
+        return self._finish(o)
+
+    def peaks_device(self, d_X, n_inst, peaks, n_peaks):
+        """Device run returning only the peak indices (into caller arrays): the bench's step."""
+        st = _abi.MusicOut(None, None, peaks.ctypes.data_as(ct.POINTER(ct.c_int32)),
+                           n_peaks.ctypes.data_as(ct.POINTER(ct.c_int32)), None)
+        _abi.check(self._lib.rsp_music_process_device(self._h, ct.c_void_p(d_X), n_inst, ct.byref(st)))
+
+    def profile(self, d_X, n_inst, iters=20):
+        ms = (ct.c_float * 2)()
+        _abi.check(self._lib.rsp_music_profile(self._h, ct.c_void_p(d_X), n_inst, iters, ms))
+        return {'cov_ms': ms[0], 'eig_ms': ms[1]}
+
+
+def MUSIC_1D(X1, M, phi_list=None, d_over_lambda=0.5, device=0):
+    """MUSIC_1D.m:26-48 on one snapshot matrix X1 [N x K]: returns (phi_e [deg], P_MUSIC_dB, EVA)."""
+    X1 = np.asarray(X1)
+    if phi_list is None:
+        phi_list = np.linspace(-np.pi / 2, np.pi / 2, 200)   # MUSIC_1D.m:35
+    plan = MusicPlan(X1.shape[0], X1.shape[1], M, phi_list, d_over_lambda, max_batch=1, device=device)
+    try:
+        o = plan.process(X1)
+    finally:
+        plan.close()
+    return o['angles_deg'][0], o['spectrum_db'][0], o['eig'][0]

@@ -1,0 +1,169 @@
+"""MUSIC DOA (MUSIC_1D.m:21-48, run_music_algorithm.m:22-69; SURVEY 8(f) rank 1, BASELINE #5).
+
+CPU tests pin the oracle (oracle/music.py) by known answers the scripts themselves imply;
+GPU tests compare librsp's MUSIC path (f32 MFMA covariance, fp32 Jacobi eig, spectrum,
+findpeaks) with the fp64 oracle on identical snapshots.
+
+Tolerances (device fp32 vs oracle fp64), written here:
+  * synthesis: max |X_dev - X_oracle| <= 1e-6 * max |X_oracle| (fp64 on both sides, one fp32 rounding);
+  * covariance: max |R_dev - R| <= 2e-6 * max |R| (R from the same fp32 snapshots);
+  * eigenvalues: max |d_dev - d| <= 2e-5 * max d;
+  * spectrum: |dB_dev - dB| <= 0.02 dB wherever the oracle is above -60 dB;
+  * peaks: the same M indices, except that a peak whose oracle height is within 0.02 dB of
+    another candidate may trade places with it.
+Parity beyond the oracle is unpinned: the reference holds no MUSIC fixtures and MATLAB is absent.
+"""
+import numpy as np
+import pytest
+
+from oracle import music as mu
+
+SEED = 20250101
+
+
+# ---------------------------------------------------------------------------- CPU: oracle
+def test_findpeaks_semantics():
+    """MATLAB findpeaks: strict local maxima, first sample of a flat top, never the ends."""
+    y = np.array([5, 1, 3, 3, 2, 4, 4, 4, 6, 0, 7, 7])
+    assert list(mu.findpeaks(y)) == [2, 8]          # plateau 3,3 -> index 2; 6 at 8; ends excluded
+    assert list(mu.findpeaks([1, 2, 2, 2])) == []   # plateau running into the end
+    assert list(mu.findpeaks([0, 1, 0, 1, 0])) == [1, 3]
+    assert list(mu.findpeaks([1, 1, 1])) == []
+
+
+def test_noise_free_nulls_sit_on_the_sources():
+    """With sources on the scan grid and no noise the noise subspace is orthogonal to the
+    source steering vectors: the pseudo-spectrum peaks exactly at them (MUSIC_1D.m:37)."""
+    scan = np.deg2rad(np.arange(-90, 91, 1.0))
+    scene = {'angles_rad': np.deg2rad([-30.0, -10.0, 60.0]), 'complex_sources': 0, 'snr_db': 300.0,
+             'snr_measured': 1}
+    X = mu.synthesize(scene, 10, 1000, 0.5, 0, SEED)       # MUSIC_1D.m:10,18 (N = 10, K = 1000)
+    r = mu.music_1d(X, 3, scan, 0.5)
+    assert np.allclose(sorted(r['angles_deg']), [-30.0, -10.0, 60.0], atol=1e-9)
+    assert np.abs(r['eig'][3:]).max() < 1e-12 * r['eig'][0]   # rank-M covariance
+
+
+def test_eigenvalue_structure_matches_the_signal_model():
+    """R -> S Rs S^H + sigma^2 I: the N - M noise eigenvalues cluster at the measured noise
+    power (awgn 'measured', MUSIC_1D.m:24) within the Marchenko-Pastur band."""
+    scene, scan, dl = mu.music_1d_scene()
+    N, K = 64, 1024
+    X = mu.synthesize(scene, N, K, dl, 3, SEED)
+    r = mu.music_1d(X, 3, scan, dl)
+    p_sig = 3.0                                                # three unit-variance real sources
+    sigma2 = p_sig / 10.0
+    lo, hi = sigma2 * (1 - np.sqrt(N / K)) ** 2, sigma2 * (1 + np.sqrt(N / K)) ** 2
+    noise = r['eig'][3:]
+    assert noise.min() > 0.8 * lo and noise.max() < 1.2 * hi
+    assert r['eig'][2] > 20 * noise.max()
+    assert np.all(np.abs(np.sort(r['angles_deg']) - np.array([-30.0, -10.0, 60.0])) < 1.0)
+
+
+def test_run_music_resolves_the_close_pair():
+    """run_music_algorithm.m:14-15: 2.0 and -1.5 deg are resolved on the 0.1 deg grid."""
+    scene, scan, dl = mu.run_music_scene()
+    X = mu.synthesize(scene, 16, 256, dl, 0, SEED)
+    r = mu.music_1d(X, 2, scan, dl)
+    assert sorted(np.round(r['angles_deg'], 1)) == [-1.5, 2.0]
+
+
+def test_batch_oracle_equals_per_instance():
+    scene, scan, dl = mu.music_1d_scene()
+    Xs = np.stack([mu.synthesize(scene, 16, 128, dl, i, SEED) for i in range(4)])
+    PdB, pk = mu.music_batch(Xs, 3, scan, dl)
+    for i in range(4):
+        r = mu.music_1d(Xs[i], 3, scan, dl)
+        assert np.abs(PdB[i] - r['spectrum_db']).max() < 1e-9
+        assert list(pk[i]) == list(r['peaks'])
+
+
+def test_music_bad_config_is_rejected():
+    from rsp import _abi
+    from rsp.music import MusicPlan
+    with pytest.raises(_abi.RspError) as e:
+        MusicPlan(65, 128, 3, np.linspace(-1, 1, 50))
+    assert e.value.code == _abi.RSP_ERR_UNSUPPORTED
+    with pytest.raises(_abi.RspError) as e:
+        MusicPlan(16, 128, 16, np.linspace(-1, 1, 50))     # M must leave a noise subspace
+    assert e.value.code == _abi.RSP_ERR_UNSUPPORTED
+
+
+# ---------------------------------------------------------------------------- GPU: parity
+CASES = {
+    # BASELINE config #5: 64 channels x 1024 snapshots, MUSIC_1D.m scene
+    'config5': (64, 1024, 3, mu.music_1d_scene),
+    # the literal MUSIC_1D.m: N = 10 (not a multiple of 4: scalar-load covariance), K = 1000
+    'music_1d': (10, 1000, 3, mu.music_1d_scene),
+    # run_music_algorithm.m: 16 channels, 256 snapshots, 401-point degree grid
+    'run_music': (16, 256, 2, mu.run_music_scene),
+}
+
+
+@pytest.fixture(scope='module', params=sorted(CASES))
+def music_case(request):
+    from rsp.music import MusicPlan
+    N, K, M, mk = CASES[request.param]
+    scene, scan, dl = mk()
+    n_inst = 8
+    plan = MusicPlan(N, K, M, scan, dl, max_batch=n_inst)
+    d_X = plan.device_alloc(n_inst)
+    plan.synthesize_device(d_X, scene, n_inst, inst0=0, seed=SEED)
+    X = plan.download(d_X, n_inst)
+    out = plan.process_device(d_X, n_inst, want_cov=True)
+    prof = plan.profile(d_X, n_inst, iters=2)
+    ref = [mu.music_1d(X[i].astype(np.complex128), M, scan, dl) for i in range(n_inst)]
+    yield dict(N=N, K=K, M=M, scene=scene, scan=scan, dl=dl, X=X, out=out, ref=ref, plan=plan, prof=prof,
+               n=n_inst)
+    plan.device_free(d_X)
+    plan.close()
+
+
+@pytest.mark.gpu
+def test_music_synthesis_matches_oracle(music_case):
+    c = music_case
+    for i in range(c['n']):
+        x = mu.synthesize(c['scene'], c['N'], c['K'], c['dl'], i, SEED)
+        assert np.abs(c['X'][i] - x).max() <= 1e-6 * np.abs(x).max()
+
+
+@pytest.mark.gpu
+def test_music_covariance_mfma(music_case):
+    c = music_case
+    for i in range(c['n']):
+        R = c['ref'][i]['R']
+        assert np.abs(c['out']['R'][i] - R).max() <= 2e-6 * np.abs(R).max()
+
+
+@pytest.mark.gpu
+def test_music_eigenvalues(music_case):
+    c = music_case
+    assert c['prof']['eig_ms'] > 0.0
+    for i in range(c['n']):
+        d = c['ref'][i]['eig']
+        assert np.abs(c['out']['eig'][i] - d).max() <= 2e-5 * d.max()
+
+
+@pytest.mark.gpu
+def test_music_spectrum_and_peaks(music_case):
+    c = music_case
+    for i in range(c['n']):
+        ref = c['ref'][i]['spectrum_db']
+        got = c['out']['spectrum_db'][i]
+        live = ref > -60.0
+        assert np.abs(got[live] - ref[live]).max() <= 0.02
+        want = list(c['ref'][i]['peaks'])
+        have = list(c['out']['peaks'][i])
+        if have != want:   # only near-equal peak heights may trade places
+            pk = mu.findpeaks(ref)
+            hv = np.sort(ref[pk])[::-1]
+            assert len(hv) > c['M'] and hv[c['M'] - 1] - hv[c['M']] <= 0.02, (have, want)
+        assert c['out']['n_peaks'][i] == c['ref'][i]['n_peaks']
+
+
+@pytest.mark.gpu
+def test_music_host_path_equals_device_path(music_case):
+    """rsp_music_process (host complex128 X, MATLAB layout) == the device-resident path."""
+    c = music_case
+    o = c['plan'].process(c['X'][:3].astype(np.complex128))
+    assert np.array_equal(o['peaks'], c['out']['peaks'][:3])
+    assert np.abs(o['spectrum_db'] - c['out']['spectrum_db'][:3]).max() == 0.0
