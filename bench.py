@@ -43,6 +43,7 @@ def parse():
     ap.add_argument('--profile-iters', type=int, default=50)
     ap.add_argument('--cpu-frames', type=int, default=0, help='oracle frames for cpu_baseline (0 = auto ~15 s)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--batch', type=int, default=1024, help='MUSIC instances per launch (--config music5)')
     ap.add_argument('--stage-timing', action='store_true',
                     help='HIP events around every kernel in the timed region (diagnostic: overlapped durations)')
     return ap.parse_args()
@@ -83,8 +84,99 @@ def cpu_baseline(cfg, cfar, clus, W, ang, k, targets, budget_s=15.0, nframes=0):
                       '(the MATLAB scalar CFAR loop fsf:192-213 would be slower)' % (len(times), 'x2', med)}
 
 
+MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense peak
+
+
+def music_cpu_baseline(scene, scan, dl, N, K, M, n=96):
+    """The MUSIC oracle (numpy complex128, batched eigh) on a bounded sample of instances."""
+    from oracle import music as mu
+    Xs = np.stack([mu.synthesize(scene, N, K, dl, i, 20250101) for i in range(n)])
+    mu.music_batch(Xs[:4], M, scan, dl)
+    t0 = time.perf_counter()
+    mu.music_batch(Xs, M, scan, dl)
+    el = time.perf_counter() - t0
+    return {'value': n / el, 'unit': 'instances/s', 'cores': 1, 'kind': 'port',
+            'sample': '%d instances of the config #5 scene through oracle.music.music_batch (numpy complex128: '
+                      'einsum covariance, batched LAPACK eigh, pseudo-spectrum, findpeaks), %.2f s' % (n, el)}
+
+
+def main_music(a):
+    """BASELINE config #5: MUSIC_1D DOA on 64-channel x 1024-snapshot instances (MUSIC_1D.m:21-48).
+    One step = one batch of --batch instances (device-resident snapshots, synthesised on the
+    device) through covariance -> eig -> pseudo-spectrum -> findpeaks, peak indices to the host.
+    Multi-GPU: instances sharded by rank (weak scaling), no collective."""
+    rank = int(os.environ.get('RANK', 0))
+    world = int(os.environ.get('WORLD_SIZE', 1))
+    local = int(os.environ.get('LOCAL_RANK', 0))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    from rsp.music import MusicPlan, music_1d_scene
+    N, K, M, I = 64, 1024, 3, a.batch
+    scene, scan, dl = music_1d_scene()
+    plan = MusicPlan(N, K, M, scan, dl, max_batch=I, device=local if world > 1 else 0)
+    ring = [plan.device_alloc(I) for _ in range(2)]   # 2 x 512 MiB > Infinity Cache
+    for r, d in enumerate(ring):
+        plan.synthesize_device(d, scene, I, inst0=(rank * 2 + r) * I)
+    peaks = np.zeros((I, M), np.int32)
+    npk = np.zeros(I, np.int32)
+    for i in range(a.warmup):
+        plan.peaks_device(ring[i % 2], I, peaks, npk)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        plan.peaks_device(ring[i % 2], I, peaks, npk)
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([el], dtype=torch.float64, device='cuda')
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    out = None
+    if rank == 0:
+        pr = plan.profile(ring[0], I, iters=a.profile_iters)
+        flops = 8.0 * N * (N + 1) / 2 * K * I   # Hermitian X X^H: N(N+1)/2 entries x K complex MACs
+        cov_tf = flops / (pr['cov_ms'] * 1e-3) / 1e12
+        bytes_ = 8.0 * N * K * I
+        stages = [{'stage': 'k_music_cov', 'ms_per_launch': pr['cov_ms'], 'instances_per_launch': I,
+                   'alg_flops_per_launch': flops, 'achieved_TFLOPs': cov_tf,
+                   'achieved_GBps': bytes_ / (pr['cov_ms'] * 1e-3) / 1e9},
+                  {'stage': 'k_music_eig', 'ms_per_launch': pr['eig_ms'], 'instances_per_launch': I,
+                   'note': 'Householder + bisection + inverse iteration + spectrum per workgroup: '
+                           'latency-bound (neither HBM nor MFMA), see DESIGN.md'}]
+        out = {'metric': 'MUSIC_1D DOA instances/sec, 64ch x 1024 snapshots (BASELINE config #5)',
+               'value': I * a.steps * world / el, 'unit': 'instances/s', 'n_gpus': world, 'steps': a.steps,
+               'warmup': a.warmup, 'ms_per_step': el / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
+               'vs_baseline': None, 'dtype': 'fp32 (complex64)',
+               'data': 'synthetic (device Philox snapshots, MUSIC_1D.m scene: -10/-30/60 deg, 10 dB measured)',
+               'config': {'workload': 'BASELINE config #5: N=64 K=1024 M=3 scan=200, %d instances per step' % I,
+                          'parallelism': 'instance-sharded x%d' % world},
+               'roofline': {'bound': 'mfma', 'kernel': 'k_music_cov', 'achieved': cov_tf,
+                            'peak': MFMA_F32_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': cov_tf / MFMA_F32_PEAK_TFLOPS,
+                            'traffic': None, 'kernel_ms': pr['cov_ms'],
+                            'timing': 'HIP events on the plan stream, %d launches' % a.profile_iters,
+                            'stages': stages},
+               'cpu_baseline': music_cpu_baseline(scene, scan, dl, N, K, M) if (world == 1 and not a.no_cpu_baseline)
+               else None}
+    for d in ring:
+        plan.device_free(d)
+    plan.close()
+    if dist is not None:
+        dist.destroy_process_group()
+    if out is not None:
+        print(json.dumps(out))
+
+
 def main():
     a = parse()
+    if a.config == 'music5':
+        return main_music(a)
     rank = int(os.environ.get('RANK', 0))
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', 0))

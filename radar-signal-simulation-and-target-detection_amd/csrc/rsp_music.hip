@@ -16,6 +16,8 @@
 
 #include <cmath>
 #include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -250,7 +252,11 @@ __device__ __forceinline__ float wave_sum(float v) {
 __global__ __launch_bounds__(MU_THREADS) void k_music_eig(int N, int M, int S, const float2* __restrict__ R,
                                                         const float2* __restrict__ S1T, int Spad,
                                                         float* __restrict__ spec_db, float* __restrict__ eig_out,
-                                                        int* __restrict__ peaks_out) {
+                                                        int* __restrict__ peaks_out, unsigned long long* __restrict__ trace) {
+    // trace (diagnostic, RSP_MUSIC_TRACE=1): s_memrealtime at the phase boundaries, thread 0
+#define MU_STAMP(i) \
+    if (trace && threadIdx.x == 0) trace[(size_t)blockIdx.x * 8 + (i)] = wall_clock64()
+    MU_STAMP(0);
     __shared__ float2 A[MU_NMAX * MU_LDA];   // R, then the reflectors; then den(s)
     __shared__ float2 vv[MU_NMAX], pp[MU_NMAX], taus[MU_NMAX], Qs[MU_MMAX][MU_NMAX];
     __shared__ float dd[MU_NMAX], ee[MU_NMAX], lam[MU_NMAX], Y[MU_MMAX][MU_NMAX];
@@ -337,6 +343,7 @@ __global__ __launch_bounds__(MU_THREADS) void k_music_eig(int N, int M, int S, c
     }
     if (tid == 0) dd[n - 1] = A[(n - 1) * MU_LDA + n - 1].x;
     __syncthreads();
+    MU_STAMP(1);
     // ---- 2. eigenvalues of T by bisection: thread k -> k-th smallest
     if (tid < n) {
         float lo = dd[0], hi = dd[0], tn = 0.f;
@@ -367,6 +374,7 @@ __global__ __launch_bounds__(MU_THREADS) void k_music_eig(int N, int M, int S, c
         eig_out[(size_t)blockIdx.x * N + (n - 1 - tid)] = l;   // descending (MUSIC_1D.m:31)
     }
     __syncthreads();
+    MU_STAMP(2);
     // ---- 3. signal eigenvectors of T: block inverse iteration
     float tnorm = 0.f;
     for (int i = 0; i < n; ++i) tnorm = fmaxf(tnorm, fabsf(dd[i]) + (i > 0 ? fabsf(ee[i - 1]) : 0.f) + (i < n - 1 ? fabsf(ee[i]) : 0.f));
@@ -443,6 +451,7 @@ __global__ __launch_bounds__(MU_THREADS) void k_music_eig(int N, int M, int S, c
         }
         __syncthreads();
     }
+    MU_STAMP(3);
     // q_j = H_0 H_1 ... H_{n-2} y_j (one wave per vector, lane = component)
     for (int j = w; j < M; j += MU_THREADS / 64) {
         float2 y = make_float2(lane < n ? Y[j][lane] : 0.f, 0.f);
@@ -459,6 +468,7 @@ __global__ __launch_bounds__(MU_THREADS) void k_music_eig(int N, int M, int S, c
         if (lane < n) Qs[j][lane] = y;
     }
     __syncthreads();
+    MU_STAMP(4);
     // ---- 4. den(s) = |a(s) - Q_s Q_s^H a(s)|^2, one thread per angle (A's LDS holds den)
     float* den = reinterpret_cast<float*>(A);
     for (int s = tid; s < S; s += MU_THREADS) {
@@ -485,6 +495,7 @@ __global__ __launch_bounds__(MU_THREADS) void k_music_eig(int N, int M, int S, c
         den[s] = r2;
     }
     __syncthreads();
+    MU_STAMP(5);
     // P = 1 ./ den, P_dB = 10 log10(P / max P) (MUSIC_1D.m:37-41)
     float pmax = 0.f;
     for (int s = tid; s < S; s += MU_THREADS) pmax = fmaxf(pmax, 1.f / den[s]);
@@ -535,6 +546,8 @@ __global__ __launch_bounds__(MU_THREADS) void k_music_eig(int N, int M, int S, c
         po[0] = npk;
         for (int i = 0; i < MU_MMAX; ++i) po[1 + i] = i < nb ? best[i] + 1 : 0;
     }
+    MU_STAMP(6);
+#undef MU_STAMP
 }
 
 }  // namespace
@@ -555,6 +568,7 @@ struct rsp_music_plan {
     int* d_peaks = nullptr;      // [max_batch][MU_MMAX + 1]
     double2* d_src = nullptr;    // synthesis: source steering [MU_MMAX][N]
     double* d_amp = nullptr;     // [MU_MMAX]
+    unsigned long long* d_trace = nullptr;   // RSP_MUSIC_TRACE: [max_batch][8] phase stamps
     hipEvent_t ev[4] = {};
 };
 
@@ -580,7 +594,7 @@ int music_run(rsp_music_plan* p, const float2* dX, int n_inst, bool timed, float
     MUCHK(hipGetLastError());
     if (timed) MUCHK(hipEventRecord(p->ev[1], p->stream));
     hipLaunchKernelGGL(k_music_eig, dim3(n_inst), dim3(MU_THREADS), 0, p->stream, p->N, p->M, p->S, p->d_R, p->d_S1T,
-                       p->Spad, p->d_spec, p->d_eig, p->d_peaks);
+                       p->Spad, p->d_spec, p->d_eig, p->d_peaks, p->d_trace);
     MUCHK(hipGetLastError());
     if (timed) {
         MUCHK(hipEventRecord(p->ev[2], p->stream));
@@ -677,6 +691,9 @@ int32_t rsp_music_create(const rsp_music_config* cfg, int32_t device, rsp_music_
         }
     if (hipMemcpy(p->d_S1T, s1.data(), s1.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess)
         return bail(rsp_set_error(RSP_ERR_DEVICE, "steering upload failed"));
+    const char* tr = getenv("RSP_MUSIC_TRACE");
+    if (tr && atoi(tr) && hipMalloc(&p->d_trace, B * 8 * sizeof(unsigned long long)) != hipSuccess)
+        return bail(rsp_set_error(RSP_ERR_NOMEM, "trace buffer"));
     *out = p;
     return RSP_OK;
 }
@@ -685,7 +702,7 @@ int32_t rsp_music_destroy(rsp_music_plan* p) {
     if (!p) return RSP_OK;
     (void)hipSetDevice(p->device);
     if (p->stream) (void)hipStreamSynchronize(p->stream);
-    void* bufs[] = {p->d_S1T, p->d_R, p->d_X, p->d_spec, p->d_eig, p->d_peaks, p->d_src, p->d_amp};
+    void* bufs[] = {p->d_S1T, p->d_R, p->d_X, p->d_spec, p->d_eig, p->d_peaks, p->d_src, p->d_amp, p->d_trace};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (auto& e : p->ev)
@@ -768,6 +785,15 @@ int32_t rsp_music_profile(rsp_music_plan* p, const void* d_X, int32_t n_inst, in
     }
     ms_out[0] = (float)(acc[0] / iters);
     ms_out[1] = (float)(acc[1] / iters);
+    if (p->d_trace) {   // mean phase durations of the last launch (s_memrealtime: 100 MHz)
+        std::vector<unsigned long long> t((size_t)n_inst * 8);
+        MUCHK(hipMemcpy(t.data(), p->d_trace, t.size() * sizeof(t[0]), hipMemcpyDeviceToHost));
+        double ph[6] = {0, 0, 0, 0, 0, 0};
+        for (int i = 0; i < n_inst; ++i)
+            for (int q = 0; q < 6; ++q) ph[q] += (double)(t[(size_t)i * 8 + q + 1] - t[(size_t)i * 8 + q]) * 0.01 / n_inst;
+        fprintf(stderr, "k_music_eig phases (us/instance): tridiag %.2f bisect %.2f inviter %.2f backxf %.2f spectrum %.2f peaks %.2f\n",
+                ph[0], ph[1], ph[2], ph[3], ph[4], ph[5]);
+    }
     return RSP_OK;
 }
 

@@ -121,6 +121,24 @@ class MusicPlan:
         return {'cov_ms': ms[0], 'eig_ms': ms[1]}
 
 
+def music_1d_scene():
+    """MUSIC_1D.m:5-35 scene at BASELINE config #5 (64 channels, 1024 snapshots): d = lambda/2,
+    real sources at (-10, -30, 60) deg, awgn 10 dB 'measured', 200-point scan over +-90 deg.
+    Returns (scene dict for MusicPlan.synthesize_device, scan grid [rad], d/lambda)."""
+    return ({'angles_rad': np.deg2rad([-10.0, -30.0, 60.0]), 'amplitudes': np.ones(3), 'complex_sources': 0,
+             'snr_db': 10.0, 'snr_measured': 1},
+            np.linspace(-np.pi / 2, np.pi / 2, 200), 0.5)
+
+
+def run_music_scene():
+    """run_music_algorithm.m:7-20,60: 16 channels at 13.8 mm, fc 9.45 GHz, complex sources at
+    2.0 / -1.5 deg with amplitudes 1 / 0.7, SNR 15 dB (fixed noise power), scan -20:0.1:20 deg."""
+    wl = 2.99792458e8 / 9450e6
+    return ({'angles_rad': np.deg2rad([2.0, -1.5]), 'amplitudes': np.array([1.0, 0.7]), 'complex_sources': 1,
+             'snr_db': 15.0, 'snr_measured': 0},
+            np.deg2rad(np.round(np.arange(-200, 201) * 0.1, 10)), 0.0138 / wl)
+
+
 def MUSIC_1D(X1, M, phi_list=None, d_over_lambda=0.5, device=0):
     """MUSIC_1D.m:26-48 on one snapshot matrix X1 [N x K]: returns (phi_e [deg], P_MUSIC_dB, EVA)."""
     X1 = np.asarray(X1)

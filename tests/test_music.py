@@ -77,6 +77,15 @@ def test_batch_oracle_equals_per_instance():
         assert list(pk[i]) == list(r['peaks'])
 
 
+def test_product_scenes_equal_oracle_scenes():
+    """rsp.music's scene constants (used by bench.py) restate the same script lines as the oracle's."""
+    from rsp import music as pm
+    for a, b in ((pm.music_1d_scene(), mu.music_1d_scene()), (pm.run_music_scene(), mu.run_music_scene())):
+        assert a[2] == b[2] and np.array_equal(a[1], b[1])
+        for k in b[0]:
+            assert np.array_equal(np.asarray(a[0][k]), np.asarray(b[0][k])), k
+
+
 def test_music_bad_config_is_rejected():
     from rsp import _abi
     from rsp.music import MusicPlan
