@@ -216,6 +216,33 @@ int32_t rsp_stage_times(const rsp_plan* plan, double* ms_sum, int32_t cap, int64
 int32_t rsp_cluster_detections(const rsp_detection* dets, int32_t n, const rsp_cluster_params* cluster,
                                rsp_target* out, int32_t cap, int32_t* n_out);
 
+/* ---- inter-frame track association (host only, no GPU) ----
+ * main_simulate_echoes_with_array_v8_3.m:253-352: cumulative_final_log (final_targets of every
+ * frame with iFrame and iAntAngle injected, :236-244) -> final_tracks_log.  Points are linked
+ * when |dRange| <= Gate_R, |dVelocity| <= Gate_V, |d iAntAngle| <= Gate_Az, |dAngle| <= Gate_El
+ * and |d iFrame| <= Max_Frame_Gap (config.inter_frame_cluster, v8_3:57-65); clusters are the
+ * reference BFS's (connected components, numbered by first member).  Per cluster: the first
+ * max-Power member gives Range / Velocity / Angle / Power, Azimuth is the power-weighted mean
+ * of iAntAngle, FirstFrame / LastFrame / NumPoints over the members. */
+typedef struct rsp_track_point {
+    double Range, Velocity, Angle, Power;   /* one final_targets entry (fsf:393-406)     */
+    double iAntAngle;                       /* servo azimuth of its frame (v8_3:238)     */
+    int32_t iFrame, reserved;               /* frame index (v8_3:237)                    */
+} rsp_track_point;
+
+typedef struct rsp_inter_frame_params {
+    double Gate_R, Gate_V, Gate_Az, Gate_El;
+    int32_t Max_Frame_Gap, reserved;
+} rsp_inter_frame_params;
+
+typedef struct rsp_track {   /* one final_tracks_log entry (v8_3:318-335) */
+    double Range, Velocity, Angle, Azimuth, Power;
+    int32_t FirstFrame, LastFrame, NumPoints, reserved;
+} rsp_track;
+
+int32_t rsp_inter_frame_cluster(const rsp_track_point* log, int32_t n, const rsp_inter_frame_params* gates,
+                                rsp_track* out, int32_t cap, int32_t* n_out);
+
 /* Device memory helpers (so hosts without a GPU runtime binding can stage cubes). */
 int32_t rsp_device_alloc(rsp_plan* plan, int64_t bytes, void** d_ptr);
 int32_t rsp_device_free(rsp_plan* plan, void* d_ptr);

@@ -3,14 +3,14 @@
 // Reference: MUSIC_1D.m:21-48 and run_music_algorithm.m:22-69.  Per instance (one snapshot
 // matrix X [N x K], N <= 64 channels):
 //   R = X X^H / K                          (MUSIC_1D.m:28)   k_music_cov   f32 MFMA
-//   [EV, D] = eig(R); sort descend          (MUSIC_1D.m:29-33) k_music_eig   Householder + bisection
+//   [EV, D] = eig(R); sort descend          (MUSIC_1D.m:29-33) k_music_eig   Householder + bisection, one wave
 //   P = 1 ./ sum(|Q_n^H S1|.^2); dB          (MUSIC_1D.m:35-41) k_music_eig   (same workgroup)
 //   findpeaks + top M                       (MUSIC_1D.m:43-48) k_music_eig   (same workgroup)
 // plus the synthetic snapshot model of MUSIC_1D.m:21-24 / run_music_algorithm.m:27-39 with the
 // Philox streams documented in oracle/music.py (k_music_synth).
 //
-// Batching: one workgroup per instance in every kernel; BASELINE config #5 runs >= 1024
-// instances per launch so that the 256 CUs are full.
+// Batching: one workgroup per instance (k_music_eig: one wave per instance); BASELINE config
+// #5 runs >= 1024 instances per launch so that the 256 CUs are full.
 #include "rsp.h"
 #include "rsp_internal.h"
 
@@ -220,331 +220,383 @@ __global__ __launch_bounds__(MU_THREADS) void k_music_cov(int N, int K, const fl
 }
 
 // ---------------------------------------------------------------------------------------
-// eig + MUSIC spectrum + findpeaks (MUSIC_1D.m:29-48), one workgroup per instance, fp32 in LDS.
+// eig + MUSIC spectrum + findpeaks (MUSIC_1D.m:29-48): ONE WAVE PER INSTANCE, fp32 in LDS.
+// Lane i owns matrix column i (N <= 64): every LDS access of A walks a row, so the 64 lanes
+// touch 64 consecutive complex words (no bank conflicts); cross-lane operands come from
+// v_readlane and DPP reductions, so no phase needs more than a one-wave barrier.
 //  1. Householder reduction of the Hermitian R to a real symmetric tridiagonal T = Q^H R Q
-//     (the lower-triangle algorithm of LAPACK zhetd2: reflectors H_k = I - tau_k v_k v_k^H
-//     with real beta_k, so the subdiagonal is real; v_k is kept in column k of A).
-//  2. All N eigenvalues of T by Sturm-count bisection, one thread per eigenvalue index
-//     (EVA, MUSIC_1D.m:29-31, sorted descending).
-//  3. The M signal eigenvectors of T by block inverse iteration on T - lambda I (partial-pivot
-//     tridiagonal LU as LAPACK dlagtf/dlagts, 3 solves, Gram-Schmidt after each), then
-//     q_j = Q y_j by applying the reflectors in reverse order (one wave per vector).
-//  4. sum_j |Q_n^H a|^2 (MUSIC_1D.m:37) = a^H (I - Q_s Q_s^H) a for the unitary eigenvector
-//     matrix [Q_s Q_n]; it is evaluated as the squared norm of the residual a - Q_s (Q_s^H a),
-//     so nothing cancels against |a|^2 = N.
+//     (LAPACK zhetd2, lower: H_k = I - tau_k v_k v_k^H, beta_k real).  Column k of A is
+//     conj(row k); v_k is kept in row k (columns k+1..), which is dead after step k.
+//  2. All N eigenvalues of T by Sturm-count bisection, lane t -> t-th smallest (EVA,
+//     MUSIC_1D.m:29-31, sorted descending).
+//  3. The M signal eigenvectors of T by block inverse iteration (partial-pivot tridiagonal
+//     LU as LAPACK dlagtf/dlagts, lane j = vector j, 3 solves with Gram-Schmidt after each),
+//     then q_j = H_0 ... H_{n-2} y_j (lane = component).
+//  4. sum_j |Q_n^H a|^2 (MUSIC_1D.m:37) = a^H (I - Q_s Q_s^H) a for the unitary [Q_s Q_n],
+//     evaluated as |a - Q_s (Q_s^H a)|^2 (no cancellation against |a|^2 = N), lane = angle.
 //  5. P = 1 / den, P_dB = 10 log10(P / max P), findpeaks + the M largest (MUSIC_1D.m:37-47).
+// Dynamic LDS per wave: A [64][64] complex | tau [64] complex | d, e^2, lambda, e [64] |
+// LU + y [5][64][M] (vector fastest) | Q_s [M][64] complex | (v, w) [64][2]; den(s) overlays A.
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ float2 cm(float2 a, float2 b) { return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
-__device__ __forceinline__ float2 cadd2(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csc(float s, float2 a) { return make_float2(s * a.x, s * a.y); }
-__device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
 __device__ __forceinline__ float2 cmc(float2 a, float2 b) {   // conj(a) * b
     return make_float2(a.x * b.x + a.y * b.y, a.x * b.y - a.y * b.x);
 }
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+__device__ __forceinline__ float2 cadd2(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub2(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 csc(float s, float2 a) { return make_float2(s * a.x, s * a.y); }
+__device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
+
+#define MU_DPP(v, ctrl) __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), (ctrl), 0xF, 0xF, false))
+__device__ __forceinline__ float rdl(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+__device__ __forceinline__ float2 rdl2(float2 v, int l) { return make_float2(rdl(v.x, l), rdl(v.y, l)); }
+// Sum / max over the 64 lanes, result uniform: DPP butterflies inside each row of 16 lanes
+// (quad_perm xor 1, xor 2, half-mirror, mirror), then the four row values by readlane.
+__device__ __forceinline__ float wsum(float v) {
+    v += MU_DPP(v, 0xB1);
+    v += MU_DPP(v, 0x4E);
+    v += MU_DPP(v, 0x141);
+    v += MU_DPP(v, 0x140);
+    return (rdl(v, 0) + rdl(v, 16)) + (rdl(v, 32) + rdl(v, 48));
+}
+__device__ __forceinline__ float wmax(float v) {
+    v = fmaxf(v, MU_DPP(v, 0xB1));
+    v = fmaxf(v, MU_DPP(v, 0x4E));
+    v = fmaxf(v, MU_DPP(v, 0x141));
+    v = fmaxf(v, MU_DPP(v, 0x140));
+    return fmaxf(fmaxf(rdl(v, 0), rdl(v, 16)), fmaxf(rdl(v, 32), rdl(v, 48)));
+}
+__device__ __forceinline__ int wmin_i(int v) {
+#define MU_DPPI(x, ctrl) __builtin_amdgcn_update_dpp(0, (x), (ctrl), 0xF, 0xF, false)
+    v = min(v, MU_DPPI(v, 0xB1));
+    v = min(v, MU_DPPI(v, 0x4E));
+    v = min(v, MU_DPPI(v, 0x141));
+    v = min(v, MU_DPPI(v, 0x140));
+#undef MU_DPPI
+    return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+               min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
 }
 
-#define MU_ITER 3   // inverse-iteration solves per signal vector
+#define MU_ITER 3            // inverse-iteration solves per signal vector
+#define MU_SPW (MU_SCAN_MAX / 64)
 
-__global__ __launch_bounds__(MU_THREADS) void k_music_eig(int N, int M, int S, const float2* __restrict__ R,
-                                                        const float2* __restrict__ S1T, int Spad,
-                                                        float* __restrict__ spec_db, float* __restrict__ eig_out,
-                                                        int* __restrict__ peaks_out, unsigned long long* __restrict__ trace) {
-    // trace (diagnostic, RSP_MUSIC_TRACE=1): s_memrealtime at the phase boundaries, thread 0
+__host__ __device__ constexpr size_t mu_eig_lds_bytes(int M) {
+    return (size_t)MU_NMAX * MU_NMAX * 8 + MU_NMAX * 8 + 4 * MU_NMAX * 4 + (size_t)5 * M * MU_NMAX * 4 +
+           (size_t)M * MU_NMAX * 8 + MU_NMAX * 16;
+}
+
+template <int M>   // signal subspace dimension (compile time: the M-vector loops unroll exactly)
+__global__ __launch_bounds__(64) void k_music_eig(int N, int S, const float2* __restrict__ R,
+                                                const float2* __restrict__ S1T, int Spad, float* __restrict__ spec_db,
+                                                float* __restrict__ eig_out, int* __restrict__ peaks_out,
+                                                unsigned long long* __restrict__ trace) {
+    // trace (diagnostic, RSP_MUSIC_TRACE=1): s_memrealtime at the phase boundaries
 #define MU_STAMP(i) \
     if (trace && threadIdx.x == 0) trace[(size_t)blockIdx.x * 8 + (i)] = wall_clock64()
     MU_STAMP(0);
-    __shared__ float2 A[MU_NMAX * MU_LDA];   // R, then the reflectors; then den(s)
-    __shared__ float2 vv[MU_NMAX], pp[MU_NMAX], taus[MU_NMAX], Qs[MU_MMAX][MU_NMAX];
-    __shared__ float dd[MU_NMAX], ee[MU_NMAX], lam[MU_NMAX], Y[MU_MMAX][MU_NMAX];
-    __shared__ float fa[MU_MMAX][MU_NMAX], fb[MU_MMAX][MU_NMAX], fc[MU_MMAX][MU_NMAX], fd[MU_MMAX][MU_NMAX];
-    __shared__ float2 sc[2];
-    __shared__ __attribute__((aligned(8))) float red[MU_THREADS];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2* A = lds;                                  // A(j, i) at A[j * 64 + i]
+    float2* taus = A + MU_NMAX * MU_NMAX;
+    float* dd = reinterpret_cast<float*>(taus + MU_NMAX);
+    float* e2 = dd + MU_NMAX;                         // e_k^2
+    float* lam = e2 + MU_NMAX;                        // ascending eigenvalues
+    float* ee = lam + MU_NMAX;                        // e_k = beta_k (signed)
+    float* lu = ee + MU_NMAX;                        // [5][64][M]: U diag, U super 1, U super 2, mult, y
+    float2* Qs = reinterpret_cast<float2*>(lu + 5 * MU_NMAX * M);   // [M][64]
+    float2* vw = Qs + M * MU_NMAX;                    // [64][2]: (v_j, w_j) of the current step
+    const int lane = threadIdx.x;
     const int n = N;
-    const float2* __restrict__ Ri = R + (size_t)blockIdx.x * MU_NMAX * MU_NMAX;
-    for (int e = tid; e < n * n; e += MU_THREADS) {   // A(i, j) = R(i, j); R column-major ld 64
-        const int j = e / n, i = e - j * n;
-        A[i * MU_LDA + j] = Ri[i + MU_NMAX * j];
+    const bool live = lane < n;
+    const float2 z2 = make_float2(0.f, 0.f);
+    {   // A(j, i) = conj(R(i, j)): R column-major ld 64, lane i reads R(i, j) (coalesced)
+        const float2* __restrict__ Ri = R + (size_t)blockIdx.x * MU_NMAX * MU_NMAX;
+        for (int j = 0; j < n; ++j) A[j * MU_NMAX + lane] = live ? cconj(Ri[lane + MU_NMAX * j]) : z2;
+        for (int j = n; j < ((n + 7) & ~7); ++j) A[j * MU_NMAX + lane] = z2;   // chunk padding rows
     }
+    const int nr = (n + 7) & ~7;
     __syncthreads();
-    // ---- 1. tridiagonalisation (zhetd2, lower)
-    const int row = tid >> 2, part = tid & 3;   // (row, column-phase) of the matvec / rank-2 update
+    // ---- 1. tridiagonalisation
     for (int k = 0; k < n - 1; ++k) {
-        const int m = n - k - 1;   // length of x = A(k+1:n-1, k)
-        if (w == 0) {   // zlarfg: H^H x = beta e1, beta real
-            float xn2 = 0.f;
-            if (lane >= 1 && lane < m) {
-                const float2 x = A[(k + 1 + lane) * MU_LDA + k];
-                xn2 = x.x * x.x + x.y * x.y;
-            }
-            xn2 = wave_sum(xn2);
-            if (lane == 0) {
-                const float2 al = A[(k + 1) * MU_LDA + k];
-                float2 tau = make_float2(0.f, 0.f), scale = make_float2(0.f, 0.f);
-                float beta = al.x;
-                if (xn2 > 0.f || al.y != 0.f) {
-                    beta = -copysignf(sqrtf(al.x * al.x + al.y * al.y + xn2), al.x);
-                    tau = make_float2((beta - al.x) / beta, -al.y / beta);
-                    const float2 dn = make_float2(al.x - beta, al.y);   // 1 / (alpha - beta)
-                    const float q = 1.f / (dn.x * dn.x + dn.y * dn.y);
-                    scale = make_float2(dn.x * q, -dn.y * q);
-                }
-                sc[0] = tau;
-                sc[1] = scale;
-                taus[k] = tau;
-                ee[k] = beta;
-                dd[k] = A[k * MU_LDA + k].x;
-            }
+        const float2 x = cconj(A[k * MU_NMAX + lane]);     // x_i = A(i, k), i > k
+        const float xn2 = wsum(lane >= k + 2 && live ? x.x * x.x + x.y * x.y : 0.f);
+        const float2 al = rdl2(x, k + 1);
+        float2 tau = z2, scale = z2;
+        float beta = al.x;
+        if (xn2 > 0.f || al.y != 0.f) {   // zlarfg (uniform)
+            beta = -copysignf(sqrtf(al.x * al.x + al.y * al.y + xn2), al.x);
+            tau = make_float2((beta - al.x) / beta, -al.y / beta);
+            const float2 dn = make_float2(al.x - beta, al.y);
+            const float q = 1.f / (dn.x * dn.x + dn.y * dn.y);
+            scale = make_float2(dn.x * q, -dn.y * q);
         }
-        __syncthreads();
-        const float2 tau = sc[0], scale = sc[1];
-        if (tid < m) {
-            float2 v = make_float2(1.f, 0.f);
-            if (tid > 0) {
-                v = cm(A[(k + 1 + tid) * MU_LDA + k], scale);
-                A[(k + 1 + tid) * MU_LDA + k] = v;
-            }
-            vv[tid] = v;
+        if (lane == k) {
+            dd[k] = x.x;          // A(k, k) (real)
+            e2[k] = beta * beta;
+            ee[k] = beta;
+            taus[k] = tau;
         }
-        __syncthreads();
-        if (tau.x == 0.f && tau.y == 0.f) continue;   // H = I (uniform)
-        // p = tau A22 v (4 threads per row)
-        float2 acc = make_float2(0.f, 0.f);
-        if (row < m) {
-            const float2* ar = A + (k + 1 + row) * MU_LDA + k + 1;
-            for (int j = part; j < m; j += 4) acc = cadd2(acc, cm(ar[j], vv[j]));
+        const float2 v = lane == k + 1 ? make_float2(1.f, 0.f) : (lane >= k + 2 && live ? cm(x, scale) : z2);
+        A[k * MU_NMAX + lane] = v;                           // v_k kept in row k
+        if (tau.x == 0.f && tau.y == 0.f) continue;
+        // p_i = tau sum_j A(i, j) v_j = tau sum_j conj(A(j, i)) v_j.  Rows in chunks of 8 from
+        // (k+1) & ~7 (v_j = w_j = 0 for j <= k and j >= n, padding rows are zero), v_j and w_j
+        // read back as LDS broadcasts ((v_j, w_j) interleaved in vw[]); 4 partial sums so the
+        // complex FMAs do not form one dependent chain.  (Holding the whole column in registers
+        // measured slower: the unrolled kernel outgrew the instruction cache.)
+        vw[2 * lane] = v;
+        __builtin_amdgcn_wave_barrier();
+        const int j0 = (k + 1) & ~7;
+        float2 acc[4] = {z2, z2, z2, z2};
+        for (int jc = j0; jc < nr; jc += 8) {
+            float2 a[8];
+            float4 b[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) a[u] = A[(jc + u) * MU_NMAX + lane];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) b[u] = *reinterpret_cast<const float4*>(vw + 2 * (jc + u));
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc[u & 3] = cadd2(acc[u & 3], cmc(a[u], make_float2(b[u].x, b[u].y)));
         }
-        acc.x += __shfl_xor(acc.x, 1);
-        acc.y += __shfl_xor(acc.y, 1);
-        acc.x += __shfl_xor(acc.x, 2);
-        acc.y += __shfl_xor(acc.y, 2);
-        if (part == 0 && row < m) pp[row] = cm(tau, acc);
-        __syncthreads();
-        // alpha = -1/2 tau (p^H v) (every wave computes it), w = p + alpha v
-        float2 t = lane < m ? cmc(pp[lane], vv[lane]) : make_float2(0.f, 0.f);
-        t.x = wave_sum(t.x);
-        t.y = wave_sum(t.y);
-        const float2 alpha = csc(-0.5f, cm(tau, t));
-        // A22 -= v w^H + w v^H
-        if (row < m) {
-            const float2 vi = vv[row], wi = cadd2(pp[row], cm(alpha, vi));
-            float2* ar = A + (k + 1 + row) * MU_LDA + k + 1;
-            for (int j = part; j < m; j += 4) {
-                const float2 vj = vv[j], wj = cadd2(pp[j], cm(alpha, vj));
-                const float2 u = cadd2(cm(vi, cconj(wj)), cm(wi, cconj(vj)));
-                ar[j] = make_float2(ar[j].x - u.x, ar[j].y - u.y);
-            }
+        const bool act = lane > k && live;
+        const float2 p = act ? cm(tau, cadd2(cadd2(acc[0], acc[1]), cadd2(acc[2], acc[3]))) : z2;
+        const float2 pv = cmc(p, v);
+        const float2 alpha = csc(-0.5f, cm(tau, make_float2(wsum(pv.x), wsum(pv.y))));
+        const float2 w = act ? cadd2(p, cm(alpha, v)) : z2;
+        vw[2 * lane + 1] = w;
+        __builtin_amdgcn_wave_barrier();
+        const float2 cw = cconj(w), cv = cconj(v);
+        // A(j, i) -= v_j conj(w_i) + w_j conj(v_i); lanes and rows outside k+1..n-1 have
+        // v = w = 0 and rewrite their value
+        for (int jc = j0; jc < nr; jc += 8) {
+            float2 a[8];
+            float4 b[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) a[u] = A[(jc + u) * MU_NMAX + lane];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) b[u] = *reinterpret_cast<const float4*>(vw + 2 * (jc + u));
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                A[(jc + u) * MU_NMAX + lane] =
+                    csub2(a[u], cadd2(cm(make_float2(b[u].x, b[u].y), cw), cm(make_float2(b[u].z, b[u].w), cv)));
         }
-        __syncthreads();
     }
-    if (tid == 0) dd[n - 1] = A[(n - 1) * MU_LDA + n - 1].x;
+    if (lane == n - 1) dd[n - 1] = A[(n - 1) * MU_NMAX + n - 1].x;
     __syncthreads();
     MU_STAMP(1);
-    // ---- 2. eigenvalues of T by bisection: thread k -> k-th smallest
-    if (tid < n) {
-        float lo = dd[0], hi = dd[0], tn = 0.f;
-        for (int i = 0; i < n; ++i) {
-            const float r = (i > 0 ? fabsf(ee[i - 1]) : 0.f) + (i < n - 1 ? fabsf(ee[i]) : 0.f);
-            lo = fminf(lo, dd[i] - r);
-            hi = fmaxf(hi, dd[i] + r);
+    // ---- 2. eigenvalues by bisection (lane t -> t-th smallest)
+    {
+        float glo = 3.4e38f, ghi = -3.4e38f;
+        for (int i = 0; i < n; ++i) {   // Gershgorin
+            const float r = (i > 0 ? sqrtf(e2[i - 1]) : 0.f) + (i < n - 1 ? sqrtf(e2[i]) : 0.f);
+            glo = fminf(glo, dd[i] - r);
+            ghi = fmaxf(ghi, dd[i] + r);
         }
-        tn = fmaxf(fabsf(lo), fabsf(hi));
+        const float tn = fmaxf(fabsf(glo), fabsf(ghi));
         const float pivmin = 1e-30f * fmaxf(1.f, tn * tn);
-        lo -= 1e-6f * tn + pivmin;
-        hi += 1e-6f * tn + pivmin;
-        for (int it = 0; it < 64 && hi - lo > 2.4e-7f * fmaxf(fabsf(lo), fabsf(hi)) + pivmin; ++it) {
+        float lo = glo - 1e-6f * tn - pivmin, hi = ghi + 1e-6f * tn + pivmin;
+        for (int it = 0; it < 64; ++it) {
+            const bool go = live && hi - lo > 2.4e-7f * fmaxf(fabsf(lo), fabsf(hi)) + pivmin;
+            if (!__builtin_amdgcn_ballot_w64(go)) break;
             const float mid = 0.5f * (lo + hi);
             int cnt = 0;
             float q = dd[0] - mid;
             if (fabsf(q) < pivmin) q = -pivmin;
             cnt += q < 0.f;
+#pragma unroll 8
             for (int i = 1; i < n; ++i) {
-                q = (dd[i] - mid) - ee[i - 1] * ee[i - 1] / q;
+                q = (dd[i] - mid) - e2[i - 1] * __builtin_amdgcn_rcpf(q);
                 if (fabsf(q) < pivmin) q = -pivmin;
                 cnt += q < 0.f;
             }
-            if (cnt > tid) hi = mid; else lo = mid;
+            if (go) {
+                if (cnt > lane) hi = mid; else lo = mid;
+            }
         }
         const float l = 0.5f * (lo + hi);
-        lam[tid] = l;
-        eig_out[(size_t)blockIdx.x * N + (n - 1 - tid)] = l;   // descending (MUSIC_1D.m:31)
+        if (live) {
+            lam[lane] = l;
+            eig_out[(size_t)blockIdx.x * N + (n - 1 - lane)] = l;   // descending (MUSIC_1D.m:31)
+        }
     }
     __syncthreads();
     MU_STAMP(2);
-    // ---- 3. signal eigenvectors of T: block inverse iteration
+    // ---- 3. signal eigenvectors of T: block inverse iteration (lane j = vector j)
     float tnorm = 0.f;
-    for (int i = 0; i < n; ++i) tnorm = fmaxf(tnorm, fabsf(dd[i]) + (i > 0 ? fabsf(ee[i - 1]) : 0.f) + (i < n - 1 ? fabsf(ee[i]) : 0.f));
+    for (int i = 0; i < n; ++i)
+        tnorm = fmaxf(tnorm, fabsf(dd[i]) + (i > 0 ? sqrtf(e2[i - 1]) : 0.f) + (i < n - 1 ? sqrtf(e2[i]) : 0.f));
     const float ptol = 1.2e-7f * tnorm + 1e-30f;
-    if (tid < M) {   // factor T - lambda_j I = P L U (dlagtf)
-        const int j = tid;
-        const float lj = lam[n - 1 - j];
-        float* a = fa[j];   // U diagonal
-        float* b = fb[j];   // U superdiagonal 1
-        float* c = fc[j];   // multipliers (bit 31 of fd = interchange flag kept separately)
-        float* d2 = fd[j];  // U superdiagonal 2
-        for (int i = 0; i < n; ++i) {
-            a[i] = dd[i] - lj;
-            b[i] = i < n - 1 ? ee[i] : 0.f;
-            c[i] = i < n - 1 ? ee[i] : 0.f;
-            d2[i] = 0.f;
-            Y[j][i] = 1.f + 0.0625f * (float)((i * 37 + j * 11) % 17);   // start vector
-        }
-        unsigned long long swp = 0ull;
+#define LU(arr, i) lu[((arr) * MU_NMAX + (i)) * M + lane]
+    unsigned long long swp = 0ull;
+    if (lane < M) {   // dlagtf on T - lambda_j I; carried values in registers, factors to LDS
+        const float lj = lam[n - 1 - lane];
+        float ak = dd[0] - lj;                                // current diagonal
+        float bk = n > 1 ? ee[0] : 0.f;                       // current super 1 (= e_k)
         for (int k = 0; k < n - 1; ++k) {
-            if (fabsf(a[k]) >= fabsf(c[k])) {
-                if (fabsf(a[k]) < ptol) a[k] = copysignf(ptol, a[k]);
-                c[k] = c[k] / a[k];
-                a[k + 1] -= c[k] * b[k];
+            const float ck = ee[k];                           // sub-diagonal e_k
+            const float an = dd[k + 1] - lj;                  // next diagonal
+            const float bn = k < n - 2 ? ee[k + 1] : 0.f;
+            if (fabsf(ak) >= fabsf(ck)) {
+                const float a0 = fabsf(ak) < ptol ? copysignf(ptol, ak) : ak;
+                const float mult = ck / a0;
+                LU(0, k) = a0; LU(1, k) = bk; LU(2, k) = 0.f; LU(3, k) = mult;
+                ak = an - mult * bk;
+                bk = bn;
             } else {
                 swp |= 1ull << k;
-                const float mult = a[k] / c[k];
-                a[k] = c[k];
-                const float tmp = a[k + 1];
-                a[k + 1] = b[k] - mult * tmp;
-                if (k < n - 2) {
-                    d2[k] = b[k + 1];
-                    b[k + 1] = -mult * d2[k];
-                }
-                b[k] = tmp;
-                c[k] = mult;
+                const float mult = ak / ck;
+                LU(0, k) = ck; LU(1, k) = an; LU(2, k) = bn; LU(3, k) = mult;
+                ak = bk - mult * an;
+                bk = -mult * bn;
             }
         }
-        if (fabsf(a[n - 1]) < ptol) a[n - 1] = copysignf(ptol, a[n - 1]);
-        reinterpret_cast<unsigned long long*>(red)[j] = swp;
+        LU(0, n - 1) = fabsf(ak) < ptol ? copysignf(ptol, ak) : ak;
+        for (int i = 0; i < n; ++i) LU(4, i) = 1.f + 0.0625f * (float)((i * 37 + lane * 11) % 17);   // start
     }
-    __syncthreads();
     for (int it = 0; it < MU_ITER; ++it) {
-        if (tid < M) {   // solve (dlagts): forward with the interchanges, then U back-substitution
-            const int j = tid;
-            const unsigned long long swp = reinterpret_cast<unsigned long long*>(red)[j];
-            float* y = Y[j];
+        if (lane < M) {   // dlagts: forward with the interchanges, then U back-substitution
+            float yk = LU(4, 0);
             for (int k = 0; k < n - 1; ++k) {
+                const float yn = LU(4, k + 1), mult = LU(3, k);
                 if (swp >> k & 1ull) {
-                    const float t0 = y[k];
-                    y[k] = y[k + 1];
-                    y[k + 1] = t0 - fc[j][k] * y[k];
+                    LU(4, k) = yn;
+                    yk = yk - mult * yn;
                 } else {
-                    y[k + 1] -= fc[j][k] * y[k];
+                    LU(4, k) = yk;
+                    yk = yn - mult * yk;
                 }
             }
-            y[n - 1] /= fa[j][n - 1];
-            if (n > 1) y[n - 2] = (y[n - 2] - fb[j][n - 2] * y[n - 1]) / fa[j][n - 2];
-            for (int k = n - 3; k >= 0; --k) y[k] = (y[k] - fb[j][k] * y[k + 1] - fd[j][k] * y[k + 2]) / fa[j][k];
-        }
-        __syncthreads();
-        if (w == 0) {   // modified Gram-Schmidt over the M vectors (lane = component)
-            for (int j = 0; j < M; ++j) {
-                float yj = lane < n ? Y[j][lane] : 0.f;
-                for (int i = 0; i < j; ++i) {
-                    const float yi = lane < n ? Y[i][lane] : 0.f;
-                    const float dot = wave_sum(yi * yj);
-                    yj -= dot * yi;
-                }
-                const float nr = wave_sum(yj * yj);
-                yj *= rsqrtf(nr);
-                if (lane < n) Y[j][lane] = yj;
+            float y1 = yk / LU(0, n - 1), y2 = 0.f;
+            LU(4, n - 1) = y1;
+            for (int k = n - 2; k >= 0; --k) {
+                const float yk2 = (LU(4, k) - LU(1, k) * y1 - LU(2, k) * y2) / LU(0, k);
+                LU(4, k) = yk2;
+                y2 = y1;
+                y1 = yk2;
             }
         }
         __syncthreads();
+        for (int j = 0; j < M; ++j) {   // modified Gram-Schmidt (lane = component)
+            float yj = live ? lu[(4 * MU_NMAX + lane) * M + j] : 0.f;
+            for (int i = 0; i < j; ++i) {
+                const float yi = live ? lu[(4 * MU_NMAX + lane) * M + i] : 0.f;
+                yj -= wsum(yi * yj) * yi;
+            }
+            yj *= rsqrtf(wsum(yj * yj));
+            if (live) lu[(4 * MU_NMAX + lane) * M + j] = yj;
+            __syncthreads();
+        }
     }
+#undef LU
     MU_STAMP(3);
-    // q_j = H_0 H_1 ... H_{n-2} y_j (one wave per vector, lane = component)
-    for (int j = w; j < M; j += MU_THREADS / 64) {
-        float2 y = make_float2(lane < n ? Y[j][lane] : 0.f, 0.f);
+    // q_j = H_0 H_1 ... H_{n-2} y_j (lane = component; the M vectors advance together)
+    {
+        float2 y[M];
+#pragma unroll
+        for (int j = 0; j < M; ++j)
+            y[j] = make_float2(j < M && live ? lu[(4 * MU_NMAX + lane) * M + j] : 0.f, 0.f);
         for (int k = n - 2; k >= 0; --k) {
             const float2 tau = taus[k];
-            const float2 v = lane == k + 1 ? make_float2(1.f, 0.f)
-                                           : (lane > k + 1 && lane < n ? A[lane * MU_LDA + k] : make_float2(0.f, 0.f));
-            float2 dot = cmc(v, y);
-            dot.x = wave_sum(dot.x);
-            dot.y = wave_sum(dot.y);
-            const float2 u = cm(tau, cm(v, dot));
-            y = make_float2(y.x - u.x, y.y - u.y);
+            const float2 v = lane == k + 1 ? make_float2(1.f, 0.f) : (lane > k + 1 && live ? A[k * MU_NMAX + lane] : z2);
+#pragma unroll
+            for (int j = 0; j < M; ++j) {
+                if (j < M) {
+                    const float2 pr = cmc(v, y[j]);
+                    const float2 dot = make_float2(wsum(pr.x), wsum(pr.y));
+                    y[j] = csub2(y[j], cm(tau, cm(v, dot)));
+                }
+            }
         }
-        if (lane < n) Qs[j][lane] = y;
+#pragma unroll
+        for (int j = 0; j < M; ++j)
+            if (j < M) Qs[j * MU_NMAX + lane] = y[j];
     }
     __syncthreads();
     MU_STAMP(4);
-    // ---- 4. den(s) = |a(s) - Q_s Q_s^H a(s)|^2, one thread per angle (A's LDS holds den)
+    // ---- 4. den(s) = |a(s) - Q_s Q_s^H a(s)|^2, lane = angle (den overlays A)
     float* den = reinterpret_cast<float*>(A);
-    for (int s = tid; s < S; s += MU_THREADS) {
-        float2 cf[MU_MMAX];
+    // (the lane's 64 steering values are loaded at once and kept for both passes; rows c >= N
+    // of S1T and of Q_s are zero)
+    for (int s = lane; s < S; s += 64) {
+        float2 a[MU_NMAX];
 #pragma unroll
-        for (int m = 0; m < MU_MMAX; ++m) cf[m] = make_float2(0.f, 0.f);
-        for (int c = 0; c < n; ++c) {
-            const float2 a = S1T[(size_t)c * Spad + s];
+        for (int c = 0; c < MU_NMAX; ++c) a[c] = S1T[(size_t)c * Spad + s];
+        float2 cf[M];
 #pragma unroll
-            for (int m = 0; m < MU_MMAX; ++m)
-                if (m < M) cf[m] = cadd2(cf[m], cmc(Qs[m][c], a));
-        }
-        float r2 = 0.f;
-        for (int c = 0; c < n; ++c) {
-            float2 r = S1T[(size_t)c * Spad + s];
+        for (int m = 0; m < M; ++m) cf[m] = z2;
 #pragma unroll
-            for (int m = 0; m < MU_MMAX; ++m)
+        for (int c = 0; c < MU_NMAX; c += 2)
+#pragma unroll
+            for (int m = 0; m < M; ++m)
                 if (m < M) {
-                    const float2 u = cm(Qs[m][c], cf[m]);
-                    r = make_float2(r.x - u.x, r.y - u.y);
+                    const float4 q = *reinterpret_cast<const float4*>(Qs + m * MU_NMAX + c);
+                    cf[m] = cadd2(cf[m], cmc(make_float2(q.x, q.y), a[c]));
+                    cf[m] = cadd2(cf[m], cmc(make_float2(q.z, q.w), a[c + 1]));
                 }
-            r2 += r.x * r.x + r.y * r.y;
+        float r2 = 0.f;
+#pragma unroll
+        for (int c = 0; c < MU_NMAX; c += 2) {
+            float2 r0 = a[c], r1 = a[c + 1];
+#pragma unroll
+            for (int m = 0; m < M; ++m)
+                if (m < M) {
+                    const float4 q = *reinterpret_cast<const float4*>(Qs + m * MU_NMAX + c);
+                    r0 = csub2(r0, cm(make_float2(q.x, q.y), cf[m]));
+                    r1 = csub2(r1, cm(make_float2(q.z, q.w), cf[m]));
+                }
+            r2 += r0.x * r0.x + r0.y * r0.y;
+            r2 += r1.x * r1.x + r1.y * r1.y;
         }
         den[s] = r2;
     }
     __syncthreads();
     MU_STAMP(5);
-    // P = 1 ./ den, P_dB = 10 log10(P / max P) (MUSIC_1D.m:37-41)
-    float pmax = 0.f;
-    for (int s = tid; s < S; s += MU_THREADS) pmax = fmaxf(pmax, 1.f / den[s]);
-    red[tid] = pmax;
-    __syncthreads();
-    for (int h = MU_THREADS / 2; h > 0; h >>= 1) {
-        if (tid < h) red[tid] = fmaxf(red[tid], red[tid + h]);
-        __syncthreads();
-    }
-    pmax = red[0];
+    // ---- 5. P = 1 ./ den, P_dB = 10 log10(P / max P) (MUSIC_1D.m:37-41)
+    float pm = 0.f;
+    for (int s = lane; s < S; s += 64) pm = fmaxf(pm, 1.f / den[s]);
+    const float pmax = wmax(pm);
     float* __restrict__ out = spec_db + (size_t)blockIdx.x * S;
-    for (int s = tid; s < S; s += MU_THREADS) {
+    for (int s = lane; s < S; s += 64) {
         const float db = 10.f * log10f((1.f / den[s]) / pmax);
         den[s] = db;
         out[s] = db;
     }
     __syncthreads();
-    // findpeaks (first sample of a flat top, ends excluded) + the M largest, stable (MUSIC_1D.m:43-47)
-    if (tid == 0) {
-        int best[MU_MMAX];
-        float bval[MU_MMAX];
-        int nb = 0, npk = 0;
-        int prev = 0;   // index of the previous distinct value
-        int t = 1;
-        while (t < S && den[t] == den[0]) ++t;
-        while (t < S) {
-            int u = t + 1;
-            while (u < S && den[u] == den[t]) ++u;   // [t, u) run of equal values
-            if (u < S && den[t] > den[prev] && den[t] > den[u]) {
-                ++npk;
-                const float v = den[t];
-                int pos = nb;
-                while (pos > 0 && v > bval[pos - 1]) --pos;   // strict: earlier index wins ties
-                if (pos < M) {
-                    for (int i = min(nb, M - 1); i > pos; --i) {
-                        best[i] = best[i - 1];
-                        bval[i] = bval[i - 1];
-                    }
-                    best[pos] = t;
-                    bval[pos] = v;
-                    if (nb < M) ++nb;
-                }
-            }
-            prev = t;
-            t = u;
+    // findpeaks (MUSIC_1D.m:43): s is a peak iff it starts a run of equal values entered by a
+    // strict rise and left by a strict fall (ends excluded); then the M largest, ties to the
+    // lower index (stable sort 'descend', :44-47)
+    unsigned long long pkm = 0ull;   // bit t: s = lane + 64 t is a peak
+    int npk = 0;
+    for (int t = 0; t * 64 < S; ++t) {
+        const int s = lane + 64 * t;
+        bool pk = false;
+        if (s >= 1 && s < S - 1 && den[s] > den[s - 1]) {
+            int u = s + 1;
+            while (u < S && den[u] == den[s]) ++u;
+            pk = u < S && den[u] < den[s];
         }
-        int* po = peaks_out + (size_t)blockIdx.x * (MU_MMAX + 1);
-        po[0] = npk;
-        for (int i = 0; i < MU_MMAX; ++i) po[1 + i] = i < nb ? best[i] + 1 : 0;
+        if (pk) pkm |= 1ull << t;
+        npk += __popcll(__builtin_amdgcn_ballot_w64(pk));
+    }
+    int* po = peaks_out + (size_t)blockIdx.x * (MU_MMAX + 1);
+    if (lane == 0) po[0] = npk;
+    for (int r = 0; r < MU_MMAX; ++r) {
+        int sel = 0;
+        if (r < M) {
+            float bv = -3.4e38f;
+            int bs = 1 << 30;
+            for (int t = 0; t * 64 < S; ++t)
+                if (pkm >> t & 1ull) {
+                    const int s = lane + 64 * t;
+                    if (den[s] > bv) { bv = den[s]; bs = s; }   // t ascending: ties keep the lower s
+                }
+            const float gv = wmax(bv);
+            const int gs = wmin_i(bv == gv ? bs : (1 << 30));
+            if (gs < (1 << 30)) {
+                sel = gs + 1;
+                if ((gs & 63) == lane) pkm &= ~(1ull << (gs >> 6));
+            }
+        }
+        if (lane == 0) po[1 + r] = sel;
     }
     MU_STAMP(6);
 #undef MU_STAMP
@@ -593,8 +645,15 @@ int music_run(rsp_music_plan* p, const float2* dX, int n_inst, bool timed, float
         hipLaunchKernelGGL(k_music_cov<false>, dim3(n_inst), dim3(MU_THREADS), 0, p->stream, p->N, p->K, dX, p->d_R);
     MUCHK(hipGetLastError());
     if (timed) MUCHK(hipEventRecord(p->ev[1], p->stream));
-    hipLaunchKernelGGL(k_music_eig, dim3(n_inst), dim3(MU_THREADS), 0, p->stream, p->N, p->M, p->S, p->d_R, p->d_S1T,
-                       p->Spad, p->d_spec, p->d_eig, p->d_peaks, p->d_trace);
+    switch (p->M) {
+#define MU_EIG(MC)                                                                                                \
+    case MC:                                                                                                      \
+        hipLaunchKernelGGL(k_music_eig<MC>, dim3(n_inst), dim3(64), mu_eig_lds_bytes(MC), p->stream, p->N, p->S, \
+                           p->d_R, p->d_S1T, p->Spad, p->d_spec, p->d_eig, p->d_peaks, p->d_trace);                \
+        break;
+        MU_EIG(1) MU_EIG(2) MU_EIG(3) MU_EIG(4) MU_EIG(5) MU_EIG(6) MU_EIG(7) MU_EIG(8)
+#undef MU_EIG
+    }
     MUCHK(hipGetLastError());
     if (timed) {
         MUCHK(hipEventRecord(p->ev[2], p->stream));

@@ -834,6 +834,54 @@ int32_t rsp_cluster_detections(const rsp_detection* dets, int32_t n, const rsp_c
     return RSP_OK;
 }
 
+// Inter-frame track association (main_simulate_echoes_with_array_v8_3.m:253-352): the BFS
+// of :270-304 over the 5-D gate (|dR|, |dV|, |dAz|, |dEl|, |dFrame|) = connected components
+// numbered by smallest member index (component_labels, sweep in Range order); then per cluster,
+// members in log order (:312-335): total power, first-max winner (R, V, El, Power), power-weighted
+// azimuth, first/last frame, count.
+int32_t rsp_inter_frame_cluster(const rsp_track_point* log, int32_t n, const rsp_inter_frame_params* gp,
+                                rsp_track* out, int32_t cap, int32_t* n_out) {
+    if ((!log && n) || n < 0 || !gp || !n_out || cap < 0) return fail(RSP_ERR_INVALID, "bad argument");
+    std::vector<rsp_track_point> pts(log, log + n);
+    std::vector<int> ids;
+    const rsp_inter_frame_params g = *gp;
+    const int nc = n ? component_labels(pts, g.Gate_R, [&](const rsp_track_point& a, const rsp_track_point& b) {
+        return std::fabs(a.Range - b.Range) <= g.Gate_R && std::fabs(a.Velocity - b.Velocity) <= g.Gate_V &&
+               std::fabs(a.iAntAngle - b.iAntAngle) <= g.Gate_Az && std::fabs(a.Angle - b.Angle) <= g.Gate_El &&
+               std::abs(a.iFrame - b.iFrame) <= g.Max_Frame_Gap;
+    }, ids) : 0;
+    std::vector<rsp_track> tr(nc);
+    std::vector<double> ptot(nc, 0.0), paz(nc, 0.0);
+    std::vector<int> win(nc, -1);
+    for (int i = 0; i < n; ++i) {   // members in log order, like detection_log(cluster_mask)
+        const int c = ids[i] - 1;
+        rsp_track& t = tr[c];
+        ptot[c] += pts[i].Power;
+        paz[c] += pts[i].iAntAngle * pts[i].Power;
+        if (win[c] < 0) {
+            t.FirstFrame = t.LastFrame = pts[i].iFrame;
+            t.NumPoints = 0;
+        }
+        if (win[c] < 0 || pts[i].Power > pts[win[c]].Power) win[c] = i;   // [max_power, idx_winner] = max(powers)
+        t.FirstFrame = std::min(t.FirstFrame, pts[i].iFrame);
+        t.LastFrame = std::max(t.LastFrame, pts[i].iFrame);
+        ++t.NumPoints;
+    }
+    for (int c = 0; c < nc; ++c) {
+        const rsp_track_point& w = pts[win[c]];
+        tr[c].Range = w.Range;
+        tr[c].Velocity = w.Velocity;
+        tr[c].Angle = w.Angle;
+        tr[c].Azimuth = paz[c] / ptot[c];
+        tr[c].Power = w.Power;
+        tr[c].reserved = 0;
+    }
+    *n_out = nc;
+    if (out) memcpy(out, tr.data(), sizeof(rsp_track) * std::min<size_t>(cap, tr.size()));
+    if (nc > cap) return fail(RSP_ERR_OVERFLOW, "%d tracks exceed cap %d", nc, cap);
+    return RSP_OK;
+}
+
 int32_t rsp_plan_destroy(rsp_plan* plan) {
     delete plan;
     return RSP_OK;

@@ -20,6 +20,7 @@ from .plan import Plan
 from ._abi import RspError
 from .matio import load_frame, save_frame
 from .music import MusicPlan, MUSIC_1D
+from .tracks import inter_frame_cluster, default_inter_frame_params
 from . import matio
 
 _PLANS = {}

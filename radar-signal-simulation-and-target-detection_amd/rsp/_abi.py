@@ -84,6 +84,22 @@ class MatWVar(ct.Structure):
                 ('dims', ct.POINTER(ct.c_int64)), ('data', ct.c_void_p)]
 
 
+class TrackPoint(ct.Structure):
+    _fields_ = [('Range', ct.c_double), ('Velocity', ct.c_double), ('Angle', ct.c_double), ('Power', ct.c_double),
+                ('iAntAngle', ct.c_double), ('iFrame', ct.c_int32), ('reserved', ct.c_int32)]
+
+
+class InterFrameParams(ct.Structure):
+    _fields_ = [('Gate_R', ct.c_double), ('Gate_V', ct.c_double), ('Gate_Az', ct.c_double), ('Gate_El', ct.c_double),
+                ('Max_Frame_Gap', ct.c_int32), ('reserved', ct.c_int32)]
+
+
+class Track(ct.Structure):
+    _fields_ = [('Range', ct.c_double), ('Velocity', ct.c_double), ('Angle', ct.c_double), ('Azimuth', ct.c_double),
+                ('Power', ct.c_double), ('FirstFrame', ct.c_int32), ('LastFrame', ct.c_int32),
+                ('NumPoints', ct.c_int32), ('reserved', ct.c_int32)]
+
+
 class MusicConfig(ct.Structure):
     _fields_ = [('channel_num', ct.c_int32), ('num_snapshots', ct.c_int32), ('num_sources', ct.c_int32),
                 ('n_scan', ct.c_int32), ('d_over_lambda', ct.c_double), ('scan_rad', _dp), ('max_batch', ct.c_int32)]
@@ -140,6 +156,8 @@ PROTOTYPES = {
                                         ct.c_int32, ct.POINTER(ct.c_int32)]),
     'rsp_mat_save_frame': (ct.c_int32, [ct.c_char_p, _dp, ct.c_int32, ct.c_int32, ct.c_int32, _dp, ct.c_int32,
                                         ct.c_int32, ct.c_int32]),
+    'rsp_inter_frame_cluster': (ct.c_int32, [ct.POINTER(TrackPoint), ct.c_int32, ct.POINTER(InterFrameParams),
+                                             ct.POINTER(Track), ct.c_int32, ct.POINTER(ct.c_int32)]),
     'rsp_music_create': (ct.c_int32, [ct.POINTER(MusicConfig), ct.c_int32, ct.POINTER(_P)]),
     'rsp_music_destroy': (ct.c_int32, [_P]),
     'rsp_music_process': (ct.c_int32, [_P, _P, ct.c_int32, ct.c_int32, ct.POINTER(MusicOut)]),

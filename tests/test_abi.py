@@ -44,7 +44,8 @@ STRUCTS = {'rsp_sig_config': _abi.SigConfig, 'rsp_cfar_params': _abi.CfarParams,
            'rsp_cluster_params': _abi.ClusterParams, 'rsp_precomputed': _abi.Precomputed,
            'rsp_target_in': _abi.TargetIn, 'rsp_target': _abi.Target, 'rsp_detection': _abi.Detection,
            'rsp_frame_out': _abi.FrameOut, 'rsp_sizes': _abi.Sizes, 'rsp_music_config': _abi.MusicConfig,
-           'rsp_music_scene': _abi.MusicScene, 'rsp_music_out': _abi.MusicOut}
+           'rsp_music_scene': _abi.MusicScene, 'rsp_music_out': _abi.MusicOut, 'rsp_track_point': _abi.TrackPoint,
+           'rsp_inter_frame_params': _abi.InterFrameParams, 'rsp_track': _abi.Track}
 
 
 def test_struct_layouts_match_header():
