@@ -100,6 +100,16 @@ def music_cpu_baseline(scene, scan, dl, N, K, M, n=96):
                       'einsum covariance, batched LAPACK eigh, pseudo-spectrum, findpeaks), %.2f s' % (n, el)}
 
 
+def music_traffic():
+    """k_music_cov HBM bytes per 1024-instance launch from the PMC passes (profiles/, made by
+    tools/pmc_traffic.py over tools/music_prof.py 1024), or None."""
+    tf = os.path.join(ROOT, 'profiles', 'pmc_traffic_music5.json')
+    if not os.path.exists(tf):
+        return None
+    with open(tf) as f:
+        return json.load(f).get('k_music_cov')
+
+
 def main_music(a):
     """BASELINE config #5: MUSIC_1D DOA on 64-channel x 1024-snapshot instances (MUSIC_1D.m:21-48).
     One step = one batch of --batch instances (device-resident snapshots, synthesised on the
@@ -159,7 +169,7 @@ def main_music(a):
                           'parallelism': 'instance-sharded x%d' % world},
                'roofline': {'bound': 'mfma', 'kernel': 'k_music_cov', 'achieved': cov_tf,
                             'peak': MFMA_F32_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': cov_tf / MFMA_F32_PEAK_TFLOPS,
-                            'traffic': None, 'kernel_ms': pr['cov_ms'],
+                            'traffic': music_traffic(), 'kernel_ms': pr['cov_ms'],
                             'timing': 'HIP events on the plan stream, %d launches' % a.profile_iters,
                             'stages': stages},
                'cpu_baseline': music_cpu_baseline(scene, scan, dl, N, K, M) if (world == 1 and not a.no_cpu_baseline)
