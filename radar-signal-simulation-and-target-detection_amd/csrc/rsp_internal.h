@@ -59,6 +59,7 @@ struct K2Job {
 
 struct Geometry {
     int C, B, P, N, G;
+    int cpitch;      // device cube channel pitch in complex samples (>= N*P; padded off power-of-two HBM strides)
     int Gp;          // row stride of the magnitude maps (G rounded up to 4 floats)
     int NT, nU, ntiles, Ppad;
     int wc_elems;    // conj(W) entries, [CP][BMAX]

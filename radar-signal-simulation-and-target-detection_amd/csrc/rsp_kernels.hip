@@ -33,6 +33,27 @@ __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 tof2(float2 a) { return f2{a.x, a.y}; }
 __device__ __forceinline__ float2 fromf2(f2 a) { return make_float2(a.x, a.y); }
+
+// Raw buffer resources (SRSRC): 32-bit byte offsets and hardware range checking.  An offset at
+// or past num_records reads 0 / drops the store, so masked lanes need no branch or select.
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+#define RSP_OOB 0x80000000u   // > any buffer this library makes (plans are validated < 2 GB/frame)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ f2 buf_ld_f2(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
+    return f2{__uint_as_float(v.x), __uint_as_float(v.y)};
+}
+__device__ __forceinline__ void buf_st_f2(__amdgpu_buffer_rsrc_t r, unsigned off, f2 x) {
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(x.x), __float_as_uint(x.y)}, r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void buf_st_f1(__amdgpu_buffer_rsrc_t r, unsigned off, float x) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, (int)off, 0, 0);
+}
+// |x| with the hardware square root (v_sqrt_f32, 1 ulp) instead of the correctly rounded
+// sequence (~15 VALU): the magnitude map feeds threshold tests at fp32 noise level anyway
+__device__ __forceinline__ float fast_abs(f2 x) { return __builtin_amdgcn_sqrtf(x.x * x.x + x.y * x.y); }
 __device__ __forceinline__ f2 vmul(f2 a, f2 b) { return a.xx * b + a.yy * f2{-b.y, b.x}; }
 template <bool INV>
 __device__ __forceinline__ f2 vrot(f2 a) {   // * (-i) forward, * (+i) inverse
@@ -306,7 +327,9 @@ __device__ __forceinline__ size_t zaddr(const Geometry& g, int b, int v, int np)
 // ======================================================================================
 // K1: DBF + MTD window + slow-time FFT + fftshift -> compacted rows
 // ======================================================================================
+#ifndef K1_THREADS
 #define K1_THREADS 512
+#endif
 #define K1_SH 4   // LDS pad shift of the slow-time FFT rows (row stride P + P/16)
 
 // Slow-time FFT of every (beam, sample) column in LDS for the runtime log2(P).
@@ -336,11 +359,17 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
     float2* twl = Y + B * NT * Ppad;
     const bool fft = (mode & 2) && g.pow2P;
     const int sh = fft ? K1_SH : 0;
-    if (fft)
-        for (int i = threadIdx.x; i < g.twPp_elems; i += K1_THREADS) twl[i] = k.twPp[i];
-    __syncthreads();
+    // twiddles: global loads issued first, LDS stores after the cube loads are in flight (the
+    // barrier before the FFT orders them), so no load waits behind a barrier at kernel start
+    constexpr int TWPRE = 2;
+    float2 twv[TWPRE];
+#pragma unroll
+    for (int u = 0; u < TWPRE; ++u) {
+        const int i = threadIdx.x + u * K1_THREADS;
+        if (fft && i < g.twPp_elems) twv[u] = k.twPp[i];
+    }
     const float2* __restrict__ x = fp.in[f];
-    const size_t NP = (size_t)g.N * P;   // channel stride
+    const size_t NP = (size_t)g.cpitch;   // channel stride
     if (mode & 1) {
         // ---- Phase A (MFMA): DBF (fsf:93-97) + MTD window (fsf:134) as a real GEMM on the
         // f32 matrix cores: D[16 x 16 pulses] += A[16 x 4 channels] * B[4 channels x 16 pulses],
@@ -359,6 +388,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
         const int ptiles = (P + 31) >> 5;
         const int ntp = NT * ptiles;
         float* Yf = reinterpret_cast<float*>(Y);
+        float sink = 0.f;
         // a wave takes TPW consecutive tiles (pulse tiles of the same sample first), so the
         // 1 KB pulse row of each (channel, sample) is fetched by one wave in one burst
         for (int t0 = wv * TPW; t0 < ntp; t0 += (K1_THREADS / 64) * TPW) {
@@ -396,6 +426,13 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
                                           : make_float4(0.f, 0.f, 0.f, 0.f);
                     }
                 }
+            }
+            if (g.dbg & 128) {   // ablation (timing only): the cube loads alone, nothing computed
+#pragma unroll
+                for (int u = 0; u < TPW; ++u)
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) sink += xv[u][j].x + xv[u][j].y + xv[u][j].z + xv[u][j].w;
+                continue;
             }
 #pragma unroll
             for (int u = 0; u < TPW; ++u) {
@@ -436,6 +473,10 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
                     }
             }
         }
+        if (g.dbg & 128) {
+            if (sink == 1.2345e-30f) fp.z[f][threadIdx.x] = make_float2(sink, 0.f);   // keeps the loads
+            return;
+        }
     } else {
         // ---- transpose only (stage-2 path: input channels are the beams)
         const int items = NT * P;
@@ -463,6 +504,14 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
                 }
             }
         }
+    }
+    if (fft) {
+#pragma unroll
+        for (int u = 0; u < TWPRE; ++u) {
+            const int i = threadIdx.x + u * K1_THREADS;
+            if (i < g.twPp_elems) twl[i] = twv[u];
+        }
+        for (int i = threadIdx.x + TWPRE * K1_THREADS; i < g.twPp_elems; i += K1_THREADS) twl[i] = k.twPp[i];
     }
     __syncthreads();
     trace_stamp(fp, 1);
@@ -520,15 +569,15 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
 __device__ __forceinline__ float cabsf(float2 a) { return sqrtf(a.x * a.x + a.y * a.y); }
 
 struct StoreRdm {   // last inverse pass: keep outputs i in [Lh-1, Lh-1+V) that map to gates < gend;
-                    // also writes |x| (the CFAR input, fsf:184-185) into the magnitude map
-    float2* rdm; float* mag; int G; int Gp; int row0; int rows_total; int Lh1; int g0; int gend;
+                    // also writes |x| (the CFAR input, fsf:184-185) into the magnitude map.
+                    // Branch-free: rejected outputs get an out-of-range buffer offset.
+    __amdgpu_buffer_rsrc_t rdm, mag; int G; int Gp; int row0; int rows_total; int Lh1; int g0; int gend;
     __device__ __forceinline__ void put(int, int row, int o, int, f2 x) const {
         const int gg = g0 + o - Lh1;
         const int rho = row0 + row;
-        if (o >= Lh1 && gg < gend && rho < rows_total) {   // 32-bit offsets: saddr + voffset stores
-            rdm[(unsigned)(rho * G + gg)] = fromf2(x);
-            mag[(unsigned)(rho * Gp + gg)] = sqrtf(x.x * x.x + x.y * x.y);
-        }
+        const bool ok = o >= Lh1 && gg < gend && rho < rows_total;
+        buf_st_f2(rdm, ok ? (unsigned)(rho * G + gg) * 8u : RSP_OOB, x);
+        buf_st_f1(mag, ok ? (unsigned)(rho * Gp + gg) * 4u : RSP_OOB, fast_abs(x));
     }
 };
 
@@ -569,6 +618,7 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     // twiddle tables
     f2 v0[NB0][R0];
     const int lgNT = ilog2(g.NT);
+    const __amdgpu_buffer_rsrc_t zr = buf_rsrc(z, (unsigned)g.B * g.ntiles * P * g.NT * 8u);
 #pragma unroll
     for (int t = 0; t < NB0; ++t) {
         const int beta = tid + t * RSP_THREADS;
@@ -585,16 +635,14 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
             for (int r = 0; r < R0; ++r) {
                 const int n = a + j + r * nb0;
                 const bool ok = rho < rows_total && n >= lo && n <= hi;
-                const f2 x = tof2(z[ok ? (unsigned)(zb + r * nb0 * P) : 0u]);
-                v0[t][r] = ok ? x : f2{0.f, 0.f};
+                v0[t][r] = buf_ld_f2(zr, ok ? (unsigned)(zb + r * nb0 * P) * 8u : RSP_OOB);
             }
         } else {
 #pragma unroll
             for (int r = 0; r < R0; ++r) {
                 const int n = a + j + r * nb0;
                 const bool ok = rho < rows_total && n >= lo && n <= hi;
-                const f2 x = tof2(z[ok ? (unsigned)zaddr(g, b, v, n - lo + off) : 0u]);
-                v0[t][r] = ok ? x : f2{0.f, 0.f};
+                v0[t][r] = buf_ld_f2(zr, ok ? (unsigned)zaddr(g, b, v, n - lo + off) * 8u : RSP_OOB);
             }
         }
     }
@@ -650,7 +698,9 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     // outputs = stitched gates
     const int gend = min(sd.gb, g0 + sd.V);
     fft_range<LGM, 1, NP, RBL, 16, true, true, K2_SH, RSP_THREADS, CMP>(
-        L, rs, rows, twl + NTWF, StoreLds{L}, StoreRdm{rdm, mag, G, g.Gp, row0, rows_total, Lh1, g0, gend});
+        L, rs, rows, twl + NTWF, StoreLds{L}, StoreRdm{buf_rsrc(rdm, (unsigned)rows_total * G * 8u),
+                                                      buf_rsrc(mag, (unsigned)rows_total * g.Gp * 4u), G, g.Gp,
+                                                      row0, rows_total, Lh1, g0, gend});
     trace_stamp(fp, 3);
 }
 
@@ -674,6 +724,10 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k,
     const int tid = threadIdx.x;
 
     if (sd.type == 1) {
+#ifdef K2_ONLY_LGM   // ISA inspection builds: one block size only
+        k2_fft_job<K2_ONLY_LGM, TWG, CMP>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp);
+        if (sd.logM >= 0) return;
+#endif
         switch (sd.logM) {
             case 6: k2_fft_job<6, TWG, CMP>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
             case 7: k2_fft_job<7, TWG, CMP>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
@@ -731,7 +785,7 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k,
                 }
             }
             rdm[(size_t)rho * G + gg] = acc;
-            mag[(size_t)rho * g.Gp + gg] = cabsf(acc);
+            mag[(size_t)rho * g.Gp + gg] = fast_abs(tof2(acc));
         }
     }
 }
@@ -1100,6 +1154,7 @@ __global__ __launch_bounds__(RSP_THREADS) void k_synth(Geometry g, const double*
     const size_t rest = i / g.P;
     const int n = (int)(rest % g.N);
     const int c = (int)(rest / g.N);
+    const size_t o = (size_t)c * g.cpitch + (size_t)n * g.P + m;   // pitched store offset
     double re = 0.0, im = 0.0;
     for (int t = 0; t < nt; ++t) {
         const int ds = tg[t].delay;
@@ -1127,7 +1182,7 @@ __global__ __launch_bounds__(RSP_THREADS) void k_synth(Geometry g, const double*
     sincos(2.0 * M_PI * ub, &sb, &cb);
     re += rr * cb * nscale;
     im += rr * sb * nscale;
-    cube[i] = make_float2((float)re, (float)im);
+    cube[o] = make_float2((float)re, (float)im);
 }
 
 }  // namespace

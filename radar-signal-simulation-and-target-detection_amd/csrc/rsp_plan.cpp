@@ -501,7 +501,8 @@ int ensure_stage(rsp_plan* p, size_t bytes) {
 }
 
 // Copy a host cube (any dtype) into d_dst as complex64.
-int upload_cube(rsp_plan* p, const void* cube, int dtype, size_t elems, float2* d_dst, hipStream_t s) {
+int upload_cube(rsp_plan* p, const void* cube, int dtype, int nch, float2* d_dst, hipStream_t s) {
+    const size_t slab = (size_t)p->g.N * p->g.P, elems = slab * nch;
     int rc = ensure_stage(p, elems * sizeof(float2));
     if (rc) return rc;
     if (dtype == RSP_C64) {
@@ -512,7 +513,8 @@ int upload_cube(rsp_plan* p, const void* cube, int dtype, size_t elems, float2* 
     } else {
         return fail(RSP_ERR_INVALID, "unknown dtype %d", dtype);
     }
-    HIPCHK(hipMemcpyAsync(d_dst, p->h_stage, elems * sizeof(float2), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpy2DAsync(d_dst, (size_t)p->g.cpitch * sizeof(float2), p->h_stage, slab * sizeof(float2),
+                            slab * sizeof(float2), nch, hipMemcpyHostToDevice, s));   // channel slabs at cpitch
     return RSP_OK;
 }
 
@@ -612,6 +614,8 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     p->p_signal_unscaled = pre->P_signal_unscaled;
     Geometry& g = p->g;
     g.C = C; g.B = B; g.P = P; g.N = N; g.G = G;
+    g.cpitch = N * P;
+    if (const char* cp = getenv("RSP_CPAD")) g.cpitch += std::max(0, atoi(cp));   // timing experiments
     g.refR = cfar->refCells_R; g.guardR = cfar->guardCells_R; g.refV = cfar->refCells_V; g.guardV = cfar->guardCells_V;
     g.T = (float)cfar->T_CFAR;
     g.max_dets = 1 << 16;
@@ -688,6 +692,7 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     g.pow2P = is_pow2(P) && P >= 16 && P <= 512;   // Stockham range of k1_fft; else direct DFT
     g.Ppad = g.pow2P ? P + P / 16 : P + 4;   // pow2: + one pad per 16 (K1_SH), see rsp_kernels.hip
     g.NT = 8;
+    if (const char* nt = getenv("RSP_NT")) g.NT = std::max(1, std::min(8, atoi(nt)));   // timing experiments
     while (g.NT > 1 && ((size_t)B * g.NT * g.Ppad * sizeof(float2) > 80 * 1024 || (g.pow2P && B * g.NT * P > 8192)))
         g.NT >>= 1;
     if ((size_t)B * g.NT * g.Ppad * sizeof(float2) > 160 * 1024 || (g.pow2P && B * g.NT * P > 8192))
@@ -792,7 +797,7 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     p->rdm_elems = (size_t)B * P * G;
     g.Gp = (G + 3) & ~3;
     p->mag_elems = (size_t)B * P * g.Gp;
-    if ((rc = p->dalloc(&p->d_cube, (size_t)std::max(C, B) * N * P))) return bail(rc);
+    if ((rc = p->dalloc(&p->d_cube, (size_t)std::max(C, B) * g.cpitch))) return bail(rc);
     {
         const char* nl = getenv("RSP_NLANES");
         if (nl) p->nlanes = std::max(1, std::min(RSP_LANES, atoi(nl)));
@@ -890,7 +895,7 @@ int32_t rsp_plan_destroy(rsp_plan* plan) {
 int32_t rsp_query_sizes(const rsp_plan* p, rsp_sizes* s) {
     if (!p || !s) return fail(RSP_ERR_INVALID, "null argument");
     const Geometry& g = p->g;
-    s->cube_elems = (int64_t)g.P * g.N * g.C;
+    s->cube_elems = (int64_t)g.cpitch * g.C;
     s->rdm_elems = (int64_t)g.P * g.G * g.B;
     s->cfar_map_elems = (int64_t)g.P * g.G * std::max(g.B - 1, 0);
     s->P = g.P; s->N = g.N; s->C = g.C; s->B = g.B; s->G = g.G;
@@ -907,7 +912,7 @@ int32_t rsp_process_cube(rsp_plan* p, const void* cube, int32_t dtype, int32_t l
     HIPCHK(hipSetDevice(p->device));
     int rc = drain_all(p);
     if (rc) return rc;
-    if ((rc = upload_cube(p, cube, dtype, (size_t)p->g.P * p->g.N * p->g.C, p->d_cube, p->lanes[0].stream))) return rc;
+    if ((rc = upload_cube(p, cube, dtype, p->g.C, p->d_cube, p->lanes[0].stream))) return rc;
     return run_sync_frame(p, p->d_cube, frame_idx, out);
 }
 
@@ -1001,7 +1006,7 @@ int32_t rsp_process_stage2(rsp_plan* p, const void* iq, int32_t dtype, double* m
     Lane& L = p->lanes[0];
     Geometry gs = p->g;
     gs.C = gs.B;   // input channels are the beams; K1 transposes only (no DBF, no MTD)
-    if ((rc = upload_cube(p, iq, dtype, (size_t)gs.B * gs.N * gs.P, p->d_cube, L.stream))) return rc;
+    if ((rc = upload_cube(p, iq, dtype, gs.B, p->d_cube, L.stream))) return rc;
     if (!p->d_aux && (rc = p->dalloc(&p->d_aux, p->rdm_elems))) return rc;
     const float2* in[1] = {p->d_cube};
     const FramePtrs fp = lane_ptrs(p, L, in, 1);
