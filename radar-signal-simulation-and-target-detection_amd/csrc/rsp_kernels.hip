@@ -332,16 +332,31 @@ __device__ __forceinline__ size_t zaddr(const Geometry& g, int b, int v, int np)
 #endif
 #define K1_SH 4   // LDS pad shift of the slow-time FFT rows (row stride P + P/16)
 
-// Slow-time FFT of every (beam, sample) column in LDS for the runtime log2(P).
-__device__ __forceinline__ void k1_fft(int lgp, float2* Y, int Ppad, int ncols, const float2* twl) {
+// Last slow-time FFT pass straight from registers to z with fftshift (fsf:135): column
+// row = b NT + nl, frequency o -> Doppler cell v = (o + P/2) mod P.  16 lanes of a butterfly
+// group write consecutive v of one column (64 B apart) and the next 16 lanes the neighbouring
+// column (+8 B), so the lines fill within the workgroup.
+struct StoreZ {
+    __amdgpu_buffer_rsrc_t z; int lgNT, ntiles, tile, P, half;
+    __device__ __forceinline__ void put(int, int row, int o, int, f2 x) const {
+        const int b = row >> lgNT, nl = row & ((1 << lgNT) - 1);
+        const int v = (o + half) & (P - 1);
+        buf_st_f2(z, (unsigned)(((((b * ntiles + tile) * P + v) << lgNT) + nl)) * 8u, x);
+    }
+};
+
+// Slow-time FFT of every (beam, sample) column in LDS for the runtime log2(P); the last pass
+// stores through `last`.
+template <class StLast>
+__device__ __forceinline__ void k1_fft(int lgp, float2* Y, int Ppad, int ncols, const float2* twl, const StLast& last) {
     StoreLds st{Y};
     switch (lgp) {
-        case 4: fft_passes<4, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, st); break;
-        case 5: fft_passes<5, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, st); break;
-        case 6: fft_passes<6, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, st); break;
-        case 7: fft_passes<7, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, st); break;
-        case 8: fft_passes<8, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, st); break;
-        default: fft_passes<9, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, st); break;
+        case 4: fft_passes<4, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
+        case 5: fft_passes<5, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
+        case 6: fft_passes<6, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
+        case 7: fft_passes<7, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
+        case 8: fft_passes<8, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
+        default: fft_passes<9, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
     }
 }
 
@@ -465,7 +480,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
                     for (int i = 0; i < 4; ++i) {   // D row m = 4*grp + i: beam mb*8 + (m & 7), part m >> 3
                         const int m = 4 * grp + i;
                         const int b = mb * 8 + (m & 7);
-                        if (b < B) {
+                        if (b < B && !(g.dbg & 1024)) {   // RSP_ABLATE=1024 skips the LDS writes
                             float* colp = Yf + 2 * (b * NT + nlv[u]) * Ppad + (m >> 3);
                             colp[2 * i0] = acc[mb][0][i] * w0;
                             colp[2 * i1] = acc[mb][1][i] * w1;
@@ -528,21 +543,12 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
     }
     const int half = P >> 1;
     if (fft) {
-        // ---- Phase B: P-point FFT of every (b, nl) column (fsf:135)
-        if (!(g.dbg & 2)) k1_fft(g.logP, Y, Ppad, B * NT, twl);   // RSP_ABLATE=2 skips it
+        // ---- Phase B + C: P-point FFT of every (b, nl) column (fsf:135); the last pass applies
+        // fftshift and stores the [P][NT] slabs from registers
+        const StoreZ sz{buf_rsrc(z, (unsigned)B * g.ntiles * zslab * 8u), lgNT, g.ntiles, tile, P, half};
+        k1_fft(g.logP, Y, Ppad, B * NT, twl, sz);
         trace_stamp(fp, 2);
-        // ---- Phase C: fftshift (fsf:135) + coalesced store of the [P][NT] slabs
-        for (int e = threadIdx.x; e < B * zslab; e += K1_THREADS) {
-            const int b = e / zslab, rem = e - b * zslab;
-            const int v = rem >> lgNT, nl = rem & (NT - 1);
-            int src = v - half;
-            if (src < 0) src += P;
-            z[((size_t)b * g.ntiles + tile) * zslab + rem] = Y[(b * NT + nl) * Ppad + src + (src >> K1_SH)];
-        }
-        if (fp.trace) {
-            __syncthreads();
-            trace_stamp(fp, 3);
-        }
+        if (fp.trace) trace_stamp(fp, 3);
     } else {
         // non power-of-two P: direct DFT straight to global (O(P^2) per column)
         for (int e = threadIdx.x; e < B * zslab; e += K1_THREADS) {

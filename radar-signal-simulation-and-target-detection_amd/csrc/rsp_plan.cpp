@@ -129,6 +129,7 @@ struct Lane {
     hipStream_t ks = nullptr;       // where the lane's K1-K3 run: the plan's shared kernel stream, or `stream`
     hipEvent_t kdone = nullptr;     // K3 of the lane's batch done (on ks)
     hipEvent_t ready = nullptr;     // work queued on `stream` before the batch (uploads), awaited by ks
+    hipEvent_t k1done = nullptr;    // K1 of the lane's batch done (pipelined queue: on the plan's K1 stream)
     hipEvent_t tev[4] = {};         // live stage timing: before K1, after K1, K2, K3 (on ks)
     bool timed = false;
     hipEvent_t done = nullptr;
@@ -179,6 +180,9 @@ struct rsp_plan {
     // all batches run back to back on ONE kernel stream (every kernel has the chip to itself)
     // while the lanes' streams carry the read-back.
     hipStream_t kstream = nullptr;
+    // RSP_QUEUE=pipe: every K1 runs on one K1 stream and each lane's K2/K3 wait for their K1, so
+    // K1 of batch i+1 (HBM-bound) runs beside K2/K3 of batch i (VALU-bound)
+    hipStream_t k1stream = nullptr;
     // live stage timing of the queue (rsp_set_stage_timing): HIP events around K1/K2/K3 of
     // every batch, summed at harvest
     bool time_stages = false;
@@ -213,17 +217,20 @@ struct rsp_plan {
 rsp_plan::~rsp_plan() {
     (void)hipSetDevice(device);
     if (kstream) (void)hipStreamSynchronize(kstream);
+    if (k1stream) (void)hipStreamSynchronize(k1stream);
     for (auto& L : lanes) {
         if (L.stream) (void)hipStreamSynchronize(L.stream);
         if (L.h_dets) (void)hipHostFree(L.h_dets);
         if (L.done) (void)hipEventDestroy(L.done);
         if (L.kdone) (void)hipEventDestroy(L.kdone);
         if (L.ready) (void)hipEventDestroy(L.ready);
+        if (L.k1done) (void)hipEventDestroy(L.k1done);
         for (auto& e : L.tev)
             if (e) (void)hipEventDestroy(e);
         if (L.stream) (void)hipStreamDestroy(L.stream);
     }
     if (kstream) (void)hipStreamDestroy(kstream);
+    if (k1stream) (void)hipStreamDestroy(k1stream);
     if (h_stage) (void)hipHostFree(h_stage);
     for (void* p : dev_allocs) (void)hipFree(p);
 }
@@ -376,6 +383,7 @@ int setup_lane(rsp_plan* p, Lane& L) {
     HIPCHK(hipEventCreateWithFlags(&L.done, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&L.kdone, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&L.ready, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&L.k1done, hipEventDisableTiming));
     for (auto& e : L.tev) HIPCHK(hipEventCreate(&e));
     L.ks = p->kstream ? p->kstream : L.stream;
     int rc;
@@ -410,7 +418,17 @@ int launch_batch(rsp_plan* p, Lane& L, const float2* const* in, const int* ids, 
     }
     L.timed = p->time_stages;
     if (L.timed) HIPCHK(hipEventRecord(L.tev[0], L.ks));
-    HIPCHK(launch_k1(p->g, p->k, fp, nf, 3, p->g.C, L.ks));
+    if (p->k1stream && !L.timed) {
+        // K1 on the plan's K1 stream after whatever the lane queued (the lane's previous batch
+        // was harvested before this launch, so its z buffer is free); K2 waits for this K1
+        HIPCHK(hipEventRecord(L.ready, L.stream));
+        HIPCHK(hipStreamWaitEvent(p->k1stream, L.ready, 0));
+        HIPCHK(launch_k1(p->g, p->k, fp, nf, 3, p->g.C, p->k1stream));
+        HIPCHK(hipEventRecord(L.k1done, p->k1stream));
+        HIPCHK(hipStreamWaitEvent(L.ks, L.k1done, 0));
+    } else {
+        HIPCHK(launch_k1(p->g, p->k, fp, nf, 3, p->g.C, L.ks));
+    }
     if (L.timed) HIPCHK(hipEventRecord(L.tev[1], L.ks));
     HIPCHK(launch_k2(p->g, p->k, fp, nf, p->g.B * p->g.P, L.ks));
     if (L.timed) HIPCHK(hipEventRecord(L.tev[2], L.ks));
@@ -803,6 +821,8 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
         if (nl) p->nlanes = std::max(1, std::min(RSP_LANES, atoi(nl)));
         const char* q = getenv("RSP_QUEUE");
         if (q && !strcmp(q, "serial") && hipStreamCreateWithFlags(&p->kstream, hipStreamNonBlocking) != hipSuccess)
+            return bail(fail(RSP_ERR_DEVICE, "hipStreamCreateWithFlags failed"));
+        if (q && !strcmp(q, "pipe") && hipStreamCreateWithFlags(&p->k1stream, hipStreamNonBlocking) != hipSuccess)
             return bail(fail(RSP_ERR_DEVICE, "hipStreamCreateWithFlags failed"));
     }
     for (auto& L : p->lanes)

@@ -8,7 +8,7 @@ the GPU.  There is no CPU fallback: if the library is missing, ``lib()`` raises.
 import ctypes as ct
 import os
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'librsp.so')
+LIB_PATH = os.environ.get('RSP_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'librsp.so')   # RSP_LIB: timing experiments
 
 RSP_OK, RSP_ERR_INVALID, RSP_ERR_UNSUPPORTED, RSP_ERR_DEVICE, RSP_ERR_NOMEM, RSP_ERR_OVERFLOW = 0, -1, -2, -3, -4, -5
 RSP_C64, RSP_C128 = 1, 2
