@@ -38,7 +38,7 @@ def parse():
     ap.add_argument('--steps', type=int, default=4000)
     ap.add_argument('--warmup', type=int, default=200)
     ap.add_argument('--config', default='x2')
-    ap.add_argument('--fpl', type=int, default=4, help='frames per launch')
+    ap.add_argument('--fpl', type=int, default=8, help='frames per launch (8: fewest tail rounds, measured)')
     ap.add_argument('--ring', type=int, default=8, help='distinct device-resident frame cubes')
     ap.add_argument('--profile-iters', type=int, default=50)
     ap.add_argument('--cpu-frames', type=int, default=0, help='oracle frames for cpu_baseline (0 = auto ~15 s)')

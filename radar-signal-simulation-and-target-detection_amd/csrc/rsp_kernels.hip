@@ -743,11 +743,12 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k,
             default: k2_fft_job<11, TWG, CMP>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
         }
     } else {
-        // direct FIR (narrow segment): filter() + circshift(-fir_delay) (fsf:111-112)
+        // direct FIR (narrow segment): filter() + circshift(-fir_delay) (fsf:111-112).  Each
+        // staged row carries ntaps - 1 leading zeros (filter()'s zero state / samples before lo),
+        // so the tap loop is branch-free.
         const int W = hi - lo + 1;
-        const int nw = rows * W;
-        float* taps = reinterpret_cast<float*>(L + nw);
-        for (int e = tid; e < sd.ntaps; e += RSP_THREADS) taps[e] = k.taps[sd.taps_off + e];
+        const int PADL = sd.ntaps - 1, WP = W + PADL;
+        const int nw = rows * WP;
         for (int e0 = 0; e0 < nw; e0 += 16 * RSP_THREADS) {
             float2 val[16];
 #pragma unroll
@@ -755,9 +756,9 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k,
                 const int e = e0 + tid + u * RSP_THREADS;
                 val[u] = make_float2(0.f, 0.f);
                 if (e < nw) {
-                    const int rl = e / W, i = e - rl * W;
+                    const int rl = e / WP, i = e - rl * WP - PADL;
                     const int rho = row0 + rl;
-                    if (rho < rows_total) {
+                    if (rho < rows_total && i >= 0) {
                         const int b = rho / P, v = rho - b * P;
                         val[u] = z[zaddr(g, b, v, i + off)];
                     }
@@ -769,30 +770,54 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k,
                 if (e < nw) L[e] = val[u];
             }
         }
+        float* tp = reinterpret_cast<float*>(L + nw);   // taps: LDS broadcast reads
+        for (int e = tid; e < sd.ntaps; e += RSP_THREADS) tp[e] = k.taps[sd.taps_off + e];
         __syncthreads();
+        trace_stamp(fp, 1);
         const int nout = sd.gb - sd.ga;
-        for (int e = tid; e < rows * nout; e += RSP_THREADS) {
-            const int rl = e / nout, gi = e - rl * nout;
+        // 4 consecutive gates per thread: the 4 outputs share a register window that slides one
+        // sample per tap (1 LDS read + 4 FMAs per tap); a group whose circshift index wraps
+        // mid-group takes the per-gate loop
+        const int ngrp = (nout + 3) >> 2;
+        for (int e = tid; e < rows * ngrp; e += RSP_THREADS) {
+            const int rl = e / ngrp, q0 = 4 * (e - rl * ngrp);
             const int rho = row0 + rl;
             if (rho >= rows_total) continue;
-            const int gg = sd.ga + gi;
-            int kk = (gg + sd.delay) % sd.Ls;
-            if (kk < 0) kk += sd.Ls;
-            const int nbase = sd.seg_lo + kk;          // sample of tap 0
-            const float2* row = L + rl * W;
-            float2 acc = make_float2(0.f, 0.f);
-            for (int j = 0; j < sd.ntaps; ++j) {
-                const int n = nbase - j;
-                if (n < lo) break;                      // zero state of filter() / samples before lo
-                if (n <= hi) {
-                    const float2 xv = row[n - lo];
-                    acc.x += taps[j] * xv.x;
-                    acc.y += taps[j] * xv.y;
+            const int gg0 = sd.ga + q0;
+            int kk0 = (gg0 + sd.delay) % sd.Ls;
+            if (kk0 < 0) kk0 += sd.Ls;
+            const float2* row = L + rl * WP + PADL - lo + sd.seg_lo;   // row[kk] = x(seg_lo + kk)
+            if (q0 + 4 <= nout && kk0 + 3 < sd.Ls) {
+                const float2* xr = row + kk0;
+                f2 w0 = tof2(xr[0]), w1 = tof2(xr[1]), w2 = tof2(xr[2]), w3 = tof2(xr[3]);
+                float t = tp[0];
+                f2 a0 = t * w0, a1 = t * w1, a2 = t * w2, a3 = t * w3;
+#pragma unroll 4
+                for (int j = 1; j < sd.ntaps; ++j) {
+                    w3 = w2; w2 = w1; w1 = w0;
+                    w0 = tof2(xr[-j]);
+                    t = tp[j];
+                    a0 += t * w0; a1 += t * w1; a2 += t * w2; a3 += t * w3;
+                }
+                float2* ro = rdm + (size_t)rho * G + gg0;
+                float* mo = mag + (size_t)rho * g.Gp + gg0;
+                ro[0] = fromf2(a0); ro[1] = fromf2(a1); ro[2] = fromf2(a2); ro[3] = fromf2(a3);
+                mo[0] = fast_abs(a0); mo[1] = fast_abs(a1); mo[2] = fast_abs(a2); mo[3] = fast_abs(a3);
+            } else {
+                for (int q = 0; q < 4 && q0 + q < nout; ++q) {
+                    const int gg = gg0 + q;
+                    int kk = (gg + sd.delay) % sd.Ls;
+                    if (kk < 0) kk += sd.Ls;
+                    const float2* xr = row + kk;
+                    f2 acc = f2{0.f, 0.f};
+                    for (int j = 0; j < sd.ntaps; ++j) acc += tp[j] * tof2(xr[-j]);
+                    rdm[(size_t)rho * G + gg] = fromf2(acc);
+                    mag[(size_t)rho * g.Gp + gg] = fast_abs(acc);
                 }
             }
-            rdm[(size_t)rho * G + gg] = acc;
-            mag[(size_t)rho * g.Gp + gg] = fast_abs(tof2(acc));
         }
+        trace_stamp(fp, 2);
+        trace_stamp(fp, 3);
     }
 }
 

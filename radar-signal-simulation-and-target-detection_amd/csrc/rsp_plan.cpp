@@ -667,8 +667,12 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
         }
         s.lo = lo; s.hi = hi;
         const int W = hi - lo + 1;
-        s.rows_per_wg = std::max(1, std::min(8, (RSP_K2_POINTS - s.ntaps / 2 - 8) / W));
-        if (W * s.rows_per_wg + (s.ntaps + 1) / 2 > RSP_K2_POINTS + RSP_K2_POINTS / 16)
+        const int WP = W + s.ntaps - 1;   // staged row: ntaps - 1 leading zeros (k2_pc narrow path)
+        // 8 rows per workgroup (measured best of 1/2/4/8 at x2)
+        int nrw = 8;
+        if (const char* e = getenv("RSP_NARROW_ROWS")) nrw = std::max(1, std::min(8, atoi(e)));   // timing experiments
+        s.rows_per_wg = std::max(1, std::min(nrw, (RSP_K2_POINTS + RSP_K2_POINTS / 16 - (s.ntaps + 1) / 2) / WP));
+        if (WP * s.rows_per_wg + (s.ntaps + 1) / 2 > RSP_K2_POINTS + RSP_K2_POINTS / 16)
             return bail(fail(RSP_ERR_UNSUPPORTED, "narrow segment window %d samples too long", W));
         s.taps_off = (int)taps.size();
         for (int j = 0; j < s.ntaps; ++j) taps.push_back((float)pre->MF_narrow[j]);
