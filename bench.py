@@ -274,9 +274,10 @@ def main():
         tf = os.path.join(ROOT, 'profiles', 'pmc_traffic_%s.json' % a.config)
         if os.path.exists(tf):
             with open(tf) as f:
-                tr = json.load(f).get(dom['stage'])
-            if tr is not None:   # the PMC passes run frames_per_launch = 4 like the default bench
-                traffic = tr * dom['frames_per_launch'] / 4.0
+                tj = json.load(f)
+            tr = tj.get(dom['stage'])
+            if tr is not None:   # scaled from the PMC passes' frames per launch to this run's
+                traffic = tr * dom['frames_per_launch'] / float(tj.get('_frames_per_launch', 4))
                 dom['pmc_traffic_bytes'] = traffic
         frame_alg_bytes = sz.C * sz.N * sz.P * 8 + cells * 8
         out = {

@@ -71,6 +71,7 @@ struct Geometry {
     float T;
     int max_dets;
     int dbg;         // RSP_ABLATE bit mask: timing-only ablations (outputs invalid when set)
+    int ncu;         // compute units of the device (persistent K1 grid)
     // used fast-time samples as <= RSP_MAX_IVL intervals: compacted n' in [ivl_start[q],
     // ivl_start[q+1]) is sample ivl_lo[q] + n' - ivl_start[q] (kernel-argument lookup, no
     // dependent global load before the cube loads)

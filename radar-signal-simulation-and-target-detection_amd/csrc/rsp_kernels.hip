@@ -45,8 +45,12 @@ __device__ __forceinline__ f2 buf_ld_f2(__amdgpu_buffer_rsrc_t r, unsigned off) 
     const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
     return f2{__uint_as_float(v.x), __uint_as_float(v.y)};
 }
+#ifndef RSP_ST_AUX
+#define RSP_ST_AUX 0
+#endif
+template <int AUX = 0>
 __device__ __forceinline__ void buf_st_f2(__amdgpu_buffer_rsrc_t r, unsigned off, f2 x) {
-    __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(x.x), __float_as_uint(x.y)}, r, (int)off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(x.x), __float_as_uint(x.y)}, r, (int)off, 0, AUX);
 }
 __device__ __forceinline__ void buf_st_f1(__amdgpu_buffer_rsrc_t r, unsigned off, float x) {
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, (int)off, 0, 0);
@@ -341,7 +345,7 @@ struct StoreZ {
     __device__ __forceinline__ void put(int, int row, int o, int, f2 x) const {
         const int b = row >> lgNT, nl = row & ((1 << lgNT) - 1);
         const int v = (o + half) & (P - 1);
-        buf_st_f2(z, (unsigned)(((((b * ntiles + tile) * P + v) << lgNT) + nl)) * 8u, x);
+        buf_st_f2<RSP_ST_AUX>(z, (unsigned)(((((b * ntiles + tile) * P + v) << lgNT) + nl)) * 8u, x);
     }
 };
 
@@ -546,7 +550,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
         // ---- Phase B + C: P-point FFT of every (b, nl) column (fsf:135); the last pass applies
         // fftshift and stores the [P][NT] slabs from registers
         const StoreZ sz{buf_rsrc(z, (unsigned)B * g.ntiles * zslab * 8u), lgNT, g.ntiles, tile, P, half};
-        k1_fft(g.logP, Y, Ppad, B * NT, twl, sz);
+        if (!(g.dbg & 2)) k1_fft(g.logP, Y, Ppad, B * NT, twl, sz);   // RSP_ABLATE=2: no FFT, no store
         trace_stamp(fp, 2);
         if (fp.trace) trace_stamp(fp, 3);
     } else {
@@ -569,6 +573,125 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
     }
 }
 
+// K1, persistent and software-pipelined (the default for power-of-two P when one load round
+// covers a tile): one workgroup per CU walks the (frame, tile) list with two LDS tile buffers.
+// While tile T's slow-time FFT runs out of one buffer and its last pass streams z to HBM, the
+// cube loads of the workgroup's next tile are already in flight in registers; the DBF of that
+// tile then fills the other buffer.  HBM reads and writes overlap instead of alternating
+// round by round.  Same arithmetic as k1_dbf_mtd (mode 3).
+template <int BMAX, int CP, int LGP>
+__global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevConsts k, FramePtrs fp, int nf) {
+    extern __shared__ __attribute__((aligned(16))) float2 Y[];   // buf 0 | buf 1 ([B][NT][Ppad] each) | twiddles
+    const int B = g.B, C = g.C, P = g.P, NT = g.NT, Ppad = g.Ppad;
+    const int bufsz = B * NT * Ppad;
+    float2* twl = Y + 2 * bufsz;
+    const int total = nf * g.ntiles;
+    int T = blockIdx.x;
+    if (T >= total) return;
+    for (int i = threadIdx.x; i < g.twPp_elems; i += K1_THREADS) twl[i] = k.twPp[i];
+    constexpr int NJ = CP / 4, MB = BMAX <= 8 ? 1 : 2, TPW = (16 / NJ) / MB > 0 ? (16 / NJ) / MB : 1;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, grp = lane >> 4, col = lane & 15;
+    float are[MB][NJ], aim[MB][NJ];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            are[mb][j] = k.Atab[((mb * NJ + j) * 2 + 0) * 64 + lane];
+            aim[mb][j] = k.Atab[((mb * NJ + j) * 2 + 1) * 64 + lane];
+        }
+    // this lane's sub-tiles are the same for every tile: (sample nl, pulses p, p + 1) and their
+    // window values (launch_k1 guarantees one round: NT * ptiles <= waves * TPW)
+    const int ptiles = (P + 31) >> 5, ntp = NT * ptiles;
+    int nlv[TPW], pv[TPW];
+    float w0v[TPW], w1v[TPW];
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) {
+        const int t = wv * TPW + u;
+        const int nl = t / ptiles;
+        pv[u] = ((t - nl * ptiles) << 5) + 2 * col;
+        nlv[u] = (t < ntp && pv[u] < P) ? nl : -1;
+        const float2 w01 = nlv[u] >= 0 ? *reinterpret_cast<const float2*>(k.win + pv[u]) : make_float2(0.f, 0.f);
+        w0v[u] = w01.x;
+        w1v[u] = w01.y;
+    }
+    const size_t NPc = (size_t)g.cpitch;
+    float4 xv[TPW][NJ];
+    auto issue = [&](int TT) {   // cube loads of tile TT (fsf:93 operands) into xv
+        const int f = TT / g.ntiles, tile = TT - f * g.ntiles;
+        const float2* __restrict__ x = fp.in[f];
+#pragma unroll
+        for (int u = 0; u < TPW; ++u) {
+            const int np = tile * NT + nlv[u];
+            int n = -1;
+            if (nlv[u] >= 0 && np < g.nU) {
+                int q = 0;
+#pragma unroll
+                for (int i = 1; i < RSP_MAX_IVL; ++i)
+                    if (i < g.nivl && np >= g.ivl_start[i]) q = i;
+                n = g.ivl_lo[q] + np - g.ivl_start[q];
+            }
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int c = min(4 * j + grp, C - 1);
+                xv[u][j] = n >= 0 ? *reinterpret_cast<const float4*>(x + (size_t)c * NPc + (size_t)n * P + pv[u])
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+    };
+    auto dbf = [&](float2* buf) {   // MFMA DBF + window of xv into buf (padded rows, K1_SH)
+        float* Yf = reinterpret_cast<float*>(buf);
+#pragma unroll
+        for (int u = 0; u < TPW; ++u) {
+            if (nlv[u] < 0) continue;
+            f32x4 acc[MB][2];
+#pragma unroll
+            for (int mb = 0; mb < MB; ++mb) {
+                acc[mb][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+                acc[mb][1] = acc[mb][0];
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(are[mb][j], xv[u][j].x, acc[mb][0], 0, 0, 0);
+                    acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(aim[mb][j], xv[u][j].y, acc[mb][0], 0, 0, 0);
+                    acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(are[mb][j], xv[u][j].z, acc[mb][1], 0, 0, 0);
+                    acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(aim[mb][j], xv[u][j].w, acc[mb][1], 0, 0, 0);
+                }
+            }
+            const int p = pv[u];
+            const int i0 = p + (p >> K1_SH), i1 = (p + 1) + ((p + 1) >> K1_SH);
+#pragma unroll
+            for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int m = 4 * grp + i;
+                    const int b = mb * 8 + (m & 7);
+                    if (b < B) {
+                        float* colp = Yf + 2 * (b * NT + nlv[u]) * Ppad + (m >> 3);
+                        colp[2 * i0] = acc[mb][0][i] * w0v[u];
+                        colp[2 * i1] = acc[mb][1][i] * w1v[u];
+                    }
+                }
+        }
+    };
+    const int zslab = P * NT, lgNT = ilog2(NT), half = P >> 1;
+    issue(T);
+    dbf(Y);
+    __syncthreads();
+    int cur = 0;
+    for (; T < total; T += gridDim.x) {
+        const int Tn = T + gridDim.x;
+        if (Tn < total) issue(Tn);   // next tile's loads fly during this tile's FFT + z stores
+        const int f = T / g.ntiles, tile = T - f * g.ntiles;
+        if (tile == 0 && threadIdx.x == 0 && fp.count[f]) *fp.count[f] = 0;   // K3's detection counter
+        float2* __restrict__ z = fp.z[f];
+        const StoreZ sz{buf_rsrc(z, (unsigned)B * g.ntiles * zslab * 8u), lgNT, g.ntiles, tile, P, half};
+        fft_passes<LGP, 0, 0, 16, false, K1_SH, K1_THREADS>(Y + cur * bufsz, Ppad, B * NT, twl,
+                                                           StoreLds{Y + cur * bufsz}, sz);   // ends with a barrier
+        if (Tn < total) dbf(Y + (cur ^ 1) * bufsz);
+        __syncthreads();
+        cur ^= 1;
+    }
+}
+
 // ======================================================================================
 // K2: pulse compression of every row (fsf:101-126)
 // ======================================================================================
@@ -582,7 +705,7 @@ struct StoreRdm {   // last inverse pass: keep outputs i in [Lh-1, Lh-1+V) that 
         const int gg = g0 + o - Lh1;
         const int rho = row0 + row;
         const bool ok = o >= Lh1 && gg < gend && rho < rows_total;
-        buf_st_f2(rdm, ok ? (unsigned)(rho * G + gg) * 8u : RSP_OOB, x);
+        buf_st_f2<RSP_ST_AUX>(rdm, ok ? (unsigned)(rho * G + gg) * 8u : RSP_OOB, x);
         buf_st_f1(mag, ok ? (unsigned)(rho * Gp + gg) * 4u : RSP_OOB, fast_abs(x));
     }
 };
@@ -1230,6 +1353,27 @@ static hipError_t allow_lds(K kernel, size_t bytes) {
 template <int BMAX, int CP>
 static hipError_t launch_k1_t(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int mode,
                               hipStream_t s) {
+    constexpr int NJ = CP / 4, MB = BMAX <= 8 ? 1 : 2, TPW = (16 / NJ) / MB > 0 ? (16 / NJ) / MB : 1;
+    const size_t ldsp = ((size_t)2 * g.B * g.NT * g.Ppad + g.P) * sizeof(float2);
+    if (mode == 3 && g.pow2P && g.NT * ((g.P + 31) >> 5) <= (K1_THREADS / 64) * TPW && ldsp <= 160 * 1024 &&
+        g.ncu > 0 && !(g.dbg & 4096)) {   // RSP_ABLATE=4096: the non-persistent kernel
+        // one FFT size per instantiation keeps the prefetch registers + FFT under 256 VGPRs
+        const int grid = std::min(g.ncu, nf * g.ntiles);
+#define K1P_LAUNCH(LGP)                                                                                     \
+    do {                                                                                                    \
+        hipError_t e = allow_lds(k1p_dbf_mtd<BMAX, CP, LGP>, ldsp);                                         \
+        if (e != hipSuccess) return e;                                                                      \
+        hipLaunchKernelGGL((k1p_dbf_mtd<BMAX, CP, LGP>), dim3(grid), dim3(K1_THREADS), ldsp, s, g, k, fp, nf); \
+        return hipGetLastError();                                                                           \
+    } while (0)
+        switch (g.logP) {
+            case 6: K1P_LAUNCH(6);
+            case 7: K1P_LAUNCH(7);
+            case 8: K1P_LAUNCH(8);
+            default: break;
+        }
+#undef K1P_LAUNCH
+    }
     const size_t lds = ((size_t)g.B * g.NT * g.Ppad + g.P) * sizeof(float2);
     hipError_t e = allow_lds(k1_dbf_mtd<BMAX, CP>, lds);
     if (e != hipSuccess) return e;

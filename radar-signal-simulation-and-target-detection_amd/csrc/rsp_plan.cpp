@@ -638,6 +638,7 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     g.T = (float)cfar->T_CFAR;
     g.max_dets = 1 << 16;
     if (const char* ab = getenv("RSP_ABLATE")) g.dbg = atoi(ab);   // timing experiments only
+    if (hipDeviceGetAttribute(&g.ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) g.ncu = 0;
     auto bail = [&](int rc) { delete p; return rc; };
     if (g.refR < 1 || g.refV < 1 || g.guardR < 0 || g.guardV < 0) return bail(fail(RSP_ERR_INVALID, "bad CFAR window"));
 

@@ -39,6 +39,8 @@ def main():
                    if k.startswith('k')}
     res['_note'] = ('bytes per launch = 2*FETCH_SIZE + WRITE_SIZE (KiB*1024), median over launches of '
                     'tools/prof_stages.py ' + ' '.join(sys.argv[4:]))
+    if len(sys.argv) > 6:
+        res['_frames_per_launch'] = int(sys.argv[6])
     json.dump(res, open(out, 'w'), indent=1)
     print(json.dumps(res))
 
