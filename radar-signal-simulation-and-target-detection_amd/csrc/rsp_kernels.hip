@@ -581,10 +581,11 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
 // round by round.  Same arithmetic as k1_dbf_mtd (mode 3).
 template <int BMAX, int CP, int LGP>
 __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevConsts k, FramePtrs fp, int nf) {
-    extern __shared__ __attribute__((aligned(16))) float2 Y[];   // buf 0 | buf 1 ([B][NT][Ppad] each) | twiddles
+    extern __shared__ __attribute__((aligned(16))) float2 Y[];   // tile [B][NT][Ppad] (x2 if nbuf = 2) | twiddles
     const int B = g.B, C = g.C, P = g.P, NT = g.NT, Ppad = g.Ppad;
+    const int nbuf = (g.dbg & 8192) ? 1 : 2;   // RSP_ABLATE=8192: one buffer (measured slower: 20.7k vs 21.2k frames/s)
     const int bufsz = B * NT * Ppad;
-    float2* twl = Y + 2 * bufsz;
+    float2* twl = Y + nbuf * bufsz;
     const int total = nf * g.ntiles;
     int T = blockIdx.x;
     if (T >= total) return;
@@ -686,9 +687,9 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
         const StoreZ sz{buf_rsrc(z, (unsigned)B * g.ntiles * zslab * 8u), lgNT, g.ntiles, tile, P, half};
         fft_passes<LGP, 0, 0, 16, false, K1_SH, K1_THREADS>(Y + cur * bufsz, Ppad, B * NT, twl,
                                                            StoreLds{Y + cur * bufsz}, sz);   // ends with a barrier
-        if (Tn < total) dbf(Y + (cur ^ 1) * bufsz);
+        if (Tn < total) dbf(Y + (nbuf == 2 ? (cur ^ 1) : 0) * bufsz);
         __syncthreads();
-        cur ^= 1;
+        if (nbuf == 2) cur ^= 1;
     }
 }
 
@@ -1354,7 +1355,7 @@ template <int BMAX, int CP>
 static hipError_t launch_k1_t(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int mode,
                               hipStream_t s) {
     constexpr int NJ = CP / 4, MB = BMAX <= 8 ? 1 : 2, TPW = (16 / NJ) / MB > 0 ? (16 / NJ) / MB : 1;
-    const size_t ldsp = ((size_t)2 * g.B * g.NT * g.Ppad + g.P) * sizeof(float2);
+    const size_t ldsp = ((size_t)((g.dbg & 8192) ? 1 : 2) * g.B * g.NT * g.Ppad + g.P) * sizeof(float2);
     if (mode == 3 && g.pow2P && g.NT * ((g.P + 31) >> 5) <= (K1_THREADS / 64) * TPW && ldsp <= 160 * 1024 &&
         g.ncu > 0 && !(g.dbg & 4096)) {   // RSP_ABLATE=4096: the non-persistent kernel
         // one FFT size per instantiation keeps the prefetch registers + FFT under 256 VGPRs

@@ -183,6 +183,8 @@ struct rsp_plan {
     // RSP_QUEUE=pipe: every K1 runs on one K1 stream and each lane's K2/K3 wait for their K1, so
     // K1 of batch i+1 (HBM-bound) runs beside K2/K3 of batch i (VALU-bound)
     hipStream_t k1stream = nullptr;
+    // K1 + K2 run in sub-batches of this many frames inside a larger batch (RSP_K12_SUB; 0 = off)
+    int k12_sub = 0;
     // live stage timing of the queue (rsp_set_stage_timing): HIP events around K1/K2/K3 of
     // every batch, summed at harvest
     bool time_stages = false;
@@ -409,6 +411,21 @@ FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const float2* const* in, i
     return fp;
 }
 
+// Frames [off, off + n) of fp as a batch of their own.
+FramePtrs sub_ptrs(const FramePtrs& fp, int off, int n) {
+    FramePtrs s{};
+    s.trace = fp.trace;
+    for (int f = 0; f < n; ++f) {
+        s.in[f] = fp.in[off + f];
+        s.z[f] = fp.z[off + f];
+        s.rdm[f] = fp.rdm[off + f];
+        s.mag[f] = fp.mag[off + f];
+        s.dets[f] = fp.dets[off + f];
+        s.count[f] = fp.count[off + f];
+    }
+    return s;
+}
+
 // Enqueue K1 -> K2 -> K3 for nf frames on lane L, plus the async detection read-back.
 int launch_batch(rsp_plan* p, Lane& L, const float2* const* in, const int* ids, int nf, bool after_stream = false) {
     const FramePtrs fp = lane_ptrs(p, L, in, nf);
@@ -426,11 +443,21 @@ int launch_batch(rsp_plan* p, Lane& L, const float2* const* in, const int* ids, 
         HIPCHK(launch_k1(p->g, p->k, fp, nf, 3, p->g.C, p->k1stream));
         HIPCHK(hipEventRecord(L.k1done, p->k1stream));
         HIPCHK(hipStreamWaitEvent(L.ks, L.k1done, 0));
+    } else if (!L.timed && p->k12_sub > 0 && nf > p->k12_sub) {
+        // K1 + K2 in sub-batches (each sub-batch's z is still in the Infinity Cache when K2 reads
+        // it), then one K3 over the whole batch (fewer tail rounds)
+        for (int f0 = 0; f0 < nf; f0 += p->k12_sub) {
+            const int n = std::min(p->k12_sub, nf - f0);
+            const FramePtrs sp = sub_ptrs(fp, f0, n);
+            HIPCHK(launch_k1(p->g, p->k, sp, n, 3, p->g.C, L.ks));
+            HIPCHK(launch_k2(p->g, p->k, sp, n, p->g.B * p->g.P, L.ks));
+        }
     } else {
         HIPCHK(launch_k1(p->g, p->k, fp, nf, 3, p->g.C, L.ks));
     }
     if (L.timed) HIPCHK(hipEventRecord(L.tev[1], L.ks));
-    HIPCHK(launch_k2(p->g, p->k, fp, nf, p->g.B * p->g.P, L.ks));
+    if (L.timed || p->k1stream || p->k12_sub <= 0 || nf <= p->k12_sub)
+        HIPCHK(launch_k2(p->g, p->k, fp, nf, p->g.B * p->g.P, L.ks));
     if (L.timed) HIPCHK(hipEventRecord(L.tev[2], L.ks));
     HIPCHK(launch_k3(p->g, p->k, fp, nf, L.ks));
     if (L.timed) HIPCHK(hipEventRecord(L.tev[3], L.ks));
@@ -824,6 +851,7 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     {
         const char* nl = getenv("RSP_NLANES");
         if (nl) p->nlanes = std::max(1, std::min(RSP_LANES, atoi(nl)));
+        if (const char* ks = getenv("RSP_K12_SUB")) p->k12_sub = std::max(0, atoi(ks));
         const char* q = getenv("RSP_QUEUE");
         if (q && !strcmp(q, "serial") && hipStreamCreateWithFlags(&p->kstream, hipStreamNonBlocking) != hipSuccess)
             return bail(fail(RSP_ERR_DEVICE, "hipStreamCreateWithFlags failed"));
