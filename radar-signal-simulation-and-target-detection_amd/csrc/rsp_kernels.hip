@@ -634,8 +634,12 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
                 const int c = min(4 * j + grp, C - 1);
-                xv[u][j] = n >= 0 ? *reinterpret_cast<const float4*>(x + (size_t)c * NPc + (size_t)n * P + pv[u])
-                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+                {   // non-temporal: the cube is read exactly once (148 vs 154 us per 8-frame launch)
+                    const f32x4 t = n >= 0 ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(
+                                                 x + (size_t)c * NPc + (size_t)n * P + pv[u]))
+                                           : f32x4{0.f, 0.f, 0.f, 0.f};
+                    xv[u][j] = make_float4(t.x, t.y, t.z, t.w);
+                }
             }
         }
     };
