@@ -192,3 +192,50 @@ def test_profile_stages_reports_three_kernels():
     plan.close()
     assert [x['stage'] for x in st] == ['k1_dbf_mtd', 'k2_pc', 'k3_cfar']
     assert all(x['ms'] > 0 and x['bytes'] > 0 for x in st)
+
+
+def _plan_with_env(s, env, **kw):
+    import os
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return Plan(s['cfg'], s['cfar'], s['clus'], s['pre_p'], **kw)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize('name', ['small', 'x2'])
+def test_persistent_k1_bit_identical_to_tiled_k1(name):
+    """The persistent software-pipelined K1 (k1p_dbf_mtd, default) and the one-tile-per-workgroup
+    K1 (RSP_ABLATE=4096) do the same fp32 operations in the same order: identical RDM bits and
+    detections, on the synchronous path and through the 8-frame queue."""
+    s = scenario(name)
+    tg = targets_for(name)
+    cube = noisy_cube(s, tg)
+    outs, queued = [], []
+    for env in ({}, {'RSP_ABLATE': '4096'}, {'RSP_ABLATE': '8192'}):
+        plan = _plan_with_env(s, env, frames_per_launch=8)
+        outs.append(plan.process_cube(cube, frame_idx=1, want_rdm=True))
+        ptrs = [plan.device_alloc(plan.sizes.cube_elems * 8) for _ in range(3)]
+        try:
+            for f, p in enumerate(ptrs):
+                plan.synthesize_device(p, tg, frame_idx=f + 1)
+            for i in range(10):
+                plan.enqueue(ptrs[i % 3], i + 1)
+            plan.drain()
+            queued.append(plan.results())
+        finally:
+            for p in ptrs:
+                plan.device_free(p)
+            plan.close()
+    for o in outs[1:]:
+        assert np.array_equal(o['rdm'], outs[0]['rdm'])
+        assert o['detections'] == outs[0]['detections']
+        assert o['final_targets'] == outs[0]['final_targets']
+    for q in queued[1:]:
+        assert [r['frame_idx'] for r in q] == [r['frame_idx'] for r in queued[0]]
+        assert [r['final_targets'] for r in q] == [r['final_targets'] for r in queued[0]]
