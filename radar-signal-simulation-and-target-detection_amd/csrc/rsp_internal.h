@@ -6,6 +6,7 @@
 #define RSP_MAX_F 8          // frames batched per launch
 #define RSP_LANES 4          // max streams of the throughput queue (batches in flight)
 #define RSP_K2_POINTS 4096   // complex points per pulse-compression workgroup
+#define K2M_POINTS_HOST 2560 // the same for the mixed-radix (5 * 2^k) blocks (K2M_POINTS)
 #define RSP_THREADS 256
 
 // Philox4x32-10 (Salmon et al., SC'11) in place on counter c with key (k0, k1); the streams
@@ -44,6 +45,7 @@ struct SegDesc {
     int ntaps, delay, Ls, taps_off;
     // FFT overlap-save: y[g] = sum_{j<Lh} h[j] x~(seg_lo + g - j), block size M, V = M-Lh+1 valid
     int Lh, M, logM, V, nblocks, H_off, tw_off;
+    int mixM;        // 0: M = 2^logM (k2_fft_job); else M = 5 * 2^k (k2m_fft_job, radices 16/8 and 10)
     int nrad, rad[8];
     int rows_per_wg;
 };

@@ -128,6 +128,44 @@ template <bool INV> struct Dft<16, INV> {
     }
 };
 
+template <bool INV> struct Dft<5, INV> {   // X1 = m1 + rot(n1), X4 = m1 - rot(n1), X2 = m2 + rot(n2), X3 = m2 - rot(n2)
+    static __device__ __forceinline__ void run(f2* a) {
+        const float c1 = 0.30901699437494742f, c2 = -0.80901699437494742f;   // cos(2 pi / 5), cos(4 pi / 5)
+        const float s1 = 0.95105651629515357f, s2 = 0.58778525229247313f;    // sin(2 pi / 5), sin(4 pi / 5)
+        const f2 t1 = a[1] + a[4], t2 = a[2] + a[3], t3 = a[1] - a[4], t4 = a[2] - a[3];
+        const f2 m1 = a[0] + c1 * t1 + c2 * t2, m2 = a[0] + c2 * t1 + c1 * t2;
+        const f2 n1 = vrot<INV>(s1 * t3 + s2 * t4), n2 = vrot<INV>(s2 * t3 - s1 * t4);
+        a[0] = a[0] + t1 + t2;
+        a[1] = m1 + n1;
+        a[4] = m1 - n1;
+        a[2] = m2 + n2;
+        a[3] = m2 - n2;
+    }
+};
+template <bool INV> struct Dft<10, INV> {   // 2 x 5 (even / odd halves, W_10^k on the odd)
+    static __device__ __forceinline__ void run(f2* a) {
+        f2 e[5], o[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            e[k] = a[2 * k];
+            o[k] = a[2 * k + 1];
+        }
+        Dft<5, INV>::run(e);
+        Dft<5, INV>::run(o);
+        const float c1 = 0.80901699437494742f, s1 = 0.58778525229247313f;   // W_10^1
+        const float c2 = 0.30901699437494742f, s2 = 0.95105651629515357f;   // W_10^2
+        o[1] = vmul(o[1], vtw<INV>(c1, s1));
+        o[2] = vmul(o[2], vtw<INV>(c2, s2));
+        o[3] = vmul(o[3], vtw<INV>(-c2, s2));
+        o[4] = vmul(o[4], vtw<INV>(-c1, s1));
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            a[k] = e[k] + o[k];
+            a[k + 5] = e[k] - o[k];
+        }
+    }
+};
+
 constexpr int clog2(int x) { return x <= 1 ? 0 : 1 + clog2(x >> 1); }
 
 // LDS index inside a row: SH > 0 inserts one complex every 2^SH to break power-of-two
@@ -165,7 +203,7 @@ __device__ __forceinline__ void load_tw(const float2* twk, f2 (&w)[R]) {
             w[r] = f2{t.x, INV ? -t.y : t.y};
         }
     } else {
-        constexpr int lgR = clog2(R);
+        constexpr int lgR = clog2(R - 1) + 1;   // bases W^(k 2^i), 2^i < R (= log2 R for powers of two)
         f2 b[lgR];
 #pragma unroll
         for (int i = 0; i < lgR; ++i) {
@@ -179,7 +217,7 @@ __device__ __forceinline__ void load_tw(const float2* twk, f2 (&w)[R]) {
         }
     }
 }
-constexpr int tw_row(int R, bool cmp) { return cmp ? clog2(R) : R - 1; }
+constexpr int tw_row(int R, bool cmp) { return cmp ? clog2(R - 1) + 1 : R - 1; }
 
 // Radix plan of a 2^m-point FFT: radix-16 passes, remainder as 8/4 (m = 5 -> 8 x 4);
 // must match radix_plan() in rsp_plan.cpp.  REV = the same radices in reverse order (the
@@ -715,11 +753,144 @@ struct StoreRdm {   // last inverse pass: keep outputs i in [Lh-1, Lh-1+V) that 
     }
 };
 
+#ifndef K2_SH
 #define K2_SH 5   // one pad complex per 32 (tools/lds_conflicts.py)
+#endif
 #define K2_LDS_DATA (RSP_K2_POINTS + (RSP_K2_POINTS >> K2_SH))
 #define K2_LDS_TW 4096       // >= tw_total(log2 M) + tw_total(log2 M, reversed) for M <= 2048
 #define K2_LDS_TW_CMP 1408   // the same for compact tables
 #define K2_MAXM 2048
+
+// ---- mixed-radix overlap-save blocks (M = 5 * 2^k): three Stockham passes of radices
+// (RA, RB, RC) forward and (RC, RB, RA) inverse, RC = 10.  Butterfly counts M / R and partial
+// products Ns need not be powers of two, so every LDS index is padded per element.
+#define K2M_POINTS K2M_POINTS_HOST   // complex points per mixed-radix workgroup (10 per thread)
+
+template <int R, bool INV, int NB, int M, int NS>
+__device__ __forceinline__ void shm_load(const float2* buf, int rs, int nrows, const float2* tw, f2 (&v)[NB][R]) {
+    constexpr int nb = M / R;
+    const int total = nb * nrows;
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+        const int beta = threadIdx.x + t * RSP_THREADS;
+        if (beta < total) {
+            const int row = beta / nb, j = beta - row * nb;
+            const float2* rowp = buf + row * rs;
+            f2 w[R];
+            if (NS > 1) load_tw<R, INV, true>(tw + (j % NS) * tw_row(R, true), w);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                f2 x = tof2(rowp[lidx<K2_SH>(j + r * nb)]);
+                if (r > 0 && NS > 1) x = vmul(x, w[r]);
+                v[t][r] = x;
+            }
+        }
+    }
+}
+
+template <int R, bool INV, int NB, int M, int NS, class St>
+__device__ __forceinline__ void shm_store(f2 (&v)[NB][R], int rs, int nrows, const St& st) {
+    constexpr int nb = M / R;
+    const int total = nb * nrows;
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+        const int beta = threadIdx.x + t * RSP_THREADS;
+        if (beta < total) {
+            const int row = beta / nb, j = beta - row * nb;
+            Dft<R, INV>::run(v[t]);
+            const int idxD = (j / NS) * (NS * R) + j % NS;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int o = idxD + r * NS;
+                st.put(t * R + r, row, o, row * rs + lidx<K2_SH>(o), v[t][r]);
+            }
+        }
+    }
+}
+
+template <int R, bool INV, int NB, int M, int NS, class St>
+__device__ __forceinline__ void shm_pass(float2* buf, int rs, int nrows, const float2* tw, const St& st) {
+    f2 v[NB][R];
+    shm_load<R, INV, NB, M, NS>(buf, rs, nrows, tw, v);
+    __syncthreads();
+    shm_store<R, INV, NB, M, NS>(v, rs, nrows, st);
+    __syncthreads();
+}
+
+// Twiddle table sizes / offsets of the mixed plans (must match build_mixed_twiddles() in
+// rsp_plan.cpp): forward tables, then inverse; pass q >= 1 owns Ns_q rows of tw_row(R_q).
+constexpr int twm_fwd(int RA, int RB, int RC) { return RA * tw_row(RB, true) + RA * RB * tw_row(RC, true); }
+
+template <int M, int RA, int RB, int RC>
+__device__ __forceinline__ void k2m_fft_job(const Geometry& g, const DevConsts& k, const SegDesc& sd, const K2Job& job,
+                                            const float2* __restrict__ z, float2* __restrict__ rdm,
+                                            float* __restrict__ mag, int row0, int rows_total, float2* L,
+                                            const FramePtrs& fp) {
+    static_assert(RA * RB * RC == M, "mixed plan must factor M");
+    constexpr int rows = K2M_POINTS / M;
+    constexpr int PTS = K2M_POINTS / RSP_THREADS;
+    constexpr int rs = M + (M >> K2_SH);
+    constexpr int NBA = (PTS + RA - 1) / RA, NBB = (PTS + RB - 1) / RB, NBC = (PTS + RC - 1) / RC;
+    constexpr int nb0 = M / RA;
+    const int P = g.P, G = g.G;
+    const int lo = sd.lo, hi = sd.hi, off = sd.off;
+    const int tid = threadIdx.x;
+    const int Lh1 = sd.Lh - 1;
+    const int g0 = sd.ga + job.blk * sd.V;
+    const int a = sd.seg_lo + g0 - Lh1;   // sample index of u[0]
+    const float2* twf = k.twM + sd.tw_off;
+    const float2* twi = twf + twm_fwd(RA, RB, RC);
+    const __amdgpu_buffer_rsrc_t zr = buf_rsrc(z, (unsigned)g.B * g.ntiles * P * g.NT * 8u);
+    // forward pass 0 (Ns = 1) straight from z
+    f2 v0[NBA][RA];
+#pragma unroll
+    for (int t = 0; t < NBA; ++t) {
+        const int beta = tid + t * RSP_THREADS;
+        const int rl = beta / nb0, j = beta - rl * nb0;
+        const int rho = row0 + rl;
+        const int b = rho / P, v = rho - b * P;
+        const bool live = beta < rows * nb0 && rho < rows_total;
+#pragma unroll
+        for (int r = 0; r < RA; ++r) {
+            const int n = a + j + r * nb0;
+            const bool ok = live && n >= lo && n <= hi;
+            v0[t][r] = buf_ld_f2(zr, ok ? (unsigned)zaddr(g, b, v, n - lo + off) * 8u : RSP_OOB);
+        }
+    }
+    // H for the last forward pass's outputs j + r M / RC (1/M folded in)
+    f2 hreg[NBC][RC];
+#pragma unroll
+    for (int t = 0; t < NBC; ++t) {
+        const int j = (tid + t * RSP_THREADS) % (M / RC);
+#pragma unroll
+        for (int r = 0; r < RC; ++r) hreg[t][r] = tof2(k.H[sd.H_off + j + r * (M / RC)]);
+    }
+    shm_store<RA, false, NBA, M, 1>(v0, rs, rows, StoreLds{L});
+    __syncthreads();
+    trace_stamp(fp, 1);
+    shm_pass<RB, false, NBB, M, RA>(L, rs, rows, twf, StoreLds{L});
+    {   // fused: forward last pass, x H, inverse pass 0 (same butterflies)
+        f2 v[NBC][RC];
+        shm_load<RC, false, NBC, M, RA * RB>(L, rs, rows, twf + RA * tw_row(RB, true), v);
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < NBC; ++t) {
+            Dft<RC, false>::run(v[t]);
+#pragma unroll
+            for (int r = 0; r < RC; ++r) v[t][r] = vmul(v[t][r], hreg[t][r]);
+        }
+        shm_store<RC, true, NBC, M, 1>(v, rs, rows, StoreLds{L});
+        __syncthreads();
+    }
+    trace_stamp(fp, 2);
+    shm_pass<RB, true, NBB, M, RC>(L, rs, rows, twi, StoreLds{L});
+    const int gend = min(sd.gb, g0 + sd.V);
+    shm_pass<RA, true, NBA, M, RC * RB>(
+        L, rs, rows, twi + RC * tw_row(RB, true),
+        StoreRdm{buf_rsrc(rdm, (unsigned)rows_total * G * 8u), buf_rsrc(mag, (unsigned)rows_total * g.Gp * 4u), G, g.Gp,
+                 row0, rows_total, Lh1, g0, gend});
+    trace_stamp(fp, 3);
+}
 
 // One overlap-save block of one FFT segment for RSP_K2_POINTS / 2^LGM adjacent rows.
 // LDS round trips: forward pass 0 runs on the samples as loaded from z; the forward FFT's
@@ -857,7 +1028,13 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k,
     const int lo = sd.lo, hi = sd.hi, off = sd.off;
     const int tid = threadIdx.x;
 
-    if (sd.type == 1) {
+    if (sd.type == 1 && sd.mixM) {
+        switch (sd.mixM) {
+            case 640: k2m_fft_job<640, 8, 8, 10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
+            case 1280: k2m_fft_job<1280, 16, 8, 10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
+            default: k2m_fft_job<2560, 16, 16, 10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
+        }
+    } else if (sd.type == 1) {
 #ifdef K2_ONLY_LGM   // ISA inspection builds: one block size only
         k2_fft_job<K2_ONLY_LGM, TWG, CMP>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp);
         if (sd.logM >= 0) return;

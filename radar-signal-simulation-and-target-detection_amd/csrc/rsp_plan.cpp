@@ -122,6 +122,32 @@ void build_pass_twiddles(int m, std::vector<float2>& out, bool rev = false, bool
     }
 }
 
+// Mixed-radix plans (k2m_fft_job): M -> forward radices (RA, RB, RC); inverse reversed.
+bool mixed_plan(int M, int* ra, int* rb, int* rc) {
+    switch (M) {
+        case 640: *ra = 8; *rb = 8; *rc = 10; return true;
+        case 1280: *ra = 16; *rb = 8; *rc = 10; return true;
+        case 2560: *ra = 16; *rb = 16; *rc = 10; return true;
+        default: return false;
+    }
+}
+
+// Compact twiddle tables of a mixed plan (must match twm_fwd() / k2m_fft_job in
+// rsp_kernels.hip): forward pass 1 (Ns = RA, R = RB), pass 2 (Ns = RA RB, R = RC), then inverse
+// pass 1 (Ns = RC, R = RB), pass 2 (Ns = RC RB, R = RA); row k holds W_{Ns R}^(k 2^i), 2^i < R.
+void build_mixed_twiddles(int M, std::vector<float2>& out) {
+    int ra, rb, rc;
+    mixed_plan(M, &ra, &rb, &rc);
+    const int ns[4] = {ra, ra * rb, rc, rc * rb}, rr[4] = {rb, rc, rb, ra};
+    for (int q = 0; q < 4; ++q)
+        for (int k = 0; k < ns[q]; ++k)
+            for (int r = 1; r < rr[q]; r *= 2) {
+                const long long e = ((long long)k * r) % ((long long)ns[q] * rr[q]);
+                const double a = -2.0 * M_PI * (double)e / ((double)ns[q] * rr[q]);
+                out.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
+            }
+}
+
 double mround(double x) { return x < 0 ? -std::floor(-x + 0.5) : std::floor(x + 0.5); }
 
 struct Lane {
@@ -349,22 +375,50 @@ int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga,
     const int nout = gb - ga;
     double best = 1e300;
     int bestM = 0;
-    for (int M = 64; M <= 2048; M *= 2) {
+    // candidates: 2^k (k2_fft_job) and, opt-in with RSP_K2_MIXED=1 (compact twiddles), 5 * 2^k
+    // (k2m_fft_job; 640 / 1280 / 2560, e.g. the x2 long segment: one 2560 block instead of two
+    // 2048 blocks, 37% fewer points).  Off by default: with 256 threads per workgroup the radix-16
+    // passes of a 2560 row keep 160 threads busy and the workgroup takes 12.5 us against 11.5 us
+    // for the 2 x 2048 rows it replaces (measured).  Cost model:
+    // blocks * M * (log2 M + 2).
+    const char* mx = getenv("RSP_K2_MIXED");
+    const bool allow_mixed = cmp && mx && atoi(mx) == 1;
+    const int cand[] = {64, 128, 256, 512, 640, 1024, 1280, 2048, 2560};
+    for (int M : cand) {
+        int ra, rb, rc;
+        const bool mixed = mixed_plan(M, &ra, &rb, &rc);
+        if (mixed && !allow_mixed) continue;
         const int V = M - Lh + 1;
         if (V < 1) continue;
         const int nb = (nout + V - 1) / V;
-        const double cost = (double)nb * M * (ilog2i(M) + 2);
+        const double cost = (double)nb * M * (std::log2((double)M) + 2);
         if (cost < best * 0.999) { best = cost; bestM = M; }
     }
-    if (!bestM) return fail(RSP_ERR_UNSUPPORTED, "%s filter length %d exceeds the 2048-point block", name, Lh);
+    if (!bestM) return fail(RSP_ERR_UNSUPPORTED, "%s filter length %d exceeds the 2560-point block", name, Lh);
     const int M = bestM;
-    s.M = M; s.logM = ilog2i(M); s.V = M - Lh + 1; s.nblocks = (nout + s.V - 1) / s.V;
-    s.rows_per_wg = RSP_K2_POINTS / M;
-    radix_plan(s.logM, &s.nrad, s.rad);
+    int ra, rb, rc;
+    const bool mixed = mixed_plan(M, &ra, &rb, &rc);
+    s.M = M; s.mixM = mixed ? M : 0; s.logM = mixed ? 0 : ilog2i(M); s.V = M - Lh + 1;
+    s.nblocks = (nout + s.V - 1) / s.V;
+    s.rows_per_wg = mixed ? K2M_POINTS_HOST / M : RSP_K2_POINTS / M;
+    if (!mixed) radix_plan(s.logM, &s.nrad, s.rad);
     // spectrum of h zero-padded to M, natural order, 1/M folded in
     std::vector<cd> hm(M, 0.0);
     for (int i = 0; i < Lh; ++i) hm[i] = h[i];
-    fft_d(hm, -1);
+    if (mixed) {   // direct DFT (M not a power of two; Lh taps, once per plan)
+        std::vector<cd> out(M, 0.0);
+        for (int f = 0; f < M; ++f) {
+            cd acc = 0.0;
+            for (int i = 0; i < Lh; ++i) {
+                const long long e = ((long long)f * i) % M;
+                acc += hm[i] * std::polar(1.0, -2.0 * M_PI * (double)e / M);
+            }
+            out[f] = acc;
+        }
+        hm = out;
+    } else {
+        fft_d(hm, -1);
+    }
     s.H_off = (int)H.size();
     for (auto& v : hm) { v /= (double)M; H.push_back(make_float2((float)v.real(), (float)v.imag())); }
     int ti = -1;
@@ -372,8 +426,12 @@ int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga,
     if (ti < 0) {
         tw_sizes.push_back(M);
         tw_offs.push_back((int)twM.size());
-        build_pass_twiddles(s.logM, twM, false, cmp);   // forward FFT
-        build_pass_twiddles(s.logM, twM, true, cmp);    // inverse FFT (reversed radices)
+        if (mixed) {
+            build_mixed_twiddles(M, twM);
+        } else {
+            build_pass_twiddles(s.logM, twM, false, cmp);   // forward FFT
+            build_pass_twiddles(s.logM, twM, true, cmp);    // inverse FFT (reversed radices)
+        }
         ti = (int)tw_sizes.size() - 1;
     }
     s.tw_off = tw_offs[ti];
@@ -781,6 +839,10 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     for (int q = 0; q < g.nseg; ++q) g.segs[q] = p->segs[q];
     for (int q = 0; q < g.njobs; ++q) g.jobs[q] = p->jobs[q];
     g.nwg_k2 = wg;
+    if (getenv("RSP_PLAN_DEBUG"))
+        for (const SegDesc& s : p->segs)
+            fprintf(stderr, "rsp plan: segment type %d gates [%d,%d) lo %d hi %d Lh %d M %d (mixed %d) V %d blocks %d rows/wg %d\n",
+                    s.type, s.ga, s.gb, s.lo, s.hi, s.Lh, s.M, s.mixM, s.V, s.nblocks, s.rows_per_wg);
     // K3 tile
     g.cfar_hR = (std::max(g.refR + g.guardR, 2) + 3) & ~3;   // halo, multiple of 4 (float4 tile loads)
     g.cfar_RT = 64;
