@@ -68,6 +68,7 @@ struct Geometry {
     int twPp_elems;  // per-pass twiddles of the P-point FFT
     int pow2P, logP, nradP, radP[8];
     int nseg, njobs, nwg_k2;
+    int nwg_k2_pow2, mix_job0;   // k2_pc covers workgroups [0, nwg_k2_pow2); k2m_pc jobs [mix_job0, njobs)
     int cfar_RT, cfar_hR, cfar_W;
     int refR, guardR, refV, guardV;
     float T;

@@ -766,13 +766,13 @@ struct StoreRdm {   // last inverse pass: keep outputs i in [Lh-1, Lh-1+V) that 
 // products Ns need not be powers of two, so every LDS index is padded per element.
 #define K2M_POINTS K2M_POINTS_HOST   // complex points per mixed-radix workgroup (10 per thread)
 
-template <int R, bool INV, int NB, int M, int NS>
+template <int R, bool INV, int NB, int M, int NS, int NTHR>
 __device__ __forceinline__ void shm_load(const float2* buf, int rs, int nrows, const float2* tw, f2 (&v)[NB][R]) {
     constexpr int nb = M / R;
     const int total = nb * nrows;
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
-        const int beta = threadIdx.x + t * RSP_THREADS;
+        const int beta = threadIdx.x + t * NTHR;
         if (beta < total) {
             const int row = beta / nb, j = beta - row * nb;
             const float2* rowp = buf + row * rs;
@@ -788,13 +788,13 @@ __device__ __forceinline__ void shm_load(const float2* buf, int rs, int nrows, c
     }
 }
 
-template <int R, bool INV, int NB, int M, int NS, class St>
+template <int R, bool INV, int NB, int M, int NS, int NTHR, class St>
 __device__ __forceinline__ void shm_store(f2 (&v)[NB][R], int rs, int nrows, const St& st) {
     constexpr int nb = M / R;
     const int total = nb * nrows;
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
-        const int beta = threadIdx.x + t * RSP_THREADS;
+        const int beta = threadIdx.x + t * NTHR;
         if (beta < total) {
             const int row = beta / nb, j = beta - row * nb;
             Dft<R, INV>::run(v[t]);
@@ -808,12 +808,12 @@ __device__ __forceinline__ void shm_store(f2 (&v)[NB][R], int rs, int nrows, con
     }
 }
 
-template <int R, bool INV, int NB, int M, int NS, class St>
+template <int R, bool INV, int NB, int M, int NS, int NTHR, class St>
 __device__ __forceinline__ void shm_pass(float2* buf, int rs, int nrows, const float2* tw, const St& st) {
     f2 v[NB][R];
-    shm_load<R, INV, NB, M, NS>(buf, rs, nrows, tw, v);
+    shm_load<R, INV, NB, M, NS, NTHR>(buf, rs, nrows, tw, v);
     __syncthreads();
-    shm_store<R, INV, NB, M, NS>(v, rs, nrows, st);
+    shm_store<R, INV, NB, M, NS, NTHR>(v, rs, nrows, st);
     __syncthreads();
 }
 
@@ -821,14 +821,14 @@ __device__ __forceinline__ void shm_pass(float2* buf, int rs, int nrows, const f
 // rsp_plan.cpp): forward tables, then inverse; pass q >= 1 owns Ns_q rows of tw_row(R_q).
 constexpr int twm_fwd(int RA, int RB, int RC) { return RA * tw_row(RB, true) + RA * RB * tw_row(RC, true); }
 
-template <int M, int RA, int RB, int RC>
+template <int M, int RA, int RB, int RC, int NTHR, int PTSW>
 __device__ __forceinline__ void k2m_fft_job(const Geometry& g, const DevConsts& k, const SegDesc& sd, const K2Job& job,
                                             const float2* __restrict__ z, float2* __restrict__ rdm,
                                             float* __restrict__ mag, int row0, int rows_total, float2* L,
                                             const FramePtrs& fp) {
     static_assert(RA * RB * RC == M, "mixed plan must factor M");
-    constexpr int rows = K2M_POINTS / M;
-    constexpr int PTS = K2M_POINTS / RSP_THREADS;
+    constexpr int rows = PTSW / M;
+    constexpr int PTS = PTSW / NTHR;
     constexpr int rs = M + (M >> K2_SH);
     constexpr int NBA = (PTS + RA - 1) / RA, NBB = (PTS + RB - 1) / RB, NBC = (PTS + RC - 1) / RC;
     constexpr int nb0 = M / RA;
@@ -845,7 +845,7 @@ __device__ __forceinline__ void k2m_fft_job(const Geometry& g, const DevConsts& 
     f2 v0[NBA][RA];
 #pragma unroll
     for (int t = 0; t < NBA; ++t) {
-        const int beta = tid + t * RSP_THREADS;
+        const int beta = tid + t * NTHR;
         const int rl = beta / nb0, j = beta - rl * nb0;
         const int rho = row0 + rl;
         const int b = rho / P, v = rho - b * P;
@@ -861,17 +861,17 @@ __device__ __forceinline__ void k2m_fft_job(const Geometry& g, const DevConsts& 
     f2 hreg[NBC][RC];
 #pragma unroll
     for (int t = 0; t < NBC; ++t) {
-        const int j = (tid + t * RSP_THREADS) % (M / RC);
+        const int j = (tid + t * NTHR) % (M / RC);
 #pragma unroll
         for (int r = 0; r < RC; ++r) hreg[t][r] = tof2(k.H[sd.H_off + j + r * (M / RC)]);
     }
-    shm_store<RA, false, NBA, M, 1>(v0, rs, rows, StoreLds{L});
+    shm_store<RA, false, NBA, M, 1, NTHR>(v0, rs, rows, StoreLds{L});
     __syncthreads();
     trace_stamp(fp, 1);
-    shm_pass<RB, false, NBB, M, RA>(L, rs, rows, twf, StoreLds{L});
+    shm_pass<RB, false, NBB, M, RA, NTHR>(L, rs, rows, twf, StoreLds{L});
     {   // fused: forward last pass, x H, inverse pass 0 (same butterflies)
         f2 v[NBC][RC];
-        shm_load<RC, false, NBC, M, RA * RB>(L, rs, rows, twf + RA * tw_row(RB, true), v);
+        shm_load<RC, false, NBC, M, RA * RB, NTHR>(L, rs, rows, twf + RA * tw_row(RB, true), v);
         __syncthreads();
 #pragma unroll
         for (int t = 0; t < NBC; ++t) {
@@ -879,17 +879,35 @@ __device__ __forceinline__ void k2m_fft_job(const Geometry& g, const DevConsts& 
 #pragma unroll
             for (int r = 0; r < RC; ++r) v[t][r] = vmul(v[t][r], hreg[t][r]);
         }
-        shm_store<RC, true, NBC, M, 1>(v, rs, rows, StoreLds{L});
+        shm_store<RC, true, NBC, M, 1, NTHR>(v, rs, rows, StoreLds{L});
         __syncthreads();
     }
     trace_stamp(fp, 2);
-    shm_pass<RB, true, NBB, M, RC>(L, rs, rows, twi, StoreLds{L});
+    shm_pass<RB, true, NBB, M, RC, NTHR>(L, rs, rows, twi, StoreLds{L});
     const int gend = min(sd.gb, g0 + sd.V);
-    shm_pass<RA, true, NBA, M, RC * RB>(
+    shm_pass<RA, true, NBA, M, RC * RB, NTHR>(
         L, rs, rows, twi + RC * tw_row(RB, true),
         StoreRdm{buf_rsrc(rdm, (unsigned)rows_total * G * 8u), buf_rsrc(mag, (unsigned)rows_total * g.Gp * 4u), G, g.Gp,
                  row0, rows_total, Lh1, g0, gend});
     trace_stamp(fp, 3);
+}
+
+// Mixed-radix jobs as a launch of their own (jobs [g.mix_job0, njobs), workgroups from
+// g.nwg_k2_pow2): 2 rows x 2560 points over 320 threads, so every radix-16 pass keeps all
+// threads busy (16 points each) and the radix-10 passes 80 % of them.
+#define K2M_THREADS 320
+template <int M, int RA, int RB, int RC>
+__global__ __launch_bounds__(K2M_THREADS, 3) void k2m_pc(Geometry g, DevConsts k, FramePtrs fp, int rows_total) {
+    extern __shared__ __attribute__((aligned(16))) float2 L[];
+    const int f = blockIdx.y;
+    const int wg = g.nwg_k2_pow2 + blockIdx.x;
+    int ji = g.mix_job0;
+    while (ji + 1 < g.njobs && wg >= g.jobs[ji + 1].wg_begin) ++ji;
+    const K2Job job = g.jobs[ji];
+    const SegDesc& sd = g.segs[job.seg];
+    const int row0 = (wg - job.wg_begin) * sd.rows_per_wg;
+    trace_stamp(fp, 0);
+    k2m_fft_job<M, RA, RB, RC, K2M_THREADS, 2 * M>(g, k, sd, job, fp.z[f], fp.rdm[f], fp.mag[f], row0, rows_total, L, fp);
 }
 
 // One overlap-save block of one FFT segment for RSP_K2_POINTS / 2^LGM adjacent rows.
@@ -1030,9 +1048,9 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k,
 
     if (sd.type == 1 && sd.mixM) {
         switch (sd.mixM) {
-            case 640: k2m_fft_job<640, 8, 8, 10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
-            case 1280: k2m_fft_job<1280, 16, 8, 10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
-            default: k2m_fft_job<2560, 16, 16, 10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
+            case 640: k2m_fft_job<640, 8, 8, 10, RSP_THREADS, K2M_POINTS>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
+            case 1280: k2m_fft_job<1280, 16, 8, 10, RSP_THREADS, K2M_POINTS>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
+            default: k2m_fft_job<2560, 16, 16, 10, RSP_THREADS, K2M_POINTS>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
         }
     } else if (sd.type == 1) {
 #ifdef K2_ONLY_LGM   // ISA inspection builds: one block size only
@@ -1593,7 +1611,8 @@ hipError_t launch_k2(const Geometry& g, const DevConsts& k, const FramePtrs& fp,
 #define K2_LAUNCH(TWG, CMP, LDS)                                                                     \
     do {                                                                                             \
         if ((e = allow_lds(k2_pc<TWG, CMP>, LDS)) != hipSuccess) return e;                           \
-        hipLaunchKernelGGL((k2_pc<TWG, CMP>), dim3(g.nwg_k2, nf), dim3(RSP_THREADS), LDS, s, g, k, fp, rows); \
+        if (g.nwg_k2_pow2 > 0)                                                                       \
+            hipLaunchKernelGGL((k2_pc<TWG, CMP>), dim3(g.nwg_k2_pow2, nf), dim3(RSP_THREADS), LDS, s, g, k, fp, rows); \
     } while (0)
     switch (g.dbg & (64 | 256)) {
         case 0: K2_LAUNCH(true, true, lds_g); break;
@@ -1602,6 +1621,22 @@ hipError_t launch_k2(const Geometry& g, const DevConsts& k, const FramePtrs& fp,
         default: K2_LAUNCH(false, false, lds_l); break;
     }
 #undef K2_LAUNCH
+    if (g.nwg_k2 > g.nwg_k2_pow2) {   // mixed-radix jobs (RSP_K2_MIXED=2): their own 320-thread launch
+        const SegDesc& sd = g.segs[g.jobs[g.mix_job0].seg];
+        const size_t lds = (size_t)2 * (sd.mixM + (sd.mixM >> K2_SH)) * sizeof(float2);
+        const dim3 grid(g.nwg_k2 - g.nwg_k2_pow2, nf);
+#define K2M_LAUNCH(M, RA, RB, RC)                                                                    \
+    do {                                                                                             \
+        if ((e = allow_lds(k2m_pc<M, RA, RB, RC>, lds)) != hipSuccess) return e;                     \
+        hipLaunchKernelGGL((k2m_pc<M, RA, RB, RC>), grid, dim3(K2M_THREADS), lds, s, g, k, fp, rows); \
+    } while (0)
+        switch (sd.mixM) {
+            case 640: K2M_LAUNCH(640, 8, 8, 10); break;
+            case 1280: K2M_LAUNCH(1280, 16, 8, 10); break;
+            default: K2M_LAUNCH(2560, 16, 16, 10); break;
+        }
+#undef K2M_LAUNCH
+    }
     return hipGetLastError();
 }
 

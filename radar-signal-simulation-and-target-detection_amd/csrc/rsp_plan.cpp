@@ -122,6 +122,13 @@ void build_pass_twiddles(int m, std::vector<float2>& out, bool rev = false, bool
     }
 }
 
+// RSP_K2_MIXED: 0 (default) power-of-two blocks only; 1 = 5 * 2^k blocks inside k2_pc (256
+// threads, one 2560 row); 2 = those jobs in their own k2m_pc launch (320 threads, two rows).
+int k2_mixed_mode() {
+    const char* mx = getenv("RSP_K2_MIXED");
+    return mx ? std::max(0, std::min(2, atoi(mx))) : 0;
+}
+
 // Mixed-radix plans (k2m_fft_job): M -> forward radices (RA, RB, RC); inverse reversed.
 bool mixed_plan(int M, int* ra, int* rb, int* rc) {
     switch (M) {
@@ -381,8 +388,8 @@ int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga,
     // passes of a 2560 row keep 160 threads busy and the workgroup takes 12.5 us against 11.5 us
     // for the 2 x 2048 rows it replaces (measured).  Cost model:
     // blocks * M * (log2 M + 2).
-    const char* mx = getenv("RSP_K2_MIXED");
-    const bool allow_mixed = cmp && mx && atoi(mx) == 1;
+    const int mixed_mode = k2_mixed_mode();   // 0 off, 1 inside k2_pc, 2 own 320-thread launch
+    const bool allow_mixed = cmp && mixed_mode > 0;
     const int cand[] = {64, 128, 256, 512, 640, 1024, 1280, 2048, 2560};
     for (int M : cand) {
         int ra, rb, rc;
@@ -400,7 +407,7 @@ int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga,
     const bool mixed = mixed_plan(M, &ra, &rb, &rc);
     s.M = M; s.mixM = mixed ? M : 0; s.logM = mixed ? 0 : ilog2i(M); s.V = M - Lh + 1;
     s.nblocks = (nout + s.V - 1) / s.V;
-    s.rows_per_wg = mixed ? K2M_POINTS_HOST / M : RSP_K2_POINTS / M;
+    s.rows_per_wg = mixed ? (mixed_mode == 2 ? 2 : K2M_POINTS_HOST / M) : RSP_K2_POINTS / M;
     if (!mixed) radix_plan(s.logM, &s.nrad, s.rad);
     // spectrum of h zero-padded to M, natural order, 1/M folded in
     std::vector<cd> hm(M, 0.0);
@@ -823,13 +830,21 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     // K2 jobs
     const int rows_total = B * P;
     int wg = 0;
-    for (size_t si = 0; si < p->segs.size(); ++si) {
-        const SegDesc& s = p->segs[si];
-        const int nwg = (rows_total + s.rows_per_wg - 1) / s.rows_per_wg;
-        const int nbl = (s.type == 1) ? s.nblocks : 1;
-        for (int blk = 0; blk < nbl; ++blk) {
-            p->jobs.push_back(K2Job{(int)si, blk, wg, nwg});
-            wg += nwg;
+    const bool own_launch = k2_mixed_mode() == 2;
+    for (int pass = 0; pass < 2; ++pass) {   // k2m_pc's jobs (mixed, own launch) last
+        if (pass == 1) {
+            g.nwg_k2_pow2 = wg;
+            g.mix_job0 = (int)p->jobs.size();
+        }
+        for (size_t si = 0; si < p->segs.size(); ++si) {
+            const SegDesc& s = p->segs[si];
+            if ((own_launch && s.mixM) != (pass == 1)) continue;
+            const int nwg = (rows_total + s.rows_per_wg - 1) / s.rows_per_wg;
+            const int nbl = (s.type == 1) ? s.nblocks : 1;
+            for (int blk = 0; blk < nbl; ++blk) {
+                p->jobs.push_back(K2Job{(int)si, blk, wg, nwg});
+                wg += nwg;
+            }
         }
     }
     g.nseg = (int)p->segs.size();

@@ -241,15 +241,17 @@ def test_persistent_k1_bit_identical_to_tiled_k1(name):
         assert [r['final_targets'] for r in q] == [r['final_targets'] for r in queued[0]]
 
 
+@pytest.mark.parametrize('mode', ['1', '2'])
 @pytest.mark.parametrize('name', ['small', 'x2'])
-def test_mixed_radix_overlap_save_parity(name):
-    """Opt-in 5 * 2^k overlap-save blocks (RSP_K2_MIXED=1: radix-10 + radix-16/8 Stockham passes)
-    against the oracle, same tolerances as the power-of-two path."""
+def test_mixed_radix_overlap_save_parity(name, mode):
+    """Opt-in 5 * 2^k overlap-save blocks (radix-10 + radix-16/8 Stockham passes; RSP_K2_MIXED=1
+    inside k2_pc, =2 as their own 320-thread k2m_pc launch) against the oracle, same tolerances
+    as the power-of-two path."""
     s = scenario(name)
     tg = targets_for(name)
     cube = noisy_cube(s, tg)
     _, st = chain.process_cube(cube.astype(np.complex128), s['cfg'], s['cfar'], s['clus'], s['pre_o'], keep=True)
-    plan = _plan_with_env(s, {'RSP_K2_MIXED': '1'})
+    plan = _plan_with_env(s, {'RSP_K2_MIXED': mode})
     try:
         gpu = plan.process_cube(cube, frame_idx=1, want_rdm=True, want_cfar=True)
     finally:
