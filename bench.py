@@ -275,7 +275,8 @@ def main():
         if os.path.exists(tf):
             with open(tf) as f:
                 tj = json.load(f)
-            tr = tj.get(dom['stage'])
+            # PMC files are keyed by kernel name: stage k1_dbf_mtd runs as k1p_dbf_mtd (persistent K1)
+            tr = tj.get(dom['stage'], tj.get({'k1_dbf_mtd': 'k1p_dbf_mtd'}.get(dom['stage'], '')))
             if tr is not None:   # scaled from the PMC passes' frames per launch to this run's
                 traffic = tr * dom['frames_per_launch'] / float(tj.get('_frames_per_launch', 4))
                 dom['pmc_traffic_bytes'] = traffic
