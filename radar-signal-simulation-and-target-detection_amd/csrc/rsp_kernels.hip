@@ -360,6 +360,20 @@ __device__ __forceinline__ void trace_stamp(const FramePtrs& fp, int i) {
     }
 }
 
+// Compacted used-sample index n' -> fast-time sample (Geometry::ivl_*).  Constant indices
+// only: a per-lane index into the kernel-argument arrays would become a vector load, and its
+// s_waitcnt vmcnt(0) would wait for every earlier vector memory op (e.g. pending z stores).
+__device__ __forceinline__ int used_sample(const Geometry& g, int np) {
+    int lo_q = g.ivl_lo[0], st_q = g.ivl_start[0];
+#pragma unroll
+    for (int i = 1; i < RSP_MAX_IVL; ++i)
+        if (i < g.nivl && np >= g.ivl_start[i]) {
+            lo_q = g.ivl_lo[i];
+            st_q = g.ivl_start[i];
+        }
+    return lo_q + np - st_q;
+}
+
 // z (compacted Doppler-domain rows) addressing: row (b, v), compacted sample n'.
 __device__ __forceinline__ size_t zaddr(const Geometry& g, int b, int v, int np) {
     const int lgNT = ilog2(g.NT);
@@ -459,11 +473,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
                 const int np = tile * NT + nl;
                 int n = -1;
                 if (t < ntp && np < g.nU && p < P) {
-                    int q = 0;
-#pragma unroll
-                    for (int i = 1; i < RSP_MAX_IVL; ++i)
-                        if (i < g.nivl && np >= g.ivl_start[i]) q = i;
-                    n = g.ivl_lo[q] + np - g.ivl_start[q];
+                    n = used_sample(g, np);
                 }
                 nlv[u] = t < ntp ? nl : -1;
                 pv[u] = p;
@@ -542,11 +552,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
             const int np = tile * NT + nl;
             int n = -1;
             if (np < g.nU) {
-                int q = 0;
-#pragma unroll
-                for (int i = 1; i < RSP_MAX_IVL; ++i)
-                    if (i < g.nivl && np >= g.ivl_start[i]) q = i;
-                n = g.ivl_lo[q] + np - g.ivl_start[q];
+                n = used_sample(g, np);
             }
             const int ip = sh ? p + (p >> K1_SH) : p;
 #pragma unroll
@@ -656,18 +662,16 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
     const size_t NPc = (size_t)g.cpitch;
     float4 xv[TPW][NJ];
     auto issue = [&](int TT) {   // cube loads of tile TT (fsf:93 operands) into xv
-        const int f = TT / g.ntiles, tile = TT - f * g.ntiles;
+        // f is wave-uniform: readfirstlane keeps fp.in[f] a scalar (kernarg) load.  As a vector
+        // load its s_waitcnt vmcnt(0) would also wait for the previous tile's z stores.
+        const int f = __builtin_amdgcn_readfirstlane(TT / g.ntiles), tile = TT - f * g.ntiles;
         const float2* __restrict__ x = fp.in[f];
 #pragma unroll
         for (int u = 0; u < TPW; ++u) {
             const int np = tile * NT + nlv[u];
             int n = -1;
             if (nlv[u] >= 0 && np < g.nU) {
-                int q = 0;
-#pragma unroll
-                for (int i = 1; i < RSP_MAX_IVL; ++i)
-                    if (i < g.nivl && np >= g.ivl_start[i]) q = i;
-                n = g.ivl_lo[q] + np - g.ivl_start[q];
+                n = used_sample(g, np);
             }
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
@@ -716,22 +720,42 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
         }
     };
     const int zslab = P * NT, lgNT = ilog2(NT), half = P >> 1;
+    // diagnostic (RSP_TRACE_FILE): stamp 0 = start, 1 / 2 = summed FFT+store / DBF phase ticks
+    // (not timestamps), 3 = end; thread 0, after the barriers that close each phase
+    const bool tr = fp.trace != nullptr && threadIdx.x == 0;
+    unsigned long long t0 = tr ? __builtin_amdgcn_s_memrealtime() : 0, tfft = 0, tdbf = 0, tiss = 0;
     issue(T);
     dbf(Y);
     __syncthreads();
+    const unsigned long long tpro = tr ? __builtin_amdgcn_s_memrealtime() : 0;
     int cur = 0;
     for (; T < total; T += gridDim.x) {
         const int Tn = T + gridDim.x;
+        const unsigned long long ti = tr ? __builtin_amdgcn_s_memrealtime() : 0;
         if (Tn < total) issue(Tn);   // next tile's loads fly during this tile's FFT + z stores
-        const int f = T / g.ntiles, tile = T - f * g.ntiles;
+        if (tr) tiss += __builtin_amdgcn_s_memrealtime() - ti;
+        const int f = __builtin_amdgcn_readfirstlane(T / g.ntiles), tile = T - f * g.ntiles;
         if (tile == 0 && threadIdx.x == 0 && fp.count[f]) *fp.count[f] = 0;   // K3's detection counter
         float2* __restrict__ z = fp.z[f];
         const StoreZ sz{buf_rsrc(z, (unsigned)B * g.ntiles * zslab * 8u), lgNT, g.ntiles, tile, P, half};
+        const unsigned long long ta = tr ? __builtin_amdgcn_s_memrealtime() : 0;
         fft_passes<LGP, 0, 0, 16, false, K1_SH, K1_THREADS>(Y + cur * bufsz, Ppad, B * NT, twl,
                                                            StoreLds{Y + cur * bufsz}, sz);   // ends with a barrier
+        const unsigned long long tb = tr ? __builtin_amdgcn_s_memrealtime() : 0;
         if (Tn < total) dbf(Y + (nbuf == 2 ? (cur ^ 1) : 0) * bufsz);
         __syncthreads();
+        if (tr) {
+            tfft += tb - ta;
+            tdbf += __builtin_amdgcn_s_memrealtime() - tb;
+        }
         if (nbuf == 2) cur ^= 1;
+    }
+    if (tr) {
+        unsigned long long* o = fp.trace + (size_t)blockIdx.x * 4;
+        o[0] = t0;
+        o[1] = (g.dbg & 16384) ? tpro - t0 : (g.dbg & 32768) ? tiss : tfft;   // 16384 / 32768: prologue / issue ticks
+        o[2] = tdbf;
+        o[3] = __builtin_amdgcn_s_memrealtime();
     }
 }
 
