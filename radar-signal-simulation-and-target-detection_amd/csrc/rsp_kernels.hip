@@ -37,6 +37,7 @@ __device__ __forceinline__ float2 fromf2(f2 a) { return make_float2(a.x, a.y); }
 // Raw buffer resources (SRSRC): 32-bit byte offsets and hardware range checking.  An offset at
 // or past num_records reads 0 / drops the store, so masked lanes need no branch or select.
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #define RSP_OOB 0x80000000u   // > any buffer this library makes (plans are validated < 2 GB/frame)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, unsigned bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
@@ -635,7 +636,8 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
     if (T >= total) return;
     for (int i = threadIdx.x; i < g.twPp_elems; i += K1_THREADS) twl[i] = k.twPp[i];
     constexpr int NJ = CP / 4, MB = BMAX <= 8 ? 1 : 2, TPW = (16 / NJ) / MB > 0 ? (16 / NJ) / MB : 1;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, grp = lane >> 4, col = lane & 15;
+    const int lane = threadIdx.x & 63, grp = lane >> 4, col = lane & 15;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: nlv[] and n are scalar
     float are[MB][NJ], aim[MB][NJ];
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb)
@@ -654,33 +656,37 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
         const int t = wv * TPW + u;
         const int nl = t / ptiles;
         pv[u] = ((t - nl * ptiles) << 5) + 2 * col;
-        nlv[u] = (t < ntp && pv[u] < P) ? nl : -1;
+        nlv[u] = t < ntp ? nl : -1;   // pv < P: P >= 64 here; wave-uniform
         const float2 w01 = nlv[u] >= 0 ? *reinterpret_cast<const float2*>(k.win + pv[u]) : make_float2(0.f, 0.f);
         w0v[u] = w01.x;
         w1v[u] = w01.y;
     }
     const size_t NPc = (size_t)g.cpitch;
+    // per-lane byte offsets of this lane's (channel, pulse pair) inside a cube: loop-invariant,
+    // so a tile's load issue is scalar sample offsets + buffer loads and writes no VGPR but xv
+    // (a VGPR temporary there could be a pending z store's data register: WAR = vmcnt wait)
+    unsigned loff[TPW][NJ];
+#pragma unroll
+    for (int u = 0; u < TPW; ++u)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) loff[u][j] = (unsigned)(((size_t)min(4 * j + grp, C - 1) * NPc + pv[u]) * 8u);
+    const unsigned cube_bytes = (unsigned)((size_t)C * NPc * 8u);
     float4 xv[TPW][NJ];
+    bool vld[TPW];   // wave-uniform: sub-tile u of the tile in flight lies inside the used samples
     auto issue = [&](int TT) {   // cube loads of tile TT (fsf:93 operands) into xv
-        // f is wave-uniform: readfirstlane keeps fp.in[f] a scalar (kernarg) load.  As a vector
-        // load its s_waitcnt vmcnt(0) would also wait for the previous tile's z stores.
         const int f = __builtin_amdgcn_readfirstlane(TT / g.ntiles), tile = TT - f * g.ntiles;
-        const float2* __restrict__ x = fp.in[f];
+        const __amdgpu_buffer_rsrc_t xr = buf_rsrc(fp.in[f], cube_bytes);
 #pragma unroll
         for (int u = 0; u < TPW; ++u) {
             const int np = tile * NT + nlv[u];
-            int n = -1;
-            if (nlv[u] >= 0 && np < g.nU) {
-                n = used_sample(g, np);
-            }
+            vld[u] = nlv[u] >= 0 && np < g.nU;
+            if (vld[u]) {   // no else: zeroing xv here would wait (vmcnt) on the pending z stores
+                const int soff = used_sample(g, np) * P * 8;
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const int c = min(4 * j + grp, C - 1);
-                {   // non-temporal: the cube is read exactly once (148 vs 154 us per 8-frame launch)
-                    const f32x4 t = n >= 0 ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(
-                                                 x + (size_t)c * NPc + (size_t)n * P + pv[u]))
-                                           : f32x4{0.f, 0.f, 0.f, 0.f};
-                    xv[u][j] = make_float4(t.x, t.y, t.z, t.w);
+                for (int j = 0; j < NJ; ++j) {   // non-temporal: the cube is read exactly once
+                    const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(xr, (int)loff[u][j], soff, 2);
+                    xv[u][j] = make_float4(__uint_as_float(t.x), __uint_as_float(t.y), __uint_as_float(t.z),
+                                           __uint_as_float(t.w));
                 }
             }
         }
@@ -690,6 +696,22 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
 #pragma unroll
         for (int u = 0; u < TPW; ++u) {
             if (nlv[u] < 0) continue;
+            if (!vld[u]) {   // samples past the used ones: zero columns, like k1_dbf_mtd's n = -1
+                const int p = pv[u];
+                const int i0 = p + (p >> K1_SH), i1 = (p + 1) + ((p + 1) >> K1_SH);
+#pragma unroll
+                for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int m = 4 * grp + i, b = mb * 8 + (m & 7);
+                        if (b < B) {
+                            float* colp = Yf + 2 * (b * NT + nlv[u]) * Ppad + (m >> 3);
+                            colp[2 * i0] = 0.f;
+                            colp[2 * i1] = 0.f;
+                        }
+                    }
+                continue;
+            }
             f32x4 acc[MB][2];
 #pragma unroll
             for (int mb = 0; mb < MB; ++mb) {
