@@ -114,6 +114,11 @@ def named_config(name):
                           point_prt_segments=(228, 723, 1860))
         W = load_reference_dbf()[:8]
         return cfg, cfar, clus, W, list(V8_BEAM_ANGLES[:8]), list(V8_K_LUT[:7])
+    if name == 'p256':   # test config: P = 256 with 8 beams (persistent K1 at NT = 4, LGP = 8)
+        cfg = make_config(prtNum=256, point_PRT=3072, channel_num=16, beam_num=8,
+                          point_prt_segments=(228, 723, 836))
+        W = load_reference_dbf()[:8]
+        return cfg, cfar, clus, W, list(V8_BEAM_ANGLES[:8]), list(V8_K_LUT[:7])
     if name == 'small':
         cfg = make_config(prtNum=64, point_PRT=3072, channel_num=16, beam_num=4,
                           point_prt_segments=(228, 723, 836))

@@ -208,7 +208,7 @@ def _plan_with_env(s, env, **kw):
                 os.environ[k] = v
 
 
-@pytest.mark.parametrize('name', ['small', 'x2'])
+@pytest.mark.parametrize('name', ['small', 'x2', 'p256'])
 def test_persistent_k1_bit_identical_to_tiled_k1(name):
     """The persistent software-pipelined K1 (k1p_dbf_mtd, default) and the one-tile-per-workgroup
     K1 (RSP_ABLATE=4096) do the same fp32 operations in the same order: identical RDM bits and
@@ -252,6 +252,21 @@ def test_mixed_radix_overlap_save_parity(name, mode):
     cube = noisy_cube(s, tg)
     _, st = chain.process_cube(cube.astype(np.complex128), s['cfg'], s['cfar'], s['clus'], s['pre_o'], keep=True)
     plan = _plan_with_env(s, {'RSP_K2_MIXED': mode})
+    try:
+        gpu = plan.process_cube(cube, frame_idx=1, want_rdm=True, want_cfar=True)
+    finally:
+        plan.close()
+    _map_close(gpu['rdm'], st['rdm'])
+    _map_close(gpu['cfar_maps'], st['S_all'])
+
+
+def test_p256_rdm_parity():
+    """P = 256 (persistent K1 with NT = 4, 256-point slow-time FFT) against the oracle."""
+    s = scenario('p256')
+    tg = targets_for('p256')
+    cube = noisy_cube(s, tg)
+    _, st = chain.process_cube(cube.astype(np.complex128), s['cfg'], s['cfar'], s['clus'], s['pre_o'], keep=True)
+    plan = Plan(s['cfg'], s['cfar'], s['clus'], s['pre_p'])
     try:
         gpu = plan.process_cube(cube, frame_idx=1, want_rdm=True, want_cfar=True)
     finally:
