@@ -7,7 +7,7 @@ frame (v8:170-173) plus Philox noise, synthesised ON the device into a ring of d
 frame cubes (ring > 256 MiB Infinity Cache, so every step reads its cube from HBM).
 One step = one frame through DBF -> MTD -> pulse compression -> GOCA-CFAR -> S9
 estimation (device) -> S10/S11 clustering (host).  Frames are batched
-``--fpl`` per launch and alternate over two HIP streams.
+``--fpl`` per launch and rotate over the plan's lanes (3 HIP streams).
 
 Multi-GPU: one process per GPU (torchrun); frames are sharded (each rank processes its
 own K frames, weak scaling); the only collective is an RCCL all-gather of the
@@ -288,8 +288,8 @@ def main():
             'vs_baseline': None, 'dtype': 'fp32 (complex64)', 'data': 'synthetic (device Philox noise + v8_2 targets)',
             'cells_per_s': fps * cells,
             'achieved_GBps_frame': fps * frame_alg_bytes / 1e9,
-            'config': {'workload': 'BASELINE config #2: %s C=%d B=%d N=%d P=%d G=%d' % (
-                a.config, sz.C, sz.B, sz.N, sz.P, sz.G), 'frames_per_launch': a.fpl, 'ring': a.ring,
+            'config': {'workload': 'BASELINE config #%s: %s C=%d B=%d N=%d P=%d G=%d' % (
+                {'x2': '2', 'x4': '4', 'plumbing': '1'}.get(a.config, '-'), a.config, sz.C, sz.B, sz.N, sz.P, sz.G), 'frames_per_launch': a.fpl, 'ring': a.ring,
                 'parallelism': 'frame-sharded x%d' % world, 'used_samples': sz.used_samples,
                 'targets_reported': n_targets_all},
             'roofline': {'bound': 'hbm', 'kernel': dom['stage'], 'achieved': achieved, 'peak': HBM_PEAK_GBS,

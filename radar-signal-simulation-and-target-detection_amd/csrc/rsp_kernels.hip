@@ -1387,22 +1387,24 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
     } while (0)
     // ---- cross GOCA-CFAR (fsf:192-213); hits go to an LDS queue so that the S9 work is
     //      spread over the whole workgroup instead of serialising in the lane that owns a range cell
-    if (FAST && RT == 64) {
+    if (FAST && (RT == 64 || RT == 32)) {   // RT = 32: long-P tiles (LDS cap in the plan)
         // a thread takes 4 adjacent range cells of one Doppler row: every window value comes
         // from float4 LDS reads (17 per 4 cells instead of 20 scalar reads per cell); sums run
         // left to right over each slice like mean()
         constexpr int DL = -(GR + RR), DR = GR + 1;              // window starts rel. to the cell
         constexpr int BL = floor4(DL), BR = floor4(DR);
         constexpr int NL = (DL + 3 + RR - BL + 3) / 4, NR = (DR + 3 + RR - BR + 3) / 4;
-        const int q = threadIdx.x & 15;
+        const int lgT = RT == 64 ? 4 : 3;                         // log2 threads per row (RT / 4)
+        const int q = threadIdx.x & ((1 << lgT) - 1);
         const int c = hR + 4 * q;                                 // first tile column of the group
         const int r = c0 + c;
         // 16-lane row groups of a wave take rows {0, 2, 1, 3} + 4w: the ds_read_b128 lane groups
         // ({0-3,12-15,20-27}, ... MI355X_MICROARCH.md §LDS) then pair rows 2 apart, 2W = 192
         // floats = 0 mod 64 banks, conflict-free (adjacent rows, W = 96 = 32 mod 64, were 2-way)
-        const int rg = threadIdx.x >> 4, rgp = (rg & ~3) | ((rg & 1) << 1) | ((rg >> 1) & 1);
+        const int rg = threadIdx.x >> lgT;
+        const int rgp = lgT == 4 ? (rg & ~3) | ((rg & 1) << 1) | ((rg >> 1) & 1) : rg;
 #pragma unroll 1
-        for (int v = v0 + rgp; v < v1; v += RSP_THREADS / 16) {
+        for (int v = v0 + rgp; v < v1; v += RSP_THREADS >> lgT) {
             const float* row = S + v * W + c;
             float xl[4 * NL], xr[4 * NR], cv[4];
             f2 lv01 = {0.f, 0.f}, lv23 = {0.f, 0.f}, tv01 = {0.f, 0.f}, tv23 = {0.f, 0.f};   // packed column sums

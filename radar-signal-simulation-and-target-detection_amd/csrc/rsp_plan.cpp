@@ -861,7 +861,8 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     // K3 tile
     g.cfar_hR = (std::max(g.refR + g.guardR, 2) + 3) & ~3;   // halo, multiple of 4 (float4 tile loads)
     g.cfar_RT = 64;
-    while (g.cfar_RT > 8 && (size_t)P * (g.cfar_RT + 2 * g.cfar_hR) * 4 > 96 * 1024) g.cfar_RT >>= 1;
+    // <= 64 KB per tile: >= 2 workgroups per CU (P = 256: RT 32, 64 KB; k3_cfar fast path covers RT 32/64)
+    while (g.cfar_RT > 8 && (size_t)P * (g.cfar_RT + 2 * g.cfar_hR) * 4 > 64 * 1024) g.cfar_RT >>= 1;
     g.cfar_W = (g.cfar_RT + 2 * g.cfar_hR + 3) & ~3;   // LDS row stride, float4 aligned
     if ((size_t)P * g.cfar_W * 4 > 160 * 1024) return bail(fail(RSP_ERR_UNSUPPORTED, "CFAR tile exceeds LDS"));
 

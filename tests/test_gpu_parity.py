@@ -23,7 +23,7 @@ MAP_TOL = 2e-5
 MARGIN = 1e-4
 
 
-@pytest.fixture(scope='module', params=['small', 'x2'])
+@pytest.fixture(scope='module', params=['small', 'x2', 'p256'])
 def case(request):
     s = scenario(request.param)
     tg = targets_for(request.param)
@@ -259,17 +259,3 @@ def test_mixed_radix_overlap_save_parity(name, mode):
     _map_close(gpu['rdm'], st['rdm'])
     _map_close(gpu['cfar_maps'], st['S_all'])
 
-
-def test_p256_rdm_parity():
-    """P = 256 (persistent K1 with NT = 4, 256-point slow-time FFT) against the oracle."""
-    s = scenario('p256')
-    tg = targets_for('p256')
-    cube = noisy_cube(s, tg)
-    _, st = chain.process_cube(cube.astype(np.complex128), s['cfg'], s['cfar'], s['clus'], s['pre_o'], keep=True)
-    plan = Plan(s['cfg'], s['cfar'], s['clus'], s['pre_p'])
-    try:
-        gpu = plan.process_cube(cube, frame_idx=1, want_rdm=True, want_cfar=True)
-    finally:
-        plan.close()
-    _map_close(gpu['rdm'], st['rdm'])
-    _map_close(gpu['cfar_maps'], st['S_all'])
