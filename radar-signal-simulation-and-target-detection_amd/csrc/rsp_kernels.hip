@@ -941,9 +941,11 @@ __device__ __forceinline__ void k2m_fft_job(const Geometry& g, const DevConsts& 
 // Mixed-radix jobs as a launch of their own (jobs [g.mix_job0, njobs), workgroups from
 // g.nwg_k2_pow2): 2 rows x 2560 points over 320 threads, so every radix-16 pass keeps all
 // threads busy (16 points each) and the radix-10 passes 80 % of them.
+#ifndef K2M_THREADS
 #define K2M_THREADS 320
+#endif
 template <int M, int RA, int RB, int RC>
-__global__ __launch_bounds__(K2M_THREADS, 3) void k2m_pc(Geometry g, DevConsts k, FramePtrs fp, int rows_total) {
+__global__ __launch_bounds__(K2M_THREADS, K2M_THREADS > 320 ? 2 : 3) void k2m_pc(Geometry g, DevConsts k, FramePtrs fp, int rows_total) {
     extern __shared__ __attribute__((aligned(16))) float2 L[];
     const int f = blockIdx.y;
     const int wg = g.nwg_k2_pow2 + blockIdx.x;
