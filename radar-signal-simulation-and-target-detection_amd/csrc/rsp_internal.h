@@ -5,7 +5,12 @@
 
 #define RSP_MAX_F 8          // frames batched per launch
 #define RSP_LANES 4          // max streams of the throughput queue (batches in flight)
+#ifndef RSP_K2_POINTS
 #define RSP_K2_POINTS 4096   // complex points per pulse-compression workgroup
+#endif
+#ifndef K2_THREADS
+#define K2_THREADS 256       // threads per pulse-compression workgroup (16 points each)
+#endif
 #define K2M_POINTS_HOST 2560 // the same for the mixed-radix (5 * 2^k) blocks (K2M_POINTS)
 #define RSP_THREADS 256
 

@@ -992,7 +992,7 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     const __amdgpu_buffer_rsrc_t zr = buf_rsrc(z, (unsigned)g.B * g.ntiles * P * g.NT * 8u);
 #pragma unroll
     for (int t = 0; t < NB0; ++t) {
-        const int beta = tid + t * RSP_THREADS;
+        const int beta = tid + t * K2_THREADS;
         const int rl = beta / nb0, j = beta & (nb0 - 1);
         const int rho = row0 + rl;
         const int b = rho / P, v = rho - b * P;
@@ -1019,40 +1019,40 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     }
     // H for the last forward pass's outputs j + r M/RL; butterflies t and t + (M/RL)/NTHR of a
     // thread have the same j (different rows), so only the distinct ones are loaded
-    constexpr int NHT = (M / RL) / RSP_THREADS >= NBL ? NBL : ((M / RL) / RSP_THREADS > 0 ? (M / RL) / RSP_THREADS : 1);
+    constexpr int NHT = (M / RL) / K2_THREADS >= NBL ? NBL : ((M / RL) / K2_THREADS > 0 ? (M / RL) / K2_THREADS : 1);
     f2 hreg[NHT * RL];
 #pragma unroll
     for (int t = 0; t < NHT; ++t) {
-        const int j = (tid + t * RSP_THREADS) & (M / RL - 1);   // last pass: Ns = nb = M / RL, idxD = j
+        const int j = (tid + t * K2_THREADS) & (M / RL - 1);   // last pass: Ns = nb = M / RL, idxD = j
 #pragma unroll
         for (int r = 0; r < RL; ++r) hreg[t * RL + r] = tof2(k.H[sd.H_off + j + r * (M / RL)]);
     }
     constexpr int NTWF = tw_total(LGM, false, CMP);
     constexpr int NTW = NTWF + tw_total(LGM, true, CMP);
     static_assert(NTW <= (CMP ? K2_LDS_TW_CMP : K2_LDS_TW), "K2 twiddle tables exceed their LDS slot");
-    constexpr int NT_TAB = TWG ? 0 : (NTW + RSP_THREADS - 1) / RSP_THREADS;
+    constexpr int NT_TAB = TWG ? 0 : (NTW + K2_THREADS - 1) / K2_THREADS;
     float2 tv[NT_TAB > 0 ? NT_TAB : 1];
 #pragma unroll
     for (int u = 0; u < NT_TAB; ++u) {
-        const int i = tid + u * RSP_THREADS;
+        const int i = tid + u * K2_THREADS;
         if (i < NTW) tv[u] = k.twM[sd.tw_off + i];
     }
     // forward pass 0 (Ns = 1, no twiddles) straight from the loaded samples
-    sh_store<R0, false, NB0, K2_SH, RSP_THREADS, LGM, 0>(v0, rs, rows, StoreLds{L});
+    sh_store<R0, false, NB0, K2_SH, K2_THREADS, LGM, 0>(v0, rs, rows, StoreLds{L});
 #pragma unroll
     for (int u = 0; u < NT_TAB; ++u) {
-        const int i = tid + u * RSP_THREADS;
+        const int i = tid + u * K2_THREADS;
         if (i < NTW) twl[i] = tv[u];
     }
     __syncthreads();
     trace_stamp(fp, 1);
     // forward passes 1 .. NP-2
-    fft_range<LGM, 1, NP - 1, RB0, 16, false, false, K2_SH, RSP_THREADS, CMP>(L, rs, rows, twl, StoreLds{L},
+    fft_range<LGM, 1, NP - 1, RB0, 16, false, false, K2_SH, K2_THREADS, CMP>(L, rs, rows, twl, StoreLds{L},
                                                                                StoreLds{L});
     // fused: forward last pass, x H (1/M folded in), inverse pass 0 of the reversed plan
     {
         f2 v[NBL][RL];
-        sh_load<RL, false, NBL, K2_SH, RSP_THREADS, LGM, LGM - RBL, CMP>(L, rs, rows,
+        sh_load<RL, false, NBL, K2_SH, K2_THREADS, LGM, LGM - RBL, CMP>(L, rs, rows,
                                                                        twl + tw_pass_off(LGM, NP - 1, false, CMP), v);
         __syncthreads();
 #pragma unroll
@@ -1061,14 +1061,14 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
 #pragma unroll
             for (int r = 0; r < RL; ++r) v[t][r] = vmul(v[t][r], hreg[(t % NHT) * RL + r]);
         }
-        sh_store<RL, true, NBL, K2_SH, RSP_THREADS, LGM, 0>(v, rs, rows, StoreLds{L});
+        sh_store<RL, true, NBL, K2_SH, K2_THREADS, LGM, 0>(v, rs, rows, StoreLds{L});
         __syncthreads();
     }
     trace_stamp(fp, 2);
     // inverse passes 1 .. NP-1 (reversed radices); the last keeps the valid overlap-save
     // outputs = stitched gates
     const int gend = min(sd.gb, g0 + sd.V);
-    fft_range<LGM, 1, NP, RBL, 16, true, true, K2_SH, RSP_THREADS, CMP>(
+    fft_range<LGM, 1, NP, RBL, 16, true, true, K2_SH, K2_THREADS, CMP>(
         L, rs, rows, twl + NTWF, StoreLds{L}, StoreRdm{buf_rsrc(rdm, (unsigned)rows_total * G * 8u),
                                                       buf_rsrc(mag, (unsigned)rows_total * g.Gp * 4u), G, g.Gp,
                                                       row0, rows_total, Lh1, g0, gend});
@@ -1076,7 +1076,7 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
 }
 
 template <bool TWG, bool CMP>
-__global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k, FramePtrs fp, int rows_total) {
+__global__ __launch_bounds__(K2_THREADS, 512 / K2_THREADS) void k2_pc(Geometry g, DevConsts k, FramePtrs fp, int rows_total) {
     extern __shared__ __attribute__((aligned(16))) float2 L[];   // data | twiddles (M) | H (M)
     const int f = blockIdx.y;
     const int wg = blockIdx.x;
@@ -1096,9 +1096,9 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k,
 
     if (sd.type == 1 && sd.mixM) {
         switch (sd.mixM) {
-            case 640: k2m_fft_job<640, 8, 8, 10, RSP_THREADS, K2M_POINTS>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
-            case 1280: k2m_fft_job<1280, 16, 8, 10, RSP_THREADS, K2M_POINTS>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
-            default: k2m_fft_job<2560, 16, 16, 10, RSP_THREADS, K2M_POINTS>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
+            case 640: k2m_fft_job<640, 8, 8, 10, K2_THREADS, K2M_POINTS>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
+            case 1280: k2m_fft_job<1280, 16, 8, 10, K2_THREADS, K2M_POINTS>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
+            default: k2m_fft_job<2560, 16, 16, 10, K2_THREADS, K2M_POINTS>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
         }
     } else if (sd.type == 1) {
 #ifdef K2_ONLY_LGM   // ISA inspection builds: one block size only
@@ -1120,11 +1120,11 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k,
         const int W = hi - lo + 1;
         const int PADL = sd.ntaps - 1, WP = W + PADL;
         const int nw = rows * WP;
-        for (int e0 = 0; e0 < nw; e0 += 16 * RSP_THREADS) {
+        for (int e0 = 0; e0 < nw; e0 += 16 * K2_THREADS) {
             float2 val[16];
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
-                const int e = e0 + tid + u * RSP_THREADS;
+                const int e = e0 + tid + u * K2_THREADS;
                 val[u] = make_float2(0.f, 0.f);
                 if (e < nw) {
                     const int rl = e / WP, i = e - rl * WP - PADL;
@@ -1137,12 +1137,12 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k,
             }
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
-                const int e = e0 + tid + u * RSP_THREADS;
+                const int e = e0 + tid + u * K2_THREADS;
                 if (e < nw) L[e] = val[u];
             }
         }
         float* tp = reinterpret_cast<float*>(L + nw);   // taps: LDS broadcast reads
-        for (int e = tid; e < sd.ntaps; e += RSP_THREADS) tp[e] = k.taps[sd.taps_off + e];
+        for (int e = tid; e < sd.ntaps; e += K2_THREADS) tp[e] = k.taps[sd.taps_off + e];
         __syncthreads();
         trace_stamp(fp, 1);
         const int nout = sd.gb - sd.ga;
@@ -1150,7 +1150,7 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k2_pc(Geometry g, DevConsts k,
         // sample per tap (1 LDS read + 4 FMAs per tap); a group whose circshift index wraps
         // mid-group takes the per-gate loop
         const int ngrp = (nout + 3) >> 2;
-        for (int e = tid; e < rows * ngrp; e += RSP_THREADS) {
+        for (int e = tid; e < rows * ngrp; e += K2_THREADS) {
             const int rl = e / ngrp, q0 = 4 * (e - rl * ngrp);
             const int rho = row0 + rl;
             if (rho >= rows_total) continue;
@@ -1662,7 +1662,7 @@ hipError_t launch_k2(const Geometry& g, const DevConsts& k, const FramePtrs& fp,
     do {                                                                                             \
         if ((e = allow_lds(k2_pc<TWG, CMP>, LDS)) != hipSuccess) return e;                           \
         if (g.nwg_k2_pow2 > 0)                                                                       \
-            hipLaunchKernelGGL((k2_pc<TWG, CMP>), dim3(g.nwg_k2_pow2, nf), dim3(RSP_THREADS), LDS, s, g, k, fp, rows); \
+            hipLaunchKernelGGL((k2_pc<TWG, CMP>), dim3(g.nwg_k2_pow2, nf), dim3(K2_THREADS), LDS, s, g, k, fp, rows); \
     } while (0)
     switch (g.dbg & (64 | 256)) {
         case 0: K2_LAUNCH(true, true, lds_g); break;
