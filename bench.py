@@ -57,7 +57,7 @@ def scene(cfg):
     return [t for t in C.v8_2_targets() if t['Range'] < rmax]
 
 
-def cpu_baseline(cfg, cfar, clus, W, ang, k, targets, budget_s=15.0, nframes=0):
+def cpu_baseline(cfg, cfar, clus, W, ang, k, targets, budget_s=15.0, nframes=0, name='x2'):
     """The oracle (numpy/scipy restatement, complex128 like MATLAB) timed on this host."""
     import scipy.fft as sfft
     from rsp import config as C
@@ -81,7 +81,7 @@ def cpu_baseline(cfg, cfar, clus, W, ang, k, targets, budget_s=15.0, nframes=0):
     return {'value': 1.0 / med, 'unit': 'frames/s', 'cores': cores, 'kind': 'port',
             'sample': '%d frames of the same %s cube, median of per-frame times (%.3f s/frame); oracle = '
                       'numpy/scipy complex128 restatement of fsf S5-S11, CFAR vectorised '
-                      '(the MATLAB scalar CFAR loop fsf:192-213 would be slower)' % (len(times), 'x2', med)}
+                      '(the MATLAB scalar CFAR loop fsf:192-213 would be slower)' % (len(times), name, med)}
 
 
 MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense peak
@@ -302,7 +302,7 @@ def main():
                          'stages': stages},
         }
         if world == 1 and not a.no_cpu_baseline:
-            out['cpu_baseline'] = cpu_baseline(cfg, cfar, clus, W, ang, k, targets, nframes=a.cpu_frames)
+            out['cpu_baseline'] = cpu_baseline(cfg, cfar, clus, W, ang, k, targets, nframes=a.cpu_frames, name=a.config)
         else:
             out['cpu_baseline'] = None
     for p in ring:
