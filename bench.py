@@ -5,9 +5,11 @@ Workload: 16-channel x 8-beam x 4096-sample x 128-pulse echo cubes (BASELINE con
 ``named_config('x2')``), synthetic: the v8_2 five-target scene (v8_2:28-51) evolved per
 frame (v8:170-173) plus Philox noise, synthesised ON the device into a ring of distinct
 frame cubes (ring > 256 MiB Infinity Cache, so every step reads its cube from HBM).
-One step = one frame through DBF -> MTD -> pulse compression -> GOCA-CFAR -> S9
-estimation (device) -> S10/S11 clustering (host).  Frames are batched
-``--fpl`` per launch and rotate over the plan's lanes (3 HIP streams).
+One step = one batch of ``--fpl`` distinct frames (one launch of each kernel) through
+DBF -> MTD -> pulse compression -> GOCA-CFAR -> S9 estimation (device) -> S10/S11
+clustering (host); batches rotate over the plan's lanes (3 HIP streams).  Warm-up
+always runs at least two batches per lane, so every stream is warm before the timed
+region whatever ``--warmup`` says.  ``value`` is frames/s = steps x fpl / time.
 
 Multi-GPU: one process per GPU (torchrun); frames are sharded (each rank processes its
 own K frames, weak scaling); the only collective is an RCCL all-gather of the
@@ -30,13 +32,39 @@ for _p in (ROOT, PKG):
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+NLANES = 3              # streams of the plan's throughput queue (rsp_plan.cpp)
+
+
+def host_cpu():
+    """CPU model, nproc, the affinity set and the cgroup CPU quota of this host; `usable` =
+    the threads the CPU baseline may run (the affinity set capped by the quota)."""
+    model = 'unknown'
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    model = line.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            q, per = f.read().split()
+            if q != 'max':
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
+    return {'model': model, 'nproc': os.cpu_count(), 'affinity': aff, 'cgroup_quota': quota, 'usable': usable}
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=4000)
-    ap.add_argument('--warmup', type=int, default=200)
+    ap.add_argument('--steps', type=int, default=500)
+    ap.add_argument('--warmup', type=int, default=20)
     ap.add_argument('--config', default='x2')
     ap.add_argument('--fpl', type=int, default=8, help='frames per launch (8: fewest tail rounds, measured)')
     ap.add_argument('--ring', type=int, default=8, help='distinct device-resident frame cubes')
@@ -62,7 +90,8 @@ def cpu_baseline(cfg, cfar, clus, W, ang, k, targets, budget_s=15.0, nframes=0, 
     import scipy.fft as sfft
     from rsp import config as C
     from oracle import chain, precompute as op
-    cores = min(16, len(os.sched_getaffinity(0)))
+    hc = host_cpu()
+    cores = hc['usable']
     pre = op.precompute(cfg, W, ang, k, C.V8_FIR)
     cube = chain.synthesize_echo(targets, cfg, pre) + chain.philox_noise(cfg, 1, 20250101)
     times = []
@@ -78,7 +107,7 @@ def cpu_baseline(cfg, cfar, clus, W, ang, k, targets, budget_s=15.0, nframes=0, 
             if not nframes and (time.perf_counter() - t_start > budget_s or len(times) >= 50):
                 break
     med = float(np.median(times))
-    return {'value': 1.0 / med, 'unit': 'frames/s', 'cores': cores, 'kind': 'port',
+    return {'value': 1.0 / med, 'unit': 'frames/s', 'cores': cores, 'kind': 'port', 'host': hc,
             'sample': '%d frames of the same %s cube, median of per-frame times (%.3f s/frame); oracle = '
                       'numpy/scipy complex128 restatement of fsf S5-S11, CFAR vectorised '
                       '(the MATLAB scalar CFAR loop fsf:192-213 would be slower)' % (len(times), name, med)}
@@ -214,12 +243,12 @@ def main():
         tg = C.evolve_targets(tg, cfg)
     plan.sync()
 
-    def run(nframes, base):
-        for i in range(nframes):
+    def run(nbatches, base):   # nbatches full batches of fpl frames
+        for i in range(nbatches * a.fpl):
             plan.enqueue(ring[i % a.ring], base + i)
         plan.drain()
 
-    run(a.warmup, 0)
+    run(max(a.warmup, 2 * NLANES), 0)   # every lane (stream) warmed with full batches
     plan.results(clear=True)
 
     if dist is not None:
@@ -250,7 +279,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
-    frames = a.steps * world
+    frames = a.steps * a.fpl * world
     fps = frames / el
     cells = sz.B * sz.G * sz.P
     out = None
@@ -289,7 +318,7 @@ def main():
             'cells_per_s': fps * cells,
             'achieved_GBps_frame': fps * frame_alg_bytes / 1e9,
             'config': {'workload': 'BASELINE config #%s: %s C=%d B=%d N=%d P=%d G=%d' % (
-                {'x2': '2', 'x4': '4', 'plumbing': '1'}.get(a.config, '-'), a.config, sz.C, sz.B, sz.N, sz.P, sz.G), 'frames_per_launch': a.fpl, 'ring': a.ring,
+                {'x2': '2', 'x4': '4', 'plumbing': '1'}.get(a.config, '-'), a.config, sz.C, sz.B, sz.N, sz.P, sz.G), 'frames_per_launch': a.fpl, 'frames_per_step': a.fpl, 'ring': a.ring,
                 'parallelism': 'frame-sharded x%d' % world, 'used_samples': sz.used_samples,
                 'targets_reported': n_targets_all},
             'roofline': {'bound': 'hbm', 'kernel': dom['stage'], 'achieved': achieved, 'peak': HBM_PEAK_GBS,
