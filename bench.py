@@ -66,6 +66,8 @@ def parse():
     ap.add_argument('--steps', type=int, default=500)
     ap.add_argument('--warmup', type=int, default=20)
     ap.add_argument('--config', default='x2')
+    ap.add_argument('--precision', default='c128', choices=['c128', 'c64'],
+                    help="c128: complex double, the reference's MATLAB arithmetic (default); c64: complex single")
     ap.add_argument('--fpl', type=int, default=8, help='frames per launch (8: fewest tail rounds, measured)')
     ap.add_argument('--ring', type=int, default=8, help='distinct device-resident frame cubes')
     ap.add_argument('--profile-iters', type=int, default=50)
@@ -232,10 +234,11 @@ def main():
 
     cfg, cfar, clus, W, ang, k = C.named_config(a.config)
     pre = precompute(cfg, W, ang, k, C.V8_FIR)
-    plan = Plan(cfg, cfar, clus, pre, device=local if world > 1 else 0, frames_per_launch=a.fpl)
+    plan = Plan(cfg, cfar, clus, pre, device=local if world > 1 else 0, frames_per_launch=a.fpl,
+                precision=a.precision)
     sz = plan.sizes
     targets = scene(cfg)
-    cube_bytes = sz.cube_elems * 8
+    cube_bytes = plan.cube_bytes
     ring = [plan.device_alloc(cube_bytes) for _ in range(a.ring)]
     tg = targets
     for i, p in enumerate(ring):
@@ -300,7 +303,7 @@ def main():
         dom = max(stages, key=lambda s: s['ms_per_launch'])
         achieved = dom['achieved_GBps']
         traffic = None
-        tf = os.path.join(ROOT, 'profiles', 'pmc_traffic_%s.json' % a.config)
+        tf = os.path.join(ROOT, 'profiles', 'pmc_traffic_%s_%s.json' % (a.config, a.precision))
         if os.path.exists(tf):
             with open(tf) as f:
                 tj = json.load(f)
@@ -309,12 +312,15 @@ def main():
             if tr is not None:   # scaled from the PMC passes' frames per launch to this run's
                 traffic = tr * dom['frames_per_launch'] / float(tj.get('_frames_per_launch', 4))
                 dom['pmc_traffic_bytes'] = traffic
-        frame_alg_bytes = sz.C * sz.N * sz.P * 8 + cells * 8
+        esz = sz.elem_bytes
+        frame_alg_bytes = sz.C * sz.N * sz.P * esz + cells * esz   # cube read + RD map write
         out = {
-            'metric': 'frames/sec + range-Doppler cells/sec, 16ch×8beam×4096samp×128pulse',
+            'metric': 'frames/sec + range-Doppler cells/sec, %dch×%dbeam×%dsamp×%dpulse' % (sz.C, sz.B, sz.N, sz.P),
             'value': fps, 'unit': 'frames/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
             'ms_per_step': el / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
-            'vs_baseline': None, 'dtype': 'fp32 (complex64)', 'data': 'synthetic (device Philox noise + v8_2 targets)',
+            'vs_baseline': None,
+            'dtype': 'fp64 (complex128)' if a.precision == 'c128' else 'fp32 (complex64)',
+            'data': 'synthetic (device Philox noise + v8_2 targets)',
             'cells_per_s': fps * cells,
             'achieved_GBps_frame': fps * frame_alg_bytes / 1e9,
             'config': {'workload': 'BASELINE config #%s: %s C=%d B=%d N=%d P=%d G=%d' % (

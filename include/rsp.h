@@ -21,6 +21,9 @@
  *     range-Doppler maps [P x G x B], CFAR maps [P x G x (B-1)];
  *   - indices reported to the caller are 1-based (fun_process_single_frame.m:220);
  *   - segment starts in rsp_precomputed are 1-based (v8:116-117,130).
+ * Arithmetic: a plan computes in complex double (RSP_C128, MATLAB's double as in
+ * fun_process_single_frame.m:47,92,101,131 -- the default) or, on request, complex
+ * single (RSP_C64); device-resident cubes and maps are in the plan's precision.
  * Errors: every function returns RSP_OK (0) or a negative rsp_status; the
  * message of the last failure on the calling thread is rsp_last_error().
  * Threading: a plan is not thread-safe; use one plan per host thread (MATLAB
@@ -36,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RSP_ABI_VERSION 1
+#define RSP_ABI_VERSION 2
 
 typedef enum rsp_status {
     RSP_OK = 0,
@@ -142,6 +145,8 @@ typedef struct rsp_sizes {
     int32_t used_samples;     /* fast-time samples the chain actually reads */
     int32_t max_detections;   /* per frame device capacity                  */
     int32_t n_stages;         /* device stages (for rsp_profile_stages)     */
+    int32_t precision;        /* RSP_C128 or RSP_C64: device cube / map type */
+    int32_t elem_bytes;       /* bytes of one device complex element (16/8) */
 } rsp_sizes;
 
 typedef struct rsp_plan rsp_plan;
@@ -149,10 +154,25 @@ typedef struct rsp_plan rsp_plan;
 int32_t rsp_abi_version(void);
 const char* rsp_last_error(void);
 
-/* Build a plan on HIP device `device`: uploads DBF weights, FIR taps, matched-filter
- * spectra (re-blocked for overlap-save), MTD window, axes, angles, K-LUT.
+/* Plan options (rsp_plan_options_default fills the defaults shown). */
+#define RSP_PLAN_K1_TILED 1   /* force the one-tile-per-workgroup K1 instead of the persistent
+                                 one (both compute the same operations; parity tests compare them) */
+typedef struct rsp_plan_options {
+    int32_t device;              /* HIP device ordinal (0)                                   */
+    int32_t frames_per_launch;   /* frames batched into each kernel launch by the queue (1)  */
+    int32_t precision;           /* RSP_C128 (MATLAB double, default) or RSP_C64             */
+    int32_t flags;               /* RSP_PLAN_* (0)                                           */
+} rsp_plan_options;
+int32_t rsp_plan_options_default(rsp_plan_options* opt);
+
+/* Build a plan: uploads DBF weights, FIR taps, matched-filter spectra (re-blocked for
+ * overlap-save), MTD window, axes, angles, K-LUT in the plan's precision.
  * `frames_per_launch` (1..8) frames are batched into each kernel launch by the
- * queue interface; rsp_process_* always run one frame. */
+ * queue interface; rsp_process_* always run one frame.  rsp_plan_create = the defaults
+ * with `device` and `frames_per_launch` (complex double). */
+int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfar,
+                           const rsp_cluster_params* cluster, const rsp_precomputed* pre,
+                           const rsp_plan_options* opt, rsp_plan** out);
 int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar,
                         const rsp_cluster_params* cluster, const rsp_precomputed* pre,
                         int32_t device, int32_t frames_per_launch, rsp_plan** out);
@@ -160,7 +180,9 @@ int32_t rsp_plan_destroy(rsp_plan* plan);
 int32_t rsp_query_sizes(const rsp_plan* plan, rsp_sizes* out);
 
 /* Cube-in path: S5..S11 of fun_process_single_frame on one host cube
- * (layout RSP_LAYOUT_PNC, dtype RSP_C64 or RSP_C128).  Synchronous. */
+ * (layout RSP_LAYOUT_PNC, dtype RSP_C64 or RSP_C128; converted to the plan's precision
+ * only if they differ).  Synchronous.  out->cfar_maps, when requested, is the map K3
+ * thresholds on the device (rdm_for_cfar_all, fsf:184-187). */
 int32_t rsp_process_cube(rsp_plan* plan, const void* cube, int32_t dtype, int32_t layout,
                          int32_t frame_idx, rsp_frame_out* out);
 
@@ -169,14 +191,14 @@ int32_t rsp_process_cube(rsp_plan* plan, const void* cube, int32_t dtype, int32_
 int32_t rsp_process_targets(rsp_plan* plan, const rsp_target_in* targets, int32_t n_targets,
                             int32_t frame_idx, uint64_t seed, double p_noise, rsp_frame_out* out);
 
-/* Synthesise (S4 + S4.1) one cube on the device into `d_cube` (complex64, PNC layout,
- * device pointer with cube_elems entries).  Enqueued on the plan's stream 0. */
+/* Synthesise (S4 + S4.1) one cube on the device into `d_cube` (the plan's precision,
+ * PNC layout, device pointer with cube_elems entries).  Synchronous. */
 int32_t rsp_synthesize_device(rsp_plan* plan, const rsp_target_in* targets, int32_t n_targets,
                               int32_t frame_idx, uint64_t seed, double p_noise, void* d_cube);
 
 /* ---- device-resident queue (throughput path) ----
- * rsp_enqueue_device: process a complex64 PNC cube already resident in device
- * memory.  Frames are batched frames_per_launch at a time and alternate over the
+ * rsp_enqueue_device: process a PNC cube (the plan's precision) already resident in
+ * device memory.  Frames are batched frames_per_launch at a time and alternate over the
  * plan's lanes (streams); detections come back asynchronously and are clustered
  * on the host.  rsp_drain waits for everything queued.  Results are kept in
  * enqueue order until rsp_results_clear. */
@@ -197,7 +219,7 @@ int32_t rsp_process_stage2(rsp_plan* plan, const void* iq_beams, int32_t dtype,
 /* ---- measurement ----
  * Time each device stage `iters` times on the plan's stream with HIP events.  Each launch
  * batches nf = min(n_cubes, frames_per_launch) frames taken from the device-resident
- * complex64 cubes d_cubes[]; launch j takes cubes (j nf + f) mod n_cubes, f < nf.  ms_out[i] = average ms per launch of stage i,
+ * cubes d_cubes[] (plan precision); launch j takes cubes (j nf + f) mod n_cubes, f < nf.  ms_out[i] = average ms per launch of stage i,
  * bytes_out[i] = algorithmic HBM bytes per launch (nf frames), *frames_out = nf.
  * Stage names via rsp_stage_name. */
 int32_t rsp_profile_stages(rsp_plan* plan, const void* const* d_cubes, int32_t n_cubes, int32_t iters,

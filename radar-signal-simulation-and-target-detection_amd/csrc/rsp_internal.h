@@ -5,14 +5,15 @@
 
 #define RSP_MAX_F 8          // frames batched per launch
 #define RSP_LANES 4          // max streams of the throughput queue (batches in flight)
-#ifndef RSP_K2_POINTS
 #define RSP_K2_POINTS 4096   // complex points per pulse-compression workgroup
-#endif
-#ifndef K2_THREADS
 #define K2_THREADS 256       // threads per pulse-compression workgroup (16 points each)
-#endif
-#define K2M_POINTS_HOST 2560 // the same for the mixed-radix (5 * 2^k) blocks (K2M_POINTS)
 #define RSP_THREADS 256
+
+// Arithmetic of a plan: every device buffer, table and operation of the chain is in one of
+// these.  PREC_F64 is MATLAB's complex double (the reference's arithmetic, fsf:47,92,101,131);
+// PREC_F32 is complex single (an explicitly narrower option).
+#define RSP_PREC_F32 0
+#define RSP_PREC_F64 1
 
 // Philox4x32-10 (Salmon et al., SC'11) in place on counter c with key (k0, k1); the streams
 // built on it are documented in oracle/philox.py (echo noise) and oracle/music.py (MUSIC).
@@ -48,10 +49,9 @@ struct SegDesc {
     int off;         // compacted sample index of `lo`
     // direct FIR: y[g] = sum_j h[j] x~(seg_lo + k - j), k = (g + delay) mod Ls
     int ntaps, delay, Ls, taps_off;
-    // FFT overlap-save: y[g] = sum_{j<Lh} h[j] x~(seg_lo + g - j), block size M, V = M-Lh+1 valid
+    // FFT overlap-save: y[g] = sum_{j<Lh} h[j] x~(seg_lo + g - j), block size M = 2^logM,
+    // V = M-Lh+1 valid outputs per block
     int Lh, M, logM, V, nblocks, H_off, tw_off;
-    int mixM;        // 0: M = 2^logM (k2_fft_job); else M = 5 * 2^k (k2m_fft_job, radices 16/8 and 10)
-    int nrad, rad[8];
     int rows_per_wg;
 };
 
@@ -65,21 +65,20 @@ struct K2Job {
 #define RSP_MAX_IVL 4
 
 struct Geometry {
+    int prec;        // RSP_PREC_F32 / RSP_PREC_F64
     int C, B, P, N, G;
-    int cpitch;      // device cube channel pitch in complex samples (>= N*P; padded off power-of-two HBM strides)
-    int Gp;          // row stride of the magnitude maps (G rounded up to 4 floats)
+    int cpitch;      // device cube channel pitch in complex samples (= N*P)
+    int Gp;          // row stride of the magnitude maps (G rounded up to 4)
     int NT, nU, ntiles, Ppad;
-    int wc_elems;    // conj(W) entries, [CP][BMAX]
     int twPp_elems;  // per-pass twiddles of the P-point FFT
-    int pow2P, logP, nradP, radP[8];
+    int pow2P, logP;
     int nseg, njobs, nwg_k2;
-    int nwg_k2_pow2, mix_job0;   // k2_pc covers workgroups [0, nwg_k2_pow2); k2m_pc jobs [mix_job0, njobs)
     int cfar_RT, cfar_hR, cfar_W;
     int refR, guardR, refV, guardV;
-    float T;
+    double T;        // T_CFAR
     int max_dets;
-    int dbg;         // RSP_ABLATE bit mask: timing-only ablations (outputs invalid when set)
     int ncu;         // compute units of the device (persistent K1 grid)
+    int k1_tiled;    // force the one-tile-per-workgroup K1 (RSP_PLAN_K1_TILED, parity tests)
     // used fast-time samples as <= RSP_MAX_IVL intervals: compacted n' in [ivl_start[q],
     // ivl_start[q+1]) is sample ivl_lo[q] + n' - ivl_start[q] (kernel-argument lookup, no
     // dependent global load before the cube loads)
@@ -96,28 +95,27 @@ __host__ __device__ inline int k3_ntiles(const Geometry& g) {
     return (g.G - rc0 - (rc0 & ~3) + g.cfar_RT - 1) / g.cfar_RT;
 }
 
+// Per-frame device buffers of one launch.  Element types follow Geometry::prec: complex
+// values are (re, im) pairs of float or double, maps are float or double.
 struct FramePtrs {
-    const float2* in[RSP_MAX_F];   // K1 input cube (PNC) or beam cube
-    float2* z[RSP_MAX_F];          // compacted Doppler-domain rows
-    float2* rdm[RSP_MAX_F];        // [B][P][G]
-    float* mag[RSP_MAX_F];         // |rdm| [B][P][Gp] (K2 epilogue, read by K3)
-    unsigned long long* trace;     // diagnostic: 4 s_memrealtime stamps per workgroup, or null
+    const void* in[RSP_MAX_F];     // K1 input cube (PNC) or beam cube
+    void* z[RSP_MAX_F];            // compacted Doppler-domain rows
+    void* rdm[RSP_MAX_F];          // [B][P][G] complex
+    void* mag[RSP_MAX_F];          // |rdm| [B][P][Gp] (K2 epilogue, read by K3)
+    void* smap[RSP_MAX_F];         // optional: rdm_for_cfar_all [B-1][P][G] as K3 thresholds it (fsf:184-187)
+    unsigned long long* trace;     // diagnostic builds (-DRSP_DEBUG_KNOBS): 4 stamps per workgroup
     DevDet* dets[RSP_MAX_F];
     int* count[RSP_MAX_F];
 };
 
 struct DevConsts {
-    const float2* Wc;        // conj(W) [CP][BMAX]
-    const float* Atab;       // DBF MFMA A operands per lane: [MB][CP/4][Re,Im][64] (build_dbf_atab)
-    const float* win;        // MTD window [P]
-    const float2* twP;       // W_P^i table (direct DFT path)
-    const float2* twPp;      // per-pass Stockham twiddles of the P-point FFT
-    const int* nof;          // compacted index -> sample index (-1 = pad)
-    const SegDesc* segs;
-    const K2Job* jobs;
-    const float* taps;
-    const float2* H;         // overlap-save spectra, 1/M scaled
-    const float2* twM;       // per-pass Stockham twiddles of each overlap-save block size
+    const void* Atab;        // DBF MFMA A operands per lane: [MB][CP/4][Re,Im][64] (build_dbf_atab), real
+    const void* win;         // MTD window [P], real
+    const void* twP;         // W_P^i table (direct DFT path), complex
+    const void* twPp;        // per-pass Stockham twiddles of the P-point FFT, complex
+    const void* taps;        // narrow FIR taps, real
+    const void* H;           // overlap-save spectra, 1/M scaled, complex
+    const void* twM;         // per-pass Stockham twiddles of each overlap-save block size, complex
     const double* range_axis;
     const double* velocity_axis;
     const double* beam_angles;
@@ -133,13 +131,11 @@ struct SynthTarget {          // per-target constants of S4 (fsf:51-73), host-co
 };
 
 // Launchers (rsp_kernels.hip).  `mode` bits for K1: 1 = apply DBF, 2 = apply MTD.
-hipError_t launch_k1(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int mode,
-                     int ch_in, hipStream_t s);
-hipError_t launch_k2(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int rows,
-                     hipStream_t s);
+hipError_t launch_k1(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int mode, hipStream_t s);
+hipError_t launch_k2(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int rows, hipStream_t s);
 hipError_t launch_k3(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, hipStream_t s);
-hipError_t launch_mtd_cols(const Geometry& g, const DevConsts& k, const float2* pc, float2* rdm,
-                           hipStream_t s);
-hipError_t launch_synth(const Geometry& g, const double* tx, const SynthTarget* tg, int nt,
-                        int frame_idx, uint64_t seed, double noise_scale, float2* cube,
-                        hipStream_t s);
+hipError_t launch_mtd_cols(const Geometry& g, const DevConsts& k, const void* pc, void* rdm, hipStream_t s);
+hipError_t launch_synth(const Geometry& g, const double* tx, const SynthTarget* tg, int nt, int frame_idx,
+                        uint64_t seed, double noise_scale, void* cube, hipStream_t s);
+// K1 tile geometry the launcher will use (persistent or tiled) for the plan's NT choice
+bool k1_persistent_fits(const Geometry& g);

@@ -9,93 +9,116 @@
 //   k2_pc       : pulse compression along fast time of every (beam, Doppler) row
 //                 (fsf:101-126): direct FIR for the narrow segment, overlap-save FFT
 //                 (Stockham radix-16/8/4/2 in LDS) for medium/long, gate stitching
-//                 fused into the output store -> RDM [B][P][G].
+//                 fused into the output store -> RDM [B][P][G] + |RDM|.
 //   k3_cfar     : |RDM| adjacent-beam sum (fsf:184-187), cross GOCA-CFAR (fsf:192-213),
 //                 atomic compaction (fsf:215-221) and S9 spline/monopulse estimation
 //                 (fsf:237-290) of each detection.
 //   k_mtd_cols  : MTD over pulses of a pulse-compressed cube (stage-2 path).
 //   k_synth     : S4 echo synthesis + S4.1 Philox noise (fsf:45-88) on the device.
+//
+// Every kernel is a template over the real type T of the plan: double (complex128, the
+// reference's MATLAB arithmetic; the default) or float (complex64).  Complex values are
+// 2-wide ext_vector pairs (re, im) of T in registers, LDS and HBM alike.
 #include "rsp_internal.h"
 #include <math.h>
+#include <algorithm>
 
 namespace {
 
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-
-// ---- complex values as 2-wide float vectors ---------------------------------------------
-// The FFT core keeps every complex value in one ext_vector pair, so complex adds are single
-// v_pk_add_f32 and complex products two packed ops, without the register shuffles the
-// compiler's SLP packing of struct float2 code produces.
 typedef float f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f2 tof2(float2 a) { return f2{a.x, a.y}; }
-__device__ __forceinline__ float2 fromf2(f2 a) { return make_float2(a.x, a.y); }
-
-// Raw buffer resources (SRSRC): 32-bit byte offsets and hardware range checking.  An offset at
-// or past num_records reads 0 / drops the store, so masked lanes need no branch or select.
+typedef double d2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-#define RSP_OOB 0x80000000u   // > any buffer this library makes (plans are validated < 2 GB/frame)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, unsigned bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ f2 buf_ld_f2(__amdgpu_buffer_rsrc_t r, unsigned off) {
-    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
-    return f2{__uint_as_float(v.x), __uint_as_float(v.y)};
-}
-#ifndef RSP_ST_AUX
-#define RSP_ST_AUX 0
-#endif
-template <int AUX = 0>
-__device__ __forceinline__ void buf_st_f2(__amdgpu_buffer_rsrc_t r, unsigned off, f2 x) {
-    __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(x.x), __float_as_uint(x.y)}, r, (int)off, 0, AUX);
-}
-__device__ __forceinline__ void buf_st_f1(__amdgpu_buffer_rsrc_t r, unsigned off, float x) {
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, (int)off, 0, 0);
-}
-// |x| with the hardware square root (v_sqrt_f32, 1 ulp) instead of the correctly rounded
-// sequence (~15 VALU): the magnitude map feeds threshold tests at fp32 noise level anyway
-__device__ __forceinline__ float fast_abs(f2 x) { return __builtin_amdgcn_sqrtf(x.x * x.x + x.y * x.y); }
+
+template <class T> struct CxT;
+template <> struct CxT<float> { typedef f2 V; };
+template <> struct CxT<double> { typedef d2 V; };
+template <class T> using cx = typename CxT<T>::V;   // complex of T
+template <class V> struct ScalT;
+template <> struct ScalT<f2> { typedef float S; };
+template <> struct ScalT<d2> { typedef double S; };
+template <class V> using scal = typename ScalT<V>::S;
+
+// ---- complex arithmetic ------------------------------------------------------------------
+// float: complex adds are single v_pk_add_f32 and products two packed ops; double: plain
+// v_fma_f64 (gfx950 has no packed f64 arithmetic).
 __device__ __forceinline__ f2 vmul(f2 a, f2 b) { return a.xx * b + a.yy * f2{-b.y, b.x}; }
+__device__ __forceinline__ d2 vmul(d2 a, d2 b) { return d2{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
 template <bool INV>
 __device__ __forceinline__ f2 vrot(f2 a) {   // * (-i) forward, * (+i) inverse
     return INV ? a.yx * f2{-1.f, 1.f} : a.yx * f2{1.f, -1.f};
 }
 template <bool INV>
-__device__ __forceinline__ f2 vtw(float c, float s) { return f2{c, INV ? s : -s}; }   // exp(-+ i theta)
+__device__ __forceinline__ d2 vrot(d2 a) {
+    return INV ? d2{-a.y, a.x} : d2{a.y, -a.x};
+}
+template <bool INV, class V>
+__device__ __forceinline__ V vtw(double c, double s) {   // exp(-+ i theta)
+    typedef scal<V> S;
+    return V{(S)c, (S)(INV ? s : -s)};
+}
+// |x| (fsf:184-185 abs): hardware square root for float (v_sqrt_f32, 1 ulp); the correctly
+// rounded square root for double
+__device__ __forceinline__ float cmag(f2 x) { return __builtin_amdgcn_sqrtf(x.x * x.x + x.y * x.y); }
+__device__ __forceinline__ double cmag(d2 x) { return __builtin_sqrt(x.x * x.x + x.y * x.y); }
+
+// Raw buffer resources (SRSRC): 32-bit byte offsets and hardware range checking.  An offset at
+// or past num_records reads 0 / drops the store, so masked lanes need no branch or select.
+#define RSP_OOB 0x80000000u   // > any buffer this library makes (plans are validated < 2 GB/frame)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+template <class V> __device__ V buf_ld(__amdgpu_buffer_rsrc_t r, unsigned off);
+template <> __device__ __forceinline__ f2 buf_ld<f2>(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+}
+template <> __device__ __forceinline__ d2 buf_ld<d2>(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, unsigned off, f2 x) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, x), r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, unsigned off, d2 x) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void buf_st1(__amdgpu_buffer_rsrc_t r, unsigned off, float x) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void buf_st1(__amdgpu_buffer_rsrc_t r, unsigned off, double x) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, x), r, (int)off, 0, 0);
+}
 
 // ---- radix-R DFT kernels in registers -------------------------------------------------
-template <int R, bool INV> struct Dft;
-template <bool INV> struct Dft<2, INV> {
-    static __device__ __forceinline__ void run(f2* a) {
-        const f2 t = a[0];
+template <int R, bool INV, class V> struct Dft;
+template <bool INV, class V> struct Dft<2, INV, V> {
+    static __device__ __forceinline__ void run(V* a) {
+        const V t = a[0];
         a[0] = t + a[1];
         a[1] = t - a[1];
     }
 };
-template <bool INV> struct Dft<4, INV> {
-    static __device__ __forceinline__ void run(f2* a) {
-        const f2 t0 = a[0] + a[2], t1 = a[0] - a[2];
-        const f2 t2 = a[1] + a[3], t3 = vrot<INV>(a[1] - a[3]);
+template <bool INV, class V> struct Dft<4, INV, V> {
+    static __device__ __forceinline__ void run(V* a) {
+        const V t0 = a[0] + a[2], t1 = a[0] - a[2];
+        const V t2 = a[1] + a[3], t3 = vrot<INV>(a[1] - a[3]);
         a[0] = t0 + t2;
         a[2] = t0 - t2;
         a[1] = t1 + t3;
         a[3] = t1 - t3;
     }
 };
-template <bool INV> struct Dft<8, INV> {
-    static __device__ __forceinline__ void run(f2* a) {
-        f2 e[4] = {a[0], a[2], a[4], a[6]};
-        f2 o[4] = {a[1], a[3], a[5], a[7]};
-        Dft<4, INV>::run(e);
-        Dft<4, INV>::run(o);
-        const float r = 0.70710678118654752f;
-        o[1] = vmul(o[1], vtw<INV>(r, r));
+template <bool INV, class V> struct Dft<8, INV, V> {
+    static __device__ __forceinline__ void run(V* a) {
+        V e[4] = {a[0], a[2], a[4], a[6]};
+        V o[4] = {a[1], a[3], a[5], a[7]};
+        Dft<4, INV, V>::run(e);
+        Dft<4, INV, V>::run(o);
+        constexpr double r = 0.70710678118654752440;
+        o[1] = vmul(o[1], vtw<INV, V>(r, r));
         o[2] = vrot<INV>(o[2]);
-        o[3] = vmul(o[3], vtw<INV>(-r, r));
+        o[3] = vmul(o[3], vtw<INV, V>(-r, r));
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             a[k] = e[k] + o[k];
@@ -103,66 +126,28 @@ template <bool INV> struct Dft<8, INV> {
         }
     }
 };
-template <bool INV> struct Dft<16, INV> {
-    static __device__ __forceinline__ void run(f2* a) {
-        f2 e[8], o[8];
+template <bool INV, class V> struct Dft<16, INV, V> {
+    static __device__ __forceinline__ void run(V* a) {
+        V e[8], o[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             e[k] = a[2 * k];
             o[k] = a[2 * k + 1];
         }
-        Dft<8, INV>::run(e);
-        Dft<8, INV>::run(o);
-        const float c1 = 0.92387953251128674f, s1 = 0.38268343236508977f, r = 0.70710678118654752f;
-        o[1] = vmul(o[1], vtw<INV>(c1, s1));
-        o[2] = vmul(o[2], vtw<INV>(r, r));
-        o[3] = vmul(o[3], vtw<INV>(s1, c1));
+        Dft<8, INV, V>::run(e);
+        Dft<8, INV, V>::run(o);
+        constexpr double c1 = 0.92387953251128675613, s1 = 0.38268343236508977173, r = 0.70710678118654752440;
+        o[1] = vmul(o[1], vtw<INV, V>(c1, s1));
+        o[2] = vmul(o[2], vtw<INV, V>(r, r));
+        o[3] = vmul(o[3], vtw<INV, V>(s1, c1));
         o[4] = vrot<INV>(o[4]);
-        o[5] = vmul(o[5], vtw<INV>(-s1, c1));
-        o[6] = vmul(o[6], vtw<INV>(-r, r));
-        o[7] = vmul(o[7], vtw<INV>(-c1, s1));
+        o[5] = vmul(o[5], vtw<INV, V>(-s1, c1));
+        o[6] = vmul(o[6], vtw<INV, V>(-r, r));
+        o[7] = vmul(o[7], vtw<INV, V>(-c1, s1));
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             a[k] = e[k] + o[k];
             a[k + 8] = e[k] - o[k];
-        }
-    }
-};
-
-template <bool INV> struct Dft<5, INV> {   // X1 = m1 + rot(n1), X4 = m1 - rot(n1), X2 = m2 + rot(n2), X3 = m2 - rot(n2)
-    static __device__ __forceinline__ void run(f2* a) {
-        const float c1 = 0.30901699437494742f, c2 = -0.80901699437494742f;   // cos(2 pi / 5), cos(4 pi / 5)
-        const float s1 = 0.95105651629515357f, s2 = 0.58778525229247313f;    // sin(2 pi / 5), sin(4 pi / 5)
-        const f2 t1 = a[1] + a[4], t2 = a[2] + a[3], t3 = a[1] - a[4], t4 = a[2] - a[3];
-        const f2 m1 = a[0] + c1 * t1 + c2 * t2, m2 = a[0] + c2 * t1 + c1 * t2;
-        const f2 n1 = vrot<INV>(s1 * t3 + s2 * t4), n2 = vrot<INV>(s2 * t3 - s1 * t4);
-        a[0] = a[0] + t1 + t2;
-        a[1] = m1 + n1;
-        a[4] = m1 - n1;
-        a[2] = m2 + n2;
-        a[3] = m2 - n2;
-    }
-};
-template <bool INV> struct Dft<10, INV> {   // 2 x 5 (even / odd halves, W_10^k on the odd)
-    static __device__ __forceinline__ void run(f2* a) {
-        f2 e[5], o[5];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            e[k] = a[2 * k];
-            o[k] = a[2 * k + 1];
-        }
-        Dft<5, INV>::run(e);
-        Dft<5, INV>::run(o);
-        const float c1 = 0.80901699437494742f, s1 = 0.58778525229247313f;   // W_10^1
-        const float c2 = 0.30901699437494742f, s2 = 0.95105651629515357f;   // W_10^2
-        o[1] = vmul(o[1], vtw<INV>(c1, s1));
-        o[2] = vmul(o[2], vtw<INV>(c2, s2));
-        o[3] = vmul(o[3], vtw<INV>(-c2, s2));
-        o[4] = vmul(o[4], vtw<INV>(-c1, s1));
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            a[k] = e[k] + o[k];
-            a[k + 5] = e[k] - o[k];
         }
     }
 };
@@ -177,39 +162,31 @@ __device__ __forceinline__ int lidx(int i) { return SH ? i + (i >> SH) : i; }
 // Store policies for the Stockham pass output.  put(idx, row, o, loff, x): idx = t * R + r for
 // butterfly t / element r of this thread (a constant after unrolling), row, natural position
 // o, and the padded LDS offset loff of (row, o).
+template <class V>
 struct StoreLds {
-    float2* buf;
-    __device__ __forceinline__ void put(int, int, int, int loff, f2 x) const { buf[loff] = fromf2(x); }
-};
-
-// Last forward pass of the overlap-save FFT: multiply by the block filter spectrum H (1/M
-// folded in), prefetched into registers at kernel start (h[t * R + r] for this thread's outputs).
-template <int NH>
-struct StoreLdsH {
-    float2* buf;
-    const f2 (&h)[NH];
-    __device__ __forceinline__ void put(int idx, int, int, int loff, f2 x) const { buf[loff] = fromf2(vmul(x, h[idx])); }
+    V* buf;
+    __device__ __forceinline__ void put(int, int, int, int loff, V x) const { buf[loff] = x; }
 };
 
 // Twiddles w[r] = W_{Ns R}^{k r}, r = 1..R-1, of one butterfly (conjugated for the inverse)
 // from this pass's table row k: CMP = false: full rows [k][r-1] (R-1 loads); CMP = true:
 // compact rows [k][i] = W^(k 2^i) (lgR loads), the other powers formed as products of at
 // most lgR - 1 of them.
-template <int R, bool INV, bool CMP>
-__device__ __forceinline__ void load_tw(const float2* twk, f2 (&w)[R]) {
+template <int R, bool INV, bool CMP, class V>
+__device__ __forceinline__ void load_tw(const V* twk, V (&w)[R]) {
     if constexpr (!CMP) {
 #pragma unroll
         for (int r = 1; r < R; ++r) {
-            const float2 t = twk[r - 1];
-            w[r] = f2{t.x, INV ? -t.y : t.y};
+            const V t = twk[r - 1];
+            w[r] = V{t.x, INV ? -t.y : t.y};
         }
     } else {
         constexpr int lgR = clog2(R - 1) + 1;   // bases W^(k 2^i), 2^i < R (= log2 R for powers of two)
-        f2 b[lgR];
+        V b[lgR];
 #pragma unroll
         for (int i = 0; i < lgR; ++i) {
-            const float2 t = twk[i];
-            b[i] = f2{t.x, INV ? -t.y : t.y};
+            const V t = twk[i];
+            b[i] = V{t.x, INV ? -t.y : t.y};
         }
 #pragma unroll
         for (int r = 1; r < R; ++r) {
@@ -261,8 +238,8 @@ constexpr int tw_total(int LG, bool rev = false, bool cmp = false) { return tw_p
 // With power-of-two nb, Ns and pads every 2^SH, lidx(j + r nb) = lidx(j) + r nb + ((r nb) >> SH)
 // and lidx(idxD + r Ns) = lidx(idxD) + r Ns + ((r Ns) >> SH): every LDS address of a butterfly
 // is a per-thread base plus a compile-time offset (ds_read/ds_write immediate offsets).
-template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP = false>
-__device__ __forceinline__ void sh_load(const float2* buf, int rs, int nrows, const float2* tw, f2 (&v)[NB][R]) {
+template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP = false, class V>
+__device__ __forceinline__ void sh_load(const V* buf, int rs, int nrows, const V* tw, V (&v)[NB][R]) {
     constexpr int lgR = clog2(R);
     constexpr int lgnb = LGL - lgR;
     constexpr int nb = 1 << lgnb;
@@ -274,12 +251,12 @@ __device__ __forceinline__ void sh_load(const float2* buf, int rs, int nrows, co
         if (beta < total) {
             const int row = beta >> lgnb, j = beta & (nb - 1);
             const int k = j & (Ns - 1);
-            const float2* src = buf + row * rs + lidx<SH>(j);
-            f2 w[R];
+            const V* src = buf + row * rs + lidx<SH>(j);
+            V w[R];
             if (LGNS > 0) load_tw<R, INV, CMP>(tw + k * tw_row(R, CMP), w);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                f2 x = tof2(src[r * nb + (SH ? (r * nb) >> SH : 0)]);
+                V x = src[r * nb + (SH ? (r * nb) >> SH : 0)];
                 if (r > 0 && LGNS > 0) x = vmul(x, w[r]);
                 v[t][r] = x;
             }
@@ -288,8 +265,8 @@ __device__ __forceinline__ void sh_load(const float2* buf, int rs, int nrows, co
 }
 
 // Radix-R DFT of the loaded butterflies and the Stockham store (through policy st).
-template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, class St>
-__device__ __forceinline__ void sh_store(f2 (&v)[NB][R], int rs, int nrows, const St& st) {
+template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, class V, class St>
+__device__ __forceinline__ void sh_store(V (&v)[NB][R], int rs, int nrows, const St& st) {
     constexpr int lgR = clog2(R);
     constexpr int lgnb = LGL - lgR;
     constexpr int nb = 1 << lgnb;
@@ -301,7 +278,7 @@ __device__ __forceinline__ void sh_store(f2 (&v)[NB][R], int rs, int nrows, cons
         if (beta < total) {
             const int row = beta >> lgnb, j = beta & (nb - 1);
             const int k = j & (Ns - 1);
-            Dft<R, INV>::run(v[t]);
+            Dft<R, INV, V>::run(v[t]);
             const int idxD = ((j >> LGNS) << (LGNS + lgR)) + k;
             const int wbase = row * rs + lidx<SH>(idxD);
 #pragma unroll
@@ -311,9 +288,9 @@ __device__ __forceinline__ void sh_store(f2 (&v)[NB][R], int rs, int nrows, cons
     }
 }
 
-template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP, class St>
-__device__ __forceinline__ void sh_pass(float2* buf, int rs, int nrows, const float2* tw, const St& st) {
-    f2 v[NB][R];
+template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP, class V, class St>
+__device__ __forceinline__ void sh_pass(V* buf, int rs, int nrows, const V* tw, const St& st) {
+    V v[NB][R];
     sh_load<R, INV, NB, SH, NTHR, LGL, LGNS, CMP>(buf, rs, nrows, tw, v);
     __syncthreads();
     sh_store<R, INV, NB, SH, NTHR, LGL, LGNS>(v, rs, nrows, st);
@@ -323,16 +300,15 @@ __device__ __forceinline__ void sh_pass(float2* buf, int rs, int nrows, const fl
 // Passes Q..QEND-1 of a 2^LG-point FFT (radix order reversed if REV) over `nrows` rows;
 // pass n_passes - 1 stores through `last`, the others through `mid`.  tw = this plan's
 // concatenated tables.  PTS = complex points per thread (nrows * L / NTHR).
-template <int LG, int Q, int QEND, int LGNS, int PTS, bool INV, bool REV, int SH, int NTHR, bool CMP, class StMid,
-          class StLast>
-__device__ __forceinline__ void fft_range(float2* buf, int rs, int nrows, const float2* tw, const StMid& mid,
-                                          const StLast& last) {
+template <int LG, int Q, int QEND, int LGNS, int PTS, bool INV, bool REV, int SH, int NTHR, bool CMP, class V,
+          class StMid, class StLast>
+__device__ __forceinline__ void fft_range(V* buf, int rs, int nrows, const V* tw, const StMid& mid, const StLast& last) {
     constexpr int NP = n_passes(LG);
     if constexpr (Q < QEND) {
         constexpr int RB = rad_bits_p(LG, Q, REV);
         constexpr int R = 1 << RB;
         constexpr int NB = (PTS + R - 1) / R;
-        const float2* twq = tw + tw_pass_off(LG, Q, REV, CMP);
+        const V* twq = tw + tw_pass_off(LG, Q, REV, CMP);
         if constexpr (Q == NP - 1)
             sh_pass<R, INV, NB, SH, NTHR, LG, LGNS, CMP>(buf, rs, nrows, twq, last);
         else
@@ -342,24 +318,16 @@ __device__ __forceinline__ void fft_range(float2* buf, int rs, int nrows, const 
 }
 
 // All passes of a 2^LG-point FFT over `nrows` rows; the last pass stores through `last`.
-template <int LG, int Q, int LGNS, int PTS, bool INV, int SH, int NTHR, class StMid, class StLast>
-__device__ __forceinline__ void fft_passes(float2* buf, int rs, int nrows, const float2* tw, const StMid& mid,
+template <int LG, int PTS, int SH, int NTHR, class V, class StMid, class StLast>
+__device__ __forceinline__ void fft_passes(V* buf, int rs, int nrows, const V* tw, const StMid& mid,
                                            const StLast& last) {
-    fft_range<LG, Q, n_passes(LG), LGNS, PTS, INV, false, SH, NTHR, false>(buf, rs, nrows, tw, mid, last);
+    fft_range<LG, 0, n_passes(LG), 0, PTS, false, false, SH, NTHR, false>(buf, rs, nrows, tw, mid, last);
 }
 
 __device__ __forceinline__ int ilog2(int x) { return 31 - __clz(x); }
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// Diagnostic phase stamps (only when FramePtrs::trace is set: rsp_profile_stages with
-// RSP_TRACE_FILE).  Stamp i of the linear workgroup id; 100 MHz constant clock.
-__device__ __forceinline__ void trace_stamp(const FramePtrs& fp, int i) {
-    if (fp.trace && threadIdx.x == 0) {
-        const size_t wg = blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z);
-        fp.trace[wg * 4 + i] = __builtin_amdgcn_s_memrealtime();
-    }
-}
+// One dynamic LDS allocation shared by every kernel of this file (each casts it to its types).
+extern __shared__ __attribute__((aligned(16))) unsigned char rsp_lds[];
 
 // Compacted used-sample index n' -> fast-time sample (Geometry::ivl_*).  Constant indices
 // only: a per-lane index into the kernel-argument arrays would become a vector load, and its
@@ -384,166 +352,175 @@ __device__ __forceinline__ size_t zaddr(const Geometry& g, int b, int v, int np)
 // ======================================================================================
 // K1: DBF + MTD window + slow-time FFT + fftshift -> compacted rows
 // ======================================================================================
-#ifndef K1_THREADS
 #define K1_THREADS 512
-#endif
 #define K1_SH 4   // LDS pad shift of the slow-time FFT rows (row stride P + P/16)
+
+// DBF (fsf:93-97) on the matrix cores as a real GEMM: D[16 rows x 16 pulses] += A[16 x 4
+// channels] * B[4 channels x 16 pulses], rows = (Re, Im) x 8 beams of conj(W), one MFMA per
+// (channel group, Re/Im part of x).  A lane's 16-B load is its B operand:
+//  - float: v_mfma_f32_16x16x4f32; the load holds pulses (p, p+1) of one channel (re, im, re,
+//    im), the B operand of two column blocks (even / odd pulses); D row 4*(lane>>4) + i.
+//  - double: v_mfma_f64_16x16x4f64; the load holds one pulse (re, im); D row (lane>>4) + 4*i
+//    (the f64 C/D layout, cdna_hip_programming.md section 3).
+template <class T> struct Dbf;
+template <> struct Dbf<float> {
+    static constexpr int PPL = 2, NACC = 2;
+    typedef f32x4 Ld;
+    typedef f32x4 Acc;
+    static __device__ __forceinline__ Ld bits(u32x4 t) { return __builtin_bit_cast(f32x4, t); }
+    static __device__ __forceinline__ void mma(Acc (&acc)[NACC], float are, float aim, Ld x) {
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(are, x.x, acc[0], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(aim, x.y, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(are, x.z, acc[1], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(aim, x.w, acc[1], 0, 0, 0);
+    }
+    static __device__ __forceinline__ int row(int grp, int i) { return 4 * grp + i; }
+};
+template <> struct Dbf<double> {
+    static constexpr int PPL = 1, NACC = 1;
+    typedef d2 Ld;
+    typedef f64x4 Acc;
+    static __device__ __forceinline__ Ld bits(u32x4 t) { return __builtin_bit_cast(d2, t); }
+    static __device__ __forceinline__ void mma(Acc (&acc)[NACC], double are, double aim, Ld x) {
+        acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(are, x.x, acc[0], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(aim, x.y, acc[0], 0, 0, 0);
+    }
+    static __device__ __forceinline__ int row(int grp, int i) { return grp + 4 * i; }
+};
+
+// D of one sub-tile (sample nl, pulses p .. p + PPL*... of this lane) x window -> padded LDS
+// columns [b * NT + nl][Ppad] (Re / Im parts as two scalar stores).
+template <class T, int MB>
+__device__ __forceinline__ void dbf_store(T* Yf, const typename Dbf<T>::Acc (&acc)[MB][Dbf<T>::NACC], int grp, int B,
+                                          int NT, int Ppad, int nl, int p, const T (&w)[Dbf<T>::NACC], int sh) {
+#pragma unroll
+    for (int a = 0; a < Dbf<T>::NACC; ++a) {
+        const int pa = p + a;
+        const int ip = sh ? pa + (pa >> K1_SH) : pa;
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {   // D row m: beam mb*8 + (m & 7), part m >> 3
+                const int m = Dbf<T>::row(grp, i);
+                const int b = mb * 8 + (m & 7);
+                if (b < B) Yf[2 * ((b * NT + nl) * Ppad + ip) + (m >> 3)] = acc[mb][a][i] * w[a];
+            }
+    }
+}
 
 // Last slow-time FFT pass straight from registers to z with fftshift (fsf:135): column
 // row = b NT + nl, frequency o -> Doppler cell v = (o + P/2) mod P.  16 lanes of a butterfly
 // group write consecutive v of one column (64 B apart) and the next 16 lanes the neighbouring
-// column (+8 B), so the lines fill within the workgroup.
+// column, so the lines fill within the workgroup.
+template <class V>
 struct StoreZ {
     __amdgpu_buffer_rsrc_t z; int lgNT, ntiles, tile, P, half;
-    __device__ __forceinline__ void put(int, int row, int o, int, f2 x) const {
+    __device__ __forceinline__ void put(int, int row, int o, int, V x) const {
         const int b = row >> lgNT, nl = row & ((1 << lgNT) - 1);
         const int v = (o + half) & (P - 1);
-        buf_st_f2<RSP_ST_AUX>(z, (unsigned)(((((b * ntiles + tile) * P + v) << lgNT) + nl)) * 8u, x);
+        buf_st(z, (unsigned)(((((b * ntiles + tile) * P + v) << lgNT) + nl)) * (unsigned)sizeof(V), x);
     }
 };
 
 // Slow-time FFT of every (beam, sample) column in LDS for the runtime log2(P); the last pass
 // stores through `last`.
-template <class StLast>
-__device__ __forceinline__ void k1_fft(int lgp, float2* Y, int Ppad, int ncols, const float2* twl, const StLast& last) {
-    StoreLds st{Y};
+template <class V, class StLast>
+__device__ __forceinline__ void k1_fft(int lgp, V* Y, int Ppad, int ncols, const V* twl, const StLast& last) {
+    StoreLds<V> st{Y};
     switch (lgp) {
-        case 4: fft_passes<4, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
-        case 5: fft_passes<5, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
-        case 6: fft_passes<6, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
-        case 7: fft_passes<7, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
-        case 8: fft_passes<8, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
-        default: fft_passes<9, 0, 0, 16, false, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
+        case 4: fft_passes<4, 16, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
+        case 5: fft_passes<5, 16, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
+        case 6: fft_passes<6, 16, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
+        case 7: fft_passes<7, 16, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
+        case 8: fft_passes<8, 16, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
+        default: fft_passes<9, 16, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
     }
 }
 
-// BMAX = beams rounded up (4/8/16), CP = channels rounded up (8/16/32).  Weights are conj(W)
-// laid out [CP][BMAX] in LDS, zero for padded beams/channels, so the DBF has no data-dependent
-// branches: CP unconditional 8-B loads per (sample, pulse) all in flight together, then
-// BMAX*CP complex FMAs whose weights are LDS broadcast reads.
-template <int BMAX, int CP>
+// BMAX = beams rounded up (4/8/16), CP = channels rounded up (8/16/32).  conj(W) enters as the
+// per-lane MFMA A operands (Atab, zero for padded beams/channels), so the DBF has no
+// data-dependent branches.  mode 3 = DBF + MTD; mode 0 = transpose only (stage-2 path: the
+// input channels are the beams).  Non-power-of-two P takes a direct DFT (O(P^2) per column).
+template <class T, int BMAX, int CP>
 __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConsts k, FramePtrs fp, int mode) {
-    extern __shared__ __attribute__((aligned(16))) float2 Y[];   // [B][NT][Ppad] | twiddles | W
+    typedef cx<T> V;
+    typedef Dbf<T> D;
+    V* Y = reinterpret_cast<V*>(rsp_lds);   // [B][NT][Ppad] | twiddles
     const int f = blockIdx.y, tile = blockIdx.x;
     const int B = g.B, C = g.C, P = g.P, NT = g.NT, Ppad = g.Ppad;
-    trace_stamp(fp, 0);
     if (tile == 0 && threadIdx.x == 0 && fp.count[f]) *fp.count[f] = 0;   // K3's detection counter
-    float2* twl = Y + B * NT * Ppad;
+    V* twl = Y + B * NT * Ppad;
     const bool fft = (mode & 2) && g.pow2P;
     const int sh = fft ? K1_SH : 0;
+    const V* __restrict__ twPp = static_cast<const V*>(k.twPp);
+    const T* __restrict__ win = static_cast<const T*>(k.win);
     // twiddles: global loads issued first, LDS stores after the cube loads are in flight (the
     // barrier before the FFT orders them), so no load waits behind a barrier at kernel start
     constexpr int TWPRE = 2;
-    float2 twv[TWPRE];
+    V twv[TWPRE];
 #pragma unroll
     for (int u = 0; u < TWPRE; ++u) {
         const int i = threadIdx.x + u * K1_THREADS;
-        if (fft && i < g.twPp_elems) twv[u] = k.twPp[i];
+        if (fft && i < g.twPp_elems) twv[u] = twPp[i];
     }
-    const float2* __restrict__ x = fp.in[f];
+    const V* __restrict__ x = static_cast<const V*>(fp.in[f]);
     const size_t NP = (size_t)g.cpitch;   // channel stride
     if (mode & 1) {
-        // ---- Phase A (MFMA): DBF (fsf:93-97) + MTD window (fsf:134) as a real GEMM on the
-        // f32 matrix cores: D[16 x 16 pulses] += A[16 x 4 channels] * B[4 channels x 16 pulses],
-        // rows = (Re, Im) x 8 beams, one MFMA per (channel group, Re/Im part, even/odd pulses).
-        // Each lane loads 16 B = pulses (p, p+1) of one channel: B operand of two column blocks.
         constexpr int NJ = CP / 4, MB = BMAX <= 8 ? 1 : 2, TPW = (16 / NJ) / MB > 0 ? (16 / NJ) / MB : 1;
+        constexpr int PT = 16 * D::PPL;   // pulses per sub-tile
         const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, grp = lane >> 4, col = lane & 15;
-        float are[MB][NJ], aim[MB][NJ];   // this lane's A operand: row lane&15, channel 4j + lane>>4
+        const T* At = static_cast<const T*>(k.Atab);
+        T are[MB][NJ], aim[MB][NJ];   // this lane's A operand: row lane&15, channel 4j + lane>>4
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
-                are[mb][j] = k.Atab[((mb * NJ + j) * 2 + 0) * 64 + lane];
-                aim[mb][j] = k.Atab[((mb * NJ + j) * 2 + 1) * 64 + lane];
+                are[mb][j] = At[((mb * NJ + j) * 2 + 0) * 64 + lane];
+                aim[mb][j] = At[((mb * NJ + j) * 2 + 1) * 64 + lane];
             }
-        const int ptiles = (P + 31) >> 5;
+        const int ptiles = (P + PT - 1) / PT;
         const int ntp = NT * ptiles;
-        float* Yf = reinterpret_cast<float*>(Y);
-        float sink = 0.f;
-        // a wave takes TPW consecutive tiles (pulse tiles of the same sample first), so the
-        // 1 KB pulse row of each (channel, sample) is fetched by one wave in one burst
+        T* Yf = reinterpret_cast<T*>(Y);
+        // a wave takes TPW consecutive sub-tiles (pulse tiles of the same sample first), so the
+        // pulse row of each (channel, sample) is fetched by one wave in one burst
         for (int t0 = wv * TPW; t0 < ntp; t0 += (K1_THREADS / 64) * TPW) {
-            float4 xv[TPW][NJ];
+            typename D::Ld xv[TPW][NJ];
             int nlv[TPW], pv[TPW];
 #pragma unroll
-            for (int u = 0; u < TPW; ++u) {      // every load of TPW tiles in flight together
+            for (int u = 0; u < TPW; ++u) {      // every load of TPW sub-tiles in flight together
                 const int t = t0 + u;
                 const int nl = t / ptiles;
-                const int p = ((t - nl * ptiles) << 5) + 2 * col;
+                const int p = (t - nl * ptiles) * PT + D::PPL * col;
                 const int np = tile * NT + nl;
                 int n = -1;
-                if (t < ntp && np < g.nU && p < P) {
-                    n = used_sample(g, np);
-                }
+                if (t < ntp && np < g.nU && p < P) n = used_sample(g, np);
                 nlv[u] = t < ntp ? nl : -1;
                 pv[u] = p;
-                if (g.dbg & 32) {   // ablation: same bytes, 1 KB-contiguous wave loads (timing only)
 #pragma unroll
-                    for (int j = 0; j < NJ; ++j) {
-                        const int c = min(4 * j + (u & 3), C - 1);
-                        const int pp = (2 * lane) % P;
-                        xv[u][j] = n >= 0 ? *reinterpret_cast<const float4*>(x + (size_t)c * NP + (size_t)n * P + pp)
-                                          : make_float4(0.f, 0.f, 0.f, 0.f);
-                    }
-                } else {
-#pragma unroll
-                    for (int j = 0; j < NJ; ++j) {
-                        const int c = min(4 * j + grp, C - 1);   // padded channels carry zero weights
-                        xv[u][j] = n >= 0 ? *reinterpret_cast<const float4*>(x + (size_t)c * NP + (size_t)n * P + p)
-                                          : make_float4(0.f, 0.f, 0.f, 0.f);
-                    }
+                for (int j = 0; j < NJ; ++j) {
+                    const int c = min(4 * j + grp, C - 1);   // padded channels carry zero weights
+                    xv[u][j] = n >= 0 ? D::bits(*reinterpret_cast<const u32x4*>(x + (size_t)c * NP + (size_t)n * P + p))
+                                      : typename D::Ld{};
                 }
-            }
-            if (g.dbg & 128) {   // ablation (timing only): the cube loads alone, nothing computed
-#pragma unroll
-                for (int u = 0; u < TPW; ++u)
-#pragma unroll
-                    for (int j = 0; j < NJ; ++j) sink += xv[u][j].x + xv[u][j].y + xv[u][j].z + xv[u][j].w;
-                continue;
             }
 #pragma unroll
             for (int u = 0; u < TPW; ++u) {
                 if (nlv[u] < 0) continue;
-                f32x4 acc[MB][2];
+                typename D::Acc acc[MB][D::NACC];
 #pragma unroll
                 for (int mb = 0; mb < MB; ++mb) {
-                    acc[mb][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-                    acc[mb][1] = acc[mb][0];
 #pragma unroll
-                    for (int j = 0; j < NJ; ++j) {
-                        acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(are[mb][j], xv[u][j].x, acc[mb][0], 0, 0, 0);
-                        acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(aim[mb][j], xv[u][j].y, acc[mb][0], 0, 0, 0);
-                        acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(are[mb][j], xv[u][j].z, acc[mb][1], 0, 0, 0);
-                        acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(aim[mb][j], xv[u][j].w, acc[mb][1], 0, 0, 0);
-                    }
+                    for (int a = 0; a < D::NACC; ++a) acc[mb][a] = typename D::Acc{};
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) D::mma(acc[mb], are[mb][j], aim[mb][j], xv[u][j]);
                 }
                 const int p = pv[u];
                 if (p >= P) continue;
-                float w0 = 1.f, w1 = 1.f;
-                if (mode & 2) {
-                    const float2 w01 = *reinterpret_cast<const float2*>(k.win + p);
-                    w0 = w01.x;
-                    w1 = w01.y;
-                }
-                const int i0 = sh ? p + (p >> K1_SH) : p, i1 = sh ? (p + 1) + ((p + 1) >> K1_SH) : p + 1;
+                T w[D::NACC];
 #pragma unroll
-                for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {   // D row m = 4*grp + i: beam mb*8 + (m & 7), part m >> 3
-                        const int m = 4 * grp + i;
-                        const int b = mb * 8 + (m & 7);
-                        if (b < B && !(g.dbg & 1024)) {   // RSP_ABLATE=1024 skips the LDS writes
-                            float* colp = Yf + 2 * (b * NT + nlv[u]) * Ppad + (m >> 3);
-                            colp[2 * i0] = acc[mb][0][i] * w0;
-                            colp[2 * i1] = acc[mb][1][i] * w1;
-                        }
-                    }
+                for (int a = 0; a < D::NACC; ++a) w[a] = (mode & 2) ? win[p + a] : (T)1;
+                dbf_store<T, MB>(Yf, acc, grp, B, NT, Ppad, nlv[u], p, w, sh);
             }
-        }
-        if (g.dbg & 128) {
-            if (sink == 1.2345e-30f) fp.z[f][threadIdx.x] = make_float2(sink, 0.f);   // keeps the loads
-            return;
         }
     } else {
         // ---- transpose only (stage-2 path: input channels are the beams)
@@ -552,18 +529,13 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
             const int nl = it / P, p = it - nl * P;
             const int np = tile * NT + nl;
             int n = -1;
-            if (np < g.nU) {
-                n = used_sample(g, np);
-            }
+            if (np < g.nU) n = used_sample(g, np);
             const int ip = sh ? p + (p >> K1_SH) : p;
 #pragma unroll
             for (int b = 0; b < BMAX; ++b) {
                 if (b < B) {
-                    float2 val = n >= 0 ? x[(size_t)b * NP + (size_t)n * P + p] : make_float2(0.f, 0.f);
-                    if (mode & 2) {
-                        val.x *= k.win[p];
-                        val.y *= k.win[p];
-                    }
+                    V val = n >= 0 ? x[(size_t)b * NP + (size_t)n * P + p] : V{};
+                    if (mode & 2) val *= win[p];
                     Y[(b * NT + nl) * Ppad + ip] = val;
                 }
             }
@@ -575,11 +547,10 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
             const int i = threadIdx.x + u * K1_THREADS;
             if (i < g.twPp_elems) twl[i] = twv[u];
         }
-        for (int i = threadIdx.x + TWPRE * K1_THREADS; i < g.twPp_elems; i += K1_THREADS) twl[i] = k.twPp[i];
+        for (int i = threadIdx.x + TWPRE * K1_THREADS; i < g.twPp_elems; i += K1_THREADS) twl[i] = twPp[i];
     }
     __syncthreads();
-    trace_stamp(fp, 1);
-    float2* __restrict__ z = fp.z[f];
+    V* __restrict__ z = static_cast<V*>(fp.z[f]);
     const int zslab = P * NT;   // contiguous [P][NT] slab per (b, tile)
     const int lgNT = ilog2(NT);
     if (!(mode & 2)) {
@@ -592,24 +563,23 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
     }
     const int half = P >> 1;
     if (fft) {
-        // ---- Phase B + C: P-point FFT of every (b, nl) column (fsf:135); the last pass applies
-        // fftshift and stores the [P][NT] slabs from registers
-        const StoreZ sz{buf_rsrc(z, (unsigned)B * g.ntiles * zslab * 8u), lgNT, g.ntiles, tile, P, half};
-        if (!(g.dbg & 2)) k1_fft(g.logP, Y, Ppad, B * NT, twl, sz);   // RSP_ABLATE=2: no FFT, no store
-        trace_stamp(fp, 2);
-        if (fp.trace) trace_stamp(fp, 3);
+        // ---- P-point FFT of every (b, nl) column (fsf:135); the last pass applies fftshift
+        // and stores the [P][NT] slabs from registers
+        const StoreZ<V> sz{buf_rsrc(z, (unsigned)(B * g.ntiles * zslab * sizeof(V))), lgNT, g.ntiles, tile, P, half};
+        k1_fft(g.logP, Y, Ppad, B * NT, twl, sz);
     } else {
         // non power-of-two P: direct DFT straight to global (O(P^2) per column)
+        const V* __restrict__ twP = static_cast<const V*>(k.twP);
         for (int e = threadIdx.x; e < B * zslab; e += K1_THREADS) {
             const int b = e / zslab, rem = e - b * zslab;
             const int v = rem >> lgNT, nl = rem & (NT - 1);
             int kk = v - half;
             if (kk < 0) kk += P;
-            const float2* col = Y + (b * NT + nl) * Ppad;
-            float2 acc = make_float2(0.f, 0.f);
+            const V* colv = Y + (b * NT + nl) * Ppad;
+            V acc = V{};
             int idx = 0;
             for (int p = 0; p < P; ++p) {
-                acc = cadd(acc, cmul(col[p], k.twP[idx]));
+                acc += vmul(colv[p], twP[idx]);
                 idx += kk;
                 if (idx >= P) idx -= P;
             }
@@ -618,360 +588,163 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
     }
 }
 
+// Points per thread of the persistent K1's slow-time FFT (B * NT * P <= K1_PTS * K1_THREADS):
+// the plan halves NT for double so that two tile buffers still fit the 160 KB of LDS.
+template <class T> constexpr int k1p_pts() { return sizeof(T) == 4 ? 16 : 8; }
+
 // K1, persistent and software-pipelined (the default for power-of-two P when one load round
 // covers a tile): one workgroup per CU walks the (frame, tile) list with two LDS tile buffers.
-// While tile T's slow-time FFT runs out of one buffer and its last pass streams z to HBM, the
+// While tile TT's slow-time FFT runs out of one buffer and its last pass streams z to HBM, the
 // cube loads of the workgroup's next tile are already in flight in registers; the DBF of that
 // tile then fills the other buffer.  HBM reads and writes overlap instead of alternating
 // round by round.  Same arithmetic as k1_dbf_mtd (mode 3).
-template <int BMAX, int CP, int LGP>
+template <class T, int BMAX, int CP, int LGP>
 __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevConsts k, FramePtrs fp, int nf) {
-    extern __shared__ __attribute__((aligned(16))) float2 Y[];   // tile [B][NT][Ppad] (x2 if nbuf = 2) | twiddles
+    typedef cx<T> V;
+    typedef Dbf<T> D;
+    V* Y = reinterpret_cast<V*>(rsp_lds);   // tile [B][NT][Ppad] x 2 | twiddles
     const int B = g.B, C = g.C, P = g.P, NT = g.NT, Ppad = g.Ppad;
-    const int nbuf = (g.dbg & 8192) ? 1 : 2;   // RSP_ABLATE=8192: one buffer (measured slower: 20.7k vs 21.2k frames/s)
     const int bufsz = B * NT * Ppad;
-    float2* twl = Y + nbuf * bufsz;
+    V* twl = Y + 2 * bufsz;
     const int total = nf * g.ntiles;
-    int T = blockIdx.x;
-    if (T >= total) return;
-    for (int i = threadIdx.x; i < g.twPp_elems; i += K1_THREADS) twl[i] = k.twPp[i];
+    int TT = blockIdx.x;
+    if (TT >= total) return;
+    const V* __restrict__ twPp = static_cast<const V*>(k.twPp);
+    for (int i = threadIdx.x; i < g.twPp_elems; i += K1_THREADS) twl[i] = twPp[i];
     constexpr int NJ = CP / 4, MB = BMAX <= 8 ? 1 : 2, TPW = (16 / NJ) / MB > 0 ? (16 / NJ) / MB : 1;
+    constexpr int PT = 16 * D::PPL;
     const int lane = threadIdx.x & 63, grp = lane >> 4, col = lane & 15;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: nlv[] and n are scalar
-    float are[MB][NJ], aim[MB][NJ];
+    const T* At = static_cast<const T*>(k.Atab);
+    T are[MB][NJ], aim[MB][NJ];
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-            are[mb][j] = k.Atab[((mb * NJ + j) * 2 + 0) * 64 + lane];
-            aim[mb][j] = k.Atab[((mb * NJ + j) * 2 + 1) * 64 + lane];
+            are[mb][j] = At[((mb * NJ + j) * 2 + 0) * 64 + lane];
+            aim[mb][j] = At[((mb * NJ + j) * 2 + 1) * 64 + lane];
         }
-    // this lane's sub-tiles are the same for every tile: (sample nl, pulses p, p + 1) and their
-    // window values (launch_k1 guarantees one round: NT * ptiles <= waves * TPW)
-    const int ptiles = (P + 31) >> 5, ntp = NT * ptiles;
+    // this lane's sub-tiles are the same for every tile: (sample nl, pulses p ..) and their
+    // window values (k1_persistent_fits guarantees one round: NT * ptiles <= waves * TPW)
+    const int ptiles = P / PT, ntp = NT * ptiles;
+    const T* __restrict__ win = static_cast<const T*>(k.win);
     int nlv[TPW], pv[TPW];
-    float w0v[TPW], w1v[TPW];
+    T wv_[TPW][D::NACC];
 #pragma unroll
     for (int u = 0; u < TPW; ++u) {
         const int t = wv * TPW + u;
         const int nl = t / ptiles;
-        pv[u] = ((t - nl * ptiles) << 5) + 2 * col;
+        pv[u] = (t - nl * ptiles) * PT + D::PPL * col;
         nlv[u] = t < ntp ? nl : -1;   // pv < P: P >= 64 here; wave-uniform
-        const float2 w01 = nlv[u] >= 0 ? *reinterpret_cast<const float2*>(k.win + pv[u]) : make_float2(0.f, 0.f);
-        w0v[u] = w01.x;
-        w1v[u] = w01.y;
+#pragma unroll
+        for (int a = 0; a < D::NACC; ++a) wv_[u][a] = nlv[u] >= 0 ? win[pv[u] + a] : (T)0;
     }
     const size_t NPc = (size_t)g.cpitch;
-    // per-lane byte offsets of this lane's (channel, pulse pair) inside a cube: loop-invariant,
+    // per-lane byte offsets of this lane's (channel, pulses) inside a cube: loop-invariant,
     // so a tile's load issue is scalar sample offsets + buffer loads and writes no VGPR but xv
     // (a VGPR temporary there could be a pending z store's data register: WAR = vmcnt wait)
     unsigned loff[TPW][NJ];
 #pragma unroll
     for (int u = 0; u < TPW; ++u)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) loff[u][j] = (unsigned)(((size_t)min(4 * j + grp, C - 1) * NPc + pv[u]) * 8u);
-    const unsigned cube_bytes = (unsigned)((size_t)C * NPc * 8u);
-    float4 xv[TPW][NJ];
+        for (int j = 0; j < NJ; ++j)
+            loff[u][j] = (unsigned)(((size_t)min(4 * j + grp, C - 1) * NPc + pv[u]) * sizeof(V));
+    const unsigned cube_bytes = (unsigned)((size_t)C * NPc * sizeof(V));
+    typename D::Ld xv[TPW][NJ];
     bool vld[TPW];   // wave-uniform: sub-tile u of the tile in flight lies inside the used samples
-    auto issue = [&](int TT) {   // cube loads of tile TT (fsf:93 operands) into xv
-        const int f = __builtin_amdgcn_readfirstlane(TT / g.ntiles), tile = TT - f * g.ntiles;
+    auto issue = [&](int Tn) {   // cube loads of tile Tn (fsf:93 operands) into xv
+        const int f = __builtin_amdgcn_readfirstlane(Tn / g.ntiles), tile = Tn - f * g.ntiles;
         const __amdgpu_buffer_rsrc_t xr = buf_rsrc(fp.in[f], cube_bytes);
 #pragma unroll
         for (int u = 0; u < TPW; ++u) {
             const int np = tile * NT + nlv[u];
             vld[u] = nlv[u] >= 0 && np < g.nU;
             if (vld[u]) {   // no else: zeroing xv here would wait (vmcnt) on the pending z stores
-                const int soff = used_sample(g, np) * P * 8;
+                const int soff = used_sample(g, np) * P * (int)sizeof(V);
 #pragma unroll
-                for (int j = 0; j < NJ; ++j) {   // non-temporal: the cube is read exactly once
-                    const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(xr, (int)loff[u][j], soff, 2);
-                    xv[u][j] = make_float4(__uint_as_float(t.x), __uint_as_float(t.y), __uint_as_float(t.z),
-                                           __uint_as_float(t.w));
-                }
+                for (int j = 0; j < NJ; ++j)   // non-temporal: the cube is read exactly once
+                    xv[u][j] = D::bits(__builtin_amdgcn_raw_buffer_load_b128(xr, (int)loff[u][j], soff, 2));
             }
         }
     };
-    auto dbf = [&](float2* buf) {   // MFMA DBF + window of xv into buf (padded rows, K1_SH)
-        float* Yf = reinterpret_cast<float*>(buf);
+    auto dbf = [&](V* buf) {   // MFMA DBF + window of xv into buf (padded rows, K1_SH)
+        T* Yf = reinterpret_cast<T*>(buf);
 #pragma unroll
         for (int u = 0; u < TPW; ++u) {
             if (nlv[u] < 0) continue;
-            if (!vld[u]) {   // samples past the used ones: zero columns, like k1_dbf_mtd's n = -1
-                const int p = pv[u];
-                const int i0 = p + (p >> K1_SH), i1 = (p + 1) + ((p + 1) >> K1_SH);
-#pragma unroll
-                for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int m = 4 * grp + i, b = mb * 8 + (m & 7);
-                        if (b < B) {
-                            float* colp = Yf + 2 * (b * NT + nlv[u]) * Ppad + (m >> 3);
-                            colp[2 * i0] = 0.f;
-                            colp[2 * i1] = 0.f;
-                        }
-                    }
-                continue;
-            }
-            f32x4 acc[MB][2];
-#pragma unroll
-            for (int mb = 0; mb < MB; ++mb) {
-                acc[mb][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-                acc[mb][1] = acc[mb][0];
-#pragma unroll
-                for (int j = 0; j < NJ; ++j) {
-                    acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(are[mb][j], xv[u][j].x, acc[mb][0], 0, 0, 0);
-                    acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(aim[mb][j], xv[u][j].y, acc[mb][0], 0, 0, 0);
-                    acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(are[mb][j], xv[u][j].z, acc[mb][1], 0, 0, 0);
-                    acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(aim[mb][j], xv[u][j].w, acc[mb][1], 0, 0, 0);
-                }
-            }
-            const int p = pv[u];
-            const int i0 = p + (p >> K1_SH), i1 = (p + 1) + ((p + 1) >> K1_SH);
+            typename D::Acc acc[MB][D::NACC];
 #pragma unroll
             for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int m = 4 * grp + i;
-                    const int b = mb * 8 + (m & 7);
-                    if (b < B) {
-                        float* colp = Yf + 2 * (b * NT + nlv[u]) * Ppad + (m >> 3);
-                        colp[2 * i0] = acc[mb][0][i] * w0v[u];
-                        colp[2 * i1] = acc[mb][1][i] * w1v[u];
-                    }
-                }
+                for (int a = 0; a < D::NACC; ++a) acc[mb][a] = typename D::Acc{};
+            if (vld[u]) {   // samples past the used ones: zero columns, like k1_dbf_mtd's n = -1
+#pragma unroll
+                for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) D::mma(acc[mb], are[mb][j], aim[mb][j], xv[u][j]);
+            }
+            dbf_store<T, MB>(Yf, acc, grp, B, NT, Ppad, nlv[u], pv[u], wv_[u], K1_SH);
         }
     };
     const int zslab = P * NT, lgNT = ilog2(NT), half = P >> 1;
-    // diagnostic (RSP_TRACE_FILE): stamp 0 = start, 1 / 2 = summed FFT+store / DBF phase ticks
-    // (not timestamps), 3 = end; thread 0, after the barriers that close each phase
-    const bool tr = fp.trace != nullptr && threadIdx.x == 0;
-    unsigned long long t0 = tr ? __builtin_amdgcn_s_memrealtime() : 0, tfft = 0, tdbf = 0, tiss = 0;
-    issue(T);
+    issue(TT);
     dbf(Y);
     __syncthreads();
-    const unsigned long long tpro = tr ? __builtin_amdgcn_s_memrealtime() : 0;
     int cur = 0;
-    for (; T < total; T += gridDim.x) {
-        const int Tn = T + gridDim.x;
-        const unsigned long long ti = tr ? __builtin_amdgcn_s_memrealtime() : 0;
+    for (; TT < total; TT += gridDim.x) {
+        const int Tn = TT + gridDim.x;
         if (Tn < total) issue(Tn);   // next tile's loads fly during this tile's FFT + z stores
-        if (tr) tiss += __builtin_amdgcn_s_memrealtime() - ti;
-        const int f = __builtin_amdgcn_readfirstlane(T / g.ntiles), tile = T - f * g.ntiles;
+        const int f = __builtin_amdgcn_readfirstlane(TT / g.ntiles), tile = TT - f * g.ntiles;
         if (tile == 0 && threadIdx.x == 0 && fp.count[f]) *fp.count[f] = 0;   // K3's detection counter
-        float2* __restrict__ z = fp.z[f];
-        const StoreZ sz{buf_rsrc(z, (unsigned)B * g.ntiles * zslab * 8u), lgNT, g.ntiles, tile, P, half};
-        const unsigned long long ta = tr ? __builtin_amdgcn_s_memrealtime() : 0;
-        fft_passes<LGP, 0, 0, 16, false, K1_SH, K1_THREADS>(Y + cur * bufsz, Ppad, B * NT, twl,
-                                                           StoreLds{Y + cur * bufsz}, sz);   // ends with a barrier
-        const unsigned long long tb = tr ? __builtin_amdgcn_s_memrealtime() : 0;
-        if (Tn < total) dbf(Y + (nbuf == 2 ? (cur ^ 1) : 0) * bufsz);
+        V* __restrict__ z = static_cast<V*>(fp.z[f]);
+        const StoreZ<V> sz{buf_rsrc(z, (unsigned)(B * g.ntiles * zslab * sizeof(V))), lgNT, g.ntiles, tile, P, half};
+        fft_passes<LGP, k1p_pts<T>(), K1_SH, K1_THREADS>(Y + cur * bufsz, Ppad, B * NT, twl,
+                                                          StoreLds<V>{Y + cur * bufsz}, sz);   // ends with a barrier
+        if (Tn < total) dbf(Y + (cur ^ 1) * bufsz);
         __syncthreads();
-        if (tr) {
-            tfft += tb - ta;
-            tdbf += __builtin_amdgcn_s_memrealtime() - tb;
-        }
-        if (nbuf == 2) cur ^= 1;
-    }
-    if (tr) {
-        unsigned long long* o = fp.trace + (size_t)blockIdx.x * 4;
-        o[0] = t0;
-        o[1] = (g.dbg & 16384) ? tpro - t0 : (g.dbg & 32768) ? tiss : tfft;   // 16384 / 32768: prologue / issue ticks
-        o[2] = tdbf;
-        o[3] = __builtin_amdgcn_s_memrealtime();
+        cur ^= 1;
     }
 }
 
 // ======================================================================================
 // K2: pulse compression of every row (fsf:101-126)
 // ======================================================================================
-__device__ __forceinline__ float cabsf(float2 a) { return sqrtf(a.x * a.x + a.y * a.y); }
-
+template <class V>
 struct StoreRdm {   // last inverse pass: keep outputs i in [Lh-1, Lh-1+V) that map to gates < gend;
                     // also writes |x| (the CFAR input, fsf:184-185) into the magnitude map.
                     // Branch-free: rejected outputs get an out-of-range buffer offset.
     __amdgpu_buffer_rsrc_t rdm, mag; int G; int Gp; int row0; int rows_total; int Lh1; int g0; int gend;
-    __device__ __forceinline__ void put(int, int row, int o, int, f2 x) const {
+    __device__ __forceinline__ void put(int, int row, int o, int, V x) const {
         const int gg = g0 + o - Lh1;
         const int rho = row0 + row;
         const bool ok = o >= Lh1 && gg < gend && rho < rows_total;
-        buf_st_f2<RSP_ST_AUX>(rdm, ok ? (unsigned)(rho * G + gg) * 8u : RSP_OOB, x);
-        buf_st_f1(mag, ok ? (unsigned)(rho * Gp + gg) * 4u : RSP_OOB, fast_abs(x));
+        buf_st(rdm, ok ? (unsigned)(rho * G + gg) * (unsigned)sizeof(V) : RSP_OOB, x);
+        buf_st1(mag, ok ? (unsigned)(rho * Gp + gg) * (unsigned)sizeof(scal<V>) : RSP_OOB, cmag(x));
     }
 };
 
-#ifndef K2_SH
-#define K2_SH 5   // one pad complex per 32 (tools/lds_conflicts.py)
-#endif
-#define K2_LDS_DATA (RSP_K2_POINTS + (RSP_K2_POINTS >> K2_SH))
-#define K2_LDS_TW 4096       // >= tw_total(log2 M) + tw_total(log2 M, reversed) for M <= 2048
-#define K2_LDS_TW_CMP 1408   // the same for compact tables
-#define K2_MAXM 2048
-
-// ---- mixed-radix overlap-save blocks (M = 5 * 2^k): three Stockham passes of radices
-// (RA, RB, RC) forward and (RC, RB, RA) inverse, RC = 10.  Butterfly counts M / R and partial
-// products Ns need not be powers of two, so every LDS index is padded per element.
-#define K2M_POINTS K2M_POINTS_HOST   // complex points per mixed-radix workgroup (10 per thread)
-
-template <int R, bool INV, int NB, int M, int NS, int NTHR>
-__device__ __forceinline__ void shm_load(const float2* buf, int rs, int nrows, const float2* tw, f2 (&v)[NB][R]) {
-    constexpr int nb = M / R;
-    const int total = nb * nrows;
-#pragma unroll
-    for (int t = 0; t < NB; ++t) {
-        const int beta = threadIdx.x + t * NTHR;
-        if (beta < total) {
-            const int row = beta / nb, j = beta - row * nb;
-            const float2* rowp = buf + row * rs;
-            f2 w[R];
-            if (NS > 1) load_tw<R, INV, true>(tw + (j % NS) * tw_row(R, true), w);
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                f2 x = tof2(rowp[lidx<K2_SH>(j + r * nb)]);
-                if (r > 0 && NS > 1) x = vmul(x, w[r]);
-                v[t][r] = x;
-            }
-        }
-    }
-}
-
-template <int R, bool INV, int NB, int M, int NS, int NTHR, class St>
-__device__ __forceinline__ void shm_store(f2 (&v)[NB][R], int rs, int nrows, const St& st) {
-    constexpr int nb = M / R;
-    const int total = nb * nrows;
-#pragma unroll
-    for (int t = 0; t < NB; ++t) {
-        const int beta = threadIdx.x + t * NTHR;
-        if (beta < total) {
-            const int row = beta / nb, j = beta - row * nb;
-            Dft<R, INV>::run(v[t]);
-            const int idxD = (j / NS) * (NS * R) + j % NS;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int o = idxD + r * NS;
-                st.put(t * R + r, row, o, row * rs + lidx<K2_SH>(o), v[t][r]);
-            }
-        }
-    }
-}
-
-template <int R, bool INV, int NB, int M, int NS, int NTHR, class St>
-__device__ __forceinline__ void shm_pass(float2* buf, int rs, int nrows, const float2* tw, const St& st) {
-    f2 v[NB][R];
-    shm_load<R, INV, NB, M, NS, NTHR>(buf, rs, nrows, tw, v);
-    __syncthreads();
-    shm_store<R, INV, NB, M, NS, NTHR>(v, rs, nrows, st);
-    __syncthreads();
-}
-
-// Twiddle table sizes / offsets of the mixed plans (must match build_mixed_twiddles() in
-// rsp_plan.cpp): forward tables, then inverse; pass q >= 1 owns Ns_q rows of tw_row(R_q).
-constexpr int twm_fwd(int RA, int RB, int RC) { return RA * tw_row(RB, true) + RA * RB * tw_row(RC, true); }
-
-template <int M, int RA, int RB, int RC, int NTHR, int PTSW>
-__device__ __forceinline__ void k2m_fft_job(const Geometry& g, const DevConsts& k, const SegDesc& sd, const K2Job& job,
-                                            const float2* __restrict__ z, float2* __restrict__ rdm,
-                                            float* __restrict__ mag, int row0, int rows_total, float2* L,
-                                            const FramePtrs& fp) {
-    static_assert(RA * RB * RC == M, "mixed plan must factor M");
-    constexpr int rows = PTSW / M;
-    constexpr int PTS = PTSW / NTHR;
-    constexpr int rs = M + (M >> K2_SH);
-    constexpr int NBA = (PTS + RA - 1) / RA, NBB = (PTS + RB - 1) / RB, NBC = (PTS + RC - 1) / RC;
-    constexpr int nb0 = M / RA;
-    const int P = g.P, G = g.G;
-    const int lo = sd.lo, hi = sd.hi, off = sd.off;
-    const int tid = threadIdx.x;
-    const int Lh1 = sd.Lh - 1;
-    const int g0 = sd.ga + job.blk * sd.V;
-    const int a = sd.seg_lo + g0 - Lh1;   // sample index of u[0]
-    const float2* twf = k.twM + sd.tw_off;
-    const float2* twi = twf + twm_fwd(RA, RB, RC);
-    const __amdgpu_buffer_rsrc_t zr = buf_rsrc(z, (unsigned)g.B * g.ntiles * P * g.NT * 8u);
-    // forward pass 0 (Ns = 1) straight from z
-    f2 v0[NBA][RA];
-#pragma unroll
-    for (int t = 0; t < NBA; ++t) {
-        const int beta = tid + t * NTHR;
-        const int rl = beta / nb0, j = beta - rl * nb0;
-        const int rho = row0 + rl;
-        const int b = rho / P, v = rho - b * P;
-        const bool live = beta < rows * nb0 && rho < rows_total;
-#pragma unroll
-        for (int r = 0; r < RA; ++r) {
-            const int n = a + j + r * nb0;
-            const bool ok = live && n >= lo && n <= hi;
-            v0[t][r] = buf_ld_f2(zr, ok ? (unsigned)zaddr(g, b, v, n - lo + off) * 8u : RSP_OOB);
-        }
-    }
-    // H for the last forward pass's outputs j + r M / RC (1/M folded in)
-    f2 hreg[NBC][RC];
-#pragma unroll
-    for (int t = 0; t < NBC; ++t) {
-        const int j = (tid + t * NTHR) % (M / RC);
-#pragma unroll
-        for (int r = 0; r < RC; ++r) hreg[t][r] = tof2(k.H[sd.H_off + j + r * (M / RC)]);
-    }
-    shm_store<RA, false, NBA, M, 1, NTHR>(v0, rs, rows, StoreLds{L});
-    __syncthreads();
-    trace_stamp(fp, 1);
-    shm_pass<RB, false, NBB, M, RA, NTHR>(L, rs, rows, twf, StoreLds{L});
-    {   // fused: forward last pass, x H, inverse pass 0 (same butterflies)
-        f2 v[NBC][RC];
-        shm_load<RC, false, NBC, M, RA * RB, NTHR>(L, rs, rows, twf + RA * tw_row(RB, true), v);
-        __syncthreads();
-#pragma unroll
-        for (int t = 0; t < NBC; ++t) {
-            Dft<RC, false>::run(v[t]);
-#pragma unroll
-            for (int r = 0; r < RC; ++r) v[t][r] = vmul(v[t][r], hreg[t][r]);
-        }
-        shm_store<RC, true, NBC, M, 1, NTHR>(v, rs, rows, StoreLds{L});
-        __syncthreads();
-    }
-    trace_stamp(fp, 2);
-    shm_pass<RB, true, NBB, M, RC, NTHR>(L, rs, rows, twi, StoreLds{L});
-    const int gend = min(sd.gb, g0 + sd.V);
-    shm_pass<RA, true, NBA, M, RC * RB, NTHR>(
-        L, rs, rows, twi + RC * tw_row(RB, true),
-        StoreRdm{buf_rsrc(rdm, (unsigned)rows_total * G * 8u), buf_rsrc(mag, (unsigned)rows_total * g.Gp * 4u), G, g.Gp,
-                 row0, rows_total, Lh1, g0, gend});
-    trace_stamp(fp, 3);
-}
-
-// Mixed-radix jobs as a launch of their own (jobs [g.mix_job0, njobs), workgroups from
-// g.nwg_k2_pow2): 2 rows x 2560 points over 320 threads, so every radix-16 pass keeps all
-// threads busy (16 points each) and the radix-10 passes 80 % of them.
-#ifndef K2M_THREADS
-#define K2M_THREADS 320
-#endif
-template <int M, int RA, int RB, int RC>
-__global__ __launch_bounds__(K2M_THREADS, K2M_THREADS > 320 ? 2 : 3) void k2m_pc(Geometry g, DevConsts k, FramePtrs fp, int rows_total) {
-    extern __shared__ __attribute__((aligned(16))) float2 L[];
-    const int f = blockIdx.y;
-    const int wg = g.nwg_k2_pow2 + blockIdx.x;
-    int ji = g.mix_job0;
-    while (ji + 1 < g.njobs && wg >= g.jobs[ji + 1].wg_begin) ++ji;
-    const K2Job job = g.jobs[ji];
-    const SegDesc& sd = g.segs[job.seg];
-    const int row0 = (wg - job.wg_begin) * sd.rows_per_wg;
-    trace_stamp(fp, 0);
-    k2m_fft_job<M, RA, RB, RC, K2M_THREADS, 2 * M>(g, k, sd, job, fp.z[f], fp.rdm[f], fp.mag[f], row0, rows_total, L, fp);
-}
+// LDS pad of the overlap-save rows: one complex per 32 (float) / 16 (double, 16-B elements:
+// a stride-16 first-pass store then walks 17 x 16 B, distinct 16-B slots of the 128-B
+// ds_write_b128 lane groups)
+template <class T> constexpr int k2_sh() { return sizeof(T) == 4 ? 5 : 4; }
+#define K2_LDS_DATA(SH) (RSP_K2_POINTS + (RSP_K2_POINTS >> (SH)))
 
 // One overlap-save block of one FFT segment for RSP_K2_POINTS / 2^LGM adjacent rows.
 // LDS round trips: forward pass 0 runs on the samples as loaded from z; the forward FFT's
 // last pass, the filter-spectrum product and the inverse FFT's first pass (radices in
 // reverse order, so that pass has the same butterflies) run in registers back to back;
 // the inverse FFT's last pass stores the kept gates to HBM.  2 (log2 M / 4) round trips
-// instead of 2 (log2 M / 4) + 3.
-template <int LGM, bool TWG, bool CMP>
+// instead of 2 (log2 M / 4) + 3.  Twiddles are compact rows read in place from global
+// memory (L1/L2 resident).
+template <class T, int LGM>
 __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k, const SegDesc& sd, const K2Job& job,
-                                           const float2* __restrict__ z, float2* __restrict__ rdm,
-                                           float* __restrict__ mag, int row0, int rows_total, float2* L,
-                                           const FramePtrs& fp) {
+                                           const cx<T>* __restrict__ z, cx<T>* __restrict__ rdm, T* __restrict__ mag,
+                                           int row0, int rows_total, cx<T>* L) {
+    typedef cx<T> V;
+    constexpr int SH = k2_sh<T>();
     constexpr int M = 1 << LGM;
     constexpr int rows = RSP_K2_POINTS / M;
-    constexpr int rs = M + (M >> K2_SH);
+    constexpr int rs = M + (M >> SH);
     constexpr int NP = n_passes(LGM);
     static_assert(NP >= 2, "overlap-save block needs >= 2 FFT passes");
     constexpr int RB0 = rad_bits(LGM, 0), R0 = 1 << RB0, NB0 = 16 / R0, nb0 = M / R0;
@@ -982,14 +755,13 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     const int Lh1 = sd.Lh - 1;
     const int g0 = sd.ga + job.blk * sd.V;
     const int a = sd.seg_lo + g0 - Lh1;           // sample index of u[0]
-    // twiddle tables: LDS copy, or (TWG) read in place from global memory (L1/L2 resident)
-    float2* twl = TWG ? const_cast<float2*>(k.twM + sd.tw_off) : L + K2_LDS_DATA;
+    const V* twl = static_cast<const V*>(k.twM) + sd.tw_off;
+    const V* __restrict__ H = static_cast<const V*>(k.H);
     // every global load of the workgroup in flight together: the 16 samples of this thread's
-    // pass-0 butterflies, its 16 filter-spectrum values (for the fused middle pass) and the
-    // twiddle tables
-    f2 v0[NB0][R0];
+    // pass-0 butterflies and its 16 filter-spectrum values (for the fused middle pass)
+    V v0[NB0][R0];
     const int lgNT = ilog2(g.NT);
-    const __amdgpu_buffer_rsrc_t zr = buf_rsrc(z, (unsigned)g.B * g.ntiles * P * g.NT * 8u);
+    const __amdgpu_buffer_rsrc_t zr = buf_rsrc(z, (unsigned)(g.B * g.ntiles * P * g.NT * sizeof(V)));
 #pragma unroll
     for (int t = 0; t < NB0; ++t) {
         const int beta = tid + t * K2_THREADS;
@@ -1000,84 +772,69 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
         // in-tile slot is fixed, so element r sits at zb + r (nb0 P) (one multiply per thread)
         const int np0 = a + j - lo + off;
         const int zb = ((b * g.ntiles + (np0 >> lgNT)) * P + v) * g.NT + (np0 & (g.NT - 1));
-        // branch-free: every lane loads (a valid address when masked) and selects
+        // branch-free: every lane loads (an out-of-range offset when masked)
         if ((nb0 & (g.NT - 1)) == 0) {   // uniform
 #pragma unroll
             for (int r = 0; r < R0; ++r) {
                 const int n = a + j + r * nb0;
                 const bool ok = rho < rows_total && n >= lo && n <= hi;
-                v0[t][r] = buf_ld_f2(zr, ok ? (unsigned)(zb + r * nb0 * P) * 8u : RSP_OOB);
+                v0[t][r] = buf_ld<V>(zr, ok ? (unsigned)(zb + r * nb0 * P) * (unsigned)sizeof(V) : RSP_OOB);
             }
         } else {
 #pragma unroll
             for (int r = 0; r < R0; ++r) {
                 const int n = a + j + r * nb0;
                 const bool ok = rho < rows_total && n >= lo && n <= hi;
-                v0[t][r] = buf_ld_f2(zr, ok ? (unsigned)zaddr(g, b, v, n - lo + off) * 8u : RSP_OOB);
+                v0[t][r] = buf_ld<V>(zr, ok ? (unsigned)zaddr(g, b, v, n - lo + off) * (unsigned)sizeof(V) : RSP_OOB);
             }
         }
     }
     // H for the last forward pass's outputs j + r M/RL; butterflies t and t + (M/RL)/NTHR of a
     // thread have the same j (different rows), so only the distinct ones are loaded
     constexpr int NHT = (M / RL) / K2_THREADS >= NBL ? NBL : ((M / RL) / K2_THREADS > 0 ? (M / RL) / K2_THREADS : 1);
-    f2 hreg[NHT * RL];
+    V hreg[NHT * RL];
 #pragma unroll
     for (int t = 0; t < NHT; ++t) {
         const int j = (tid + t * K2_THREADS) & (M / RL - 1);   // last pass: Ns = nb = M / RL, idxD = j
 #pragma unroll
-        for (int r = 0; r < RL; ++r) hreg[t * RL + r] = tof2(k.H[sd.H_off + j + r * (M / RL)]);
+        for (int r = 0; r < RL; ++r) hreg[t * RL + r] = H[sd.H_off + j + r * (M / RL)];
     }
-    constexpr int NTWF = tw_total(LGM, false, CMP);
-    constexpr int NTW = NTWF + tw_total(LGM, true, CMP);
-    static_assert(NTW <= (CMP ? K2_LDS_TW_CMP : K2_LDS_TW), "K2 twiddle tables exceed their LDS slot");
-    constexpr int NT_TAB = TWG ? 0 : (NTW + K2_THREADS - 1) / K2_THREADS;
-    float2 tv[NT_TAB > 0 ? NT_TAB : 1];
-#pragma unroll
-    for (int u = 0; u < NT_TAB; ++u) {
-        const int i = tid + u * K2_THREADS;
-        if (i < NTW) tv[u] = k.twM[sd.tw_off + i];
-    }
+    constexpr int NTWF = tw_total(LGM, false, true);
     // forward pass 0 (Ns = 1, no twiddles) straight from the loaded samples
-    sh_store<R0, false, NB0, K2_SH, K2_THREADS, LGM, 0>(v0, rs, rows, StoreLds{L});
-#pragma unroll
-    for (int u = 0; u < NT_TAB; ++u) {
-        const int i = tid + u * K2_THREADS;
-        if (i < NTW) twl[i] = tv[u];
-    }
+    sh_store<R0, false, NB0, SH, K2_THREADS, LGM, 0>(v0, rs, rows, StoreLds<V>{L});
     __syncthreads();
-    trace_stamp(fp, 1);
     // forward passes 1 .. NP-2
-    fft_range<LGM, 1, NP - 1, RB0, 16, false, false, K2_SH, K2_THREADS, CMP>(L, rs, rows, twl, StoreLds{L},
-                                                                               StoreLds{L});
+    fft_range<LGM, 1, NP - 1, RB0, 16, false, false, SH, K2_THREADS, true>(L, rs, rows, twl, StoreLds<V>{L},
+                                                                          StoreLds<V>{L});
     // fused: forward last pass, x H (1/M folded in), inverse pass 0 of the reversed plan
     {
-        f2 v[NBL][RL];
-        sh_load<RL, false, NBL, K2_SH, K2_THREADS, LGM, LGM - RBL, CMP>(L, rs, rows,
-                                                                       twl + tw_pass_off(LGM, NP - 1, false, CMP), v);
+        V v[NBL][RL];
+        sh_load<RL, false, NBL, SH, K2_THREADS, LGM, LGM - RBL, true>(L, rs, rows,
+                                                                       twl + tw_pass_off(LGM, NP - 1, false, true), v);
         __syncthreads();
 #pragma unroll
         for (int t = 0; t < NBL; ++t) {
-            Dft<RL, false>::run(v[t]);
+            Dft<RL, false, V>::run(v[t]);
 #pragma unroll
             for (int r = 0; r < RL; ++r) v[t][r] = vmul(v[t][r], hreg[(t % NHT) * RL + r]);
         }
-        sh_store<RL, true, NBL, K2_SH, K2_THREADS, LGM, 0>(v, rs, rows, StoreLds{L});
+        sh_store<RL, true, NBL, SH, K2_THREADS, LGM, 0>(v, rs, rows, StoreLds<V>{L});
         __syncthreads();
     }
-    trace_stamp(fp, 2);
     // inverse passes 1 .. NP-1 (reversed radices); the last keeps the valid overlap-save
     // outputs = stitched gates
     const int gend = min(sd.gb, g0 + sd.V);
-    fft_range<LGM, 1, NP, RBL, 16, true, true, K2_SH, K2_THREADS, CMP>(
-        L, rs, rows, twl + NTWF, StoreLds{L}, StoreRdm{buf_rsrc(rdm, (unsigned)rows_total * G * 8u),
-                                                      buf_rsrc(mag, (unsigned)rows_total * g.Gp * 4u), G, g.Gp,
-                                                      row0, rows_total, Lh1, g0, gend});
-    trace_stamp(fp, 3);
+    fft_range<LGM, 1, NP, RBL, 16, true, true, SH, K2_THREADS, true>(
+        L, rs, rows, twl + NTWF, StoreLds<V>{L},
+        StoreRdm<V>{buf_rsrc(rdm, (unsigned)(rows_total * G * sizeof(V))),
+                    buf_rsrc(mag, (unsigned)(rows_total * g.Gp * sizeof(T))), G, g.Gp, row0, rows_total, Lh1, g0,
+                    gend});
 }
 
-template <bool TWG, bool CMP>
+template <class T>
 __global__ __launch_bounds__(K2_THREADS, 512 / K2_THREADS) void k2_pc(Geometry g, DevConsts k, FramePtrs fp, int rows_total) {
-    extern __shared__ __attribute__((aligned(16))) float2 L[];   // data | twiddles (M) | H (M)
+    typedef cx<T> V;
+    V* L = reinterpret_cast<V*>(rsp_lds);   // overlap-save rows | narrow: staged rows + taps
     const int f = blockIdx.y;
     const int wg = blockIdx.x;
     int ji = 0;
@@ -1086,32 +843,21 @@ __global__ __launch_bounds__(K2_THREADS, 512 / K2_THREADS) void k2_pc(Geometry g
     const SegDesc& sd = g.segs[job.seg];
     const int rows = sd.rows_per_wg;
     const int row0 = (wg - job.wg_begin) * rows;
-    trace_stamp(fp, 0);
-    const float2* __restrict__ z = fp.z[f];
-    float2* __restrict__ rdm = fp.rdm[f];
-    float* __restrict__ mag = fp.mag[f];
+    const V* __restrict__ z = static_cast<const V*>(fp.z[f]);
+    V* __restrict__ rdm = static_cast<V*>(fp.rdm[f]);
+    T* __restrict__ mag = static_cast<T*>(fp.mag[f]);
     const int P = g.P, G = g.G;
     const int lo = sd.lo, hi = sd.hi, off = sd.off;
     const int tid = threadIdx.x;
 
-    if (sd.type == 1 && sd.mixM) {
-        switch (sd.mixM) {
-            case 640: k2m_fft_job<640, 8, 8, 10, K2_THREADS, K2M_POINTS>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
-            case 1280: k2m_fft_job<1280, 16, 8, 10, K2_THREADS, K2M_POINTS>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
-            default: k2m_fft_job<2560, 16, 16, 10, K2_THREADS, K2M_POINTS>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
-        }
-    } else if (sd.type == 1) {
-#ifdef K2_ONLY_LGM   // ISA inspection builds: one block size only
-        k2_fft_job<K2_ONLY_LGM, TWG, CMP>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp);
-        if (sd.logM >= 0) return;
-#endif
+    if (sd.type == 1) {
         switch (sd.logM) {
-            case 6: k2_fft_job<6, TWG, CMP>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
-            case 7: k2_fft_job<7, TWG, CMP>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
-            case 8: k2_fft_job<8, TWG, CMP>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
-            case 9: k2_fft_job<9, TWG, CMP>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
-            case 10: k2_fft_job<10, TWG, CMP>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
-            default: k2_fft_job<11, TWG, CMP>(g, k, sd, job, z, rdm, mag, row0, rows_total, L, fp); break;
+            case 6: k2_fft_job<T, 6>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+            case 7: k2_fft_job<T, 7>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+            case 8: k2_fft_job<T, 8>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+            case 9: k2_fft_job<T, 9>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+            case 10: k2_fft_job<T, 10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+            default: k2_fft_job<T, 11>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
         }
     } else {
         // direct FIR (narrow segment): filter() + circshift(-fir_delay) (fsf:111-112).  Each
@@ -1121,11 +867,11 @@ __global__ __launch_bounds__(K2_THREADS, 512 / K2_THREADS) void k2_pc(Geometry g
         const int PADL = sd.ntaps - 1, WP = W + PADL;
         const int nw = rows * WP;
         for (int e0 = 0; e0 < nw; e0 += 16 * K2_THREADS) {
-            float2 val[16];
+            V val[16];
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
                 const int e = e0 + tid + u * K2_THREADS;
-                val[u] = make_float2(0.f, 0.f);
+                val[u] = V{};
                 if (e < nw) {
                     const int rl = e / WP, i = e - rl * WP - PADL;
                     const int rho = row0 + rl;
@@ -1141,10 +887,10 @@ __global__ __launch_bounds__(K2_THREADS, 512 / K2_THREADS) void k2_pc(Geometry g
                 if (e < nw) L[e] = val[u];
             }
         }
-        float* tp = reinterpret_cast<float*>(L + nw);   // taps: LDS broadcast reads
-        for (int e = tid; e < sd.ntaps; e += K2_THREADS) tp[e] = k.taps[sd.taps_off + e];
+        T* tp = reinterpret_cast<T*>(L + nw);   // taps: LDS broadcast reads
+        const T* __restrict__ taps = static_cast<const T*>(k.taps);
+        for (int e = tid; e < sd.ntaps; e += K2_THREADS) tp[e] = taps[sd.taps_off + e];
         __syncthreads();
-        trace_stamp(fp, 1);
         const int nout = sd.gb - sd.ga;
         // 4 consecutive gates per thread: the 4 outputs share a register window that slides one
         // sample per tap (1 LDS read + 4 FMAs per tap); a group whose circshift index wraps
@@ -1157,38 +903,36 @@ __global__ __launch_bounds__(K2_THREADS, 512 / K2_THREADS) void k2_pc(Geometry g
             const int gg0 = sd.ga + q0;
             int kk0 = (gg0 + sd.delay) % sd.Ls;
             if (kk0 < 0) kk0 += sd.Ls;
-            const float2* row = L + rl * WP + PADL - lo + sd.seg_lo;   // row[kk] = x(seg_lo + kk)
+            const V* row = L + rl * WP + PADL - lo + sd.seg_lo;   // row[kk] = x(seg_lo + kk)
             if (q0 + 4 <= nout && kk0 + 3 < sd.Ls) {
-                const float2* xr = row + kk0;
-                f2 w0 = tof2(xr[0]), w1 = tof2(xr[1]), w2 = tof2(xr[2]), w3 = tof2(xr[3]);
-                float t = tp[0];
-                f2 a0 = t * w0, a1 = t * w1, a2 = t * w2, a3 = t * w3;
+                const V* xr = row + kk0;
+                V w0 = xr[0], w1 = xr[1], w2 = xr[2], w3 = xr[3];
+                T t = tp[0];
+                V a0 = t * w0, a1 = t * w1, a2 = t * w2, a3 = t * w3;
 #pragma unroll 4
                 for (int j = 1; j < sd.ntaps; ++j) {
                     w3 = w2; w2 = w1; w1 = w0;
-                    w0 = tof2(xr[-j]);
+                    w0 = xr[-j];
                     t = tp[j];
                     a0 += t * w0; a1 += t * w1; a2 += t * w2; a3 += t * w3;
                 }
-                float2* ro = rdm + (size_t)rho * G + gg0;
-                float* mo = mag + (size_t)rho * g.Gp + gg0;
-                ro[0] = fromf2(a0); ro[1] = fromf2(a1); ro[2] = fromf2(a2); ro[3] = fromf2(a3);
-                mo[0] = fast_abs(a0); mo[1] = fast_abs(a1); mo[2] = fast_abs(a2); mo[3] = fast_abs(a3);
+                V* ro = rdm + (size_t)rho * G + gg0;
+                T* mo = mag + (size_t)rho * g.Gp + gg0;
+                ro[0] = a0; ro[1] = a1; ro[2] = a2; ro[3] = a3;
+                mo[0] = cmag(a0); mo[1] = cmag(a1); mo[2] = cmag(a2); mo[3] = cmag(a3);
             } else {
                 for (int q = 0; q < 4 && q0 + q < nout; ++q) {
                     const int gg = gg0 + q;
                     int kk = (gg + sd.delay) % sd.Ls;
                     if (kk < 0) kk += sd.Ls;
-                    const float2* xr = row + kk;
-                    f2 acc = f2{0.f, 0.f};
-                    for (int j = 0; j < sd.ntaps; ++j) acc += tp[j] * tof2(xr[-j]);
-                    rdm[(size_t)rho * G + gg] = fromf2(acc);
-                    mag[(size_t)rho * g.Gp + gg] = fast_abs(acc);
+                    const V* xr = row + kk;
+                    V acc = V{};
+                    for (int j = 0; j < sd.ntaps; ++j) acc += tp[j] * xr[-j];
+                    rdm[(size_t)rho * G + gg] = acc;
+                    mag[(size_t)rho * g.Gp + gg] = cmag(acc);
                 }
             }
         }
-        trace_stamp(fp, 2);
-        trace_stamp(fp, 3);
     }
 }
 
@@ -1198,7 +942,7 @@ __global__ __launch_bounds__(K2_THREADS, 512 / K2_THREADS) void k2_pc(Geometry g
 // Peak of MATLAB interp1(...,'spline') (not-a-knot) sampled at step 1/interp over n
 // equally spaced points (fsf:257-260, 272-275); returns the first-argmax abscissa.
 template <int INTERP>
-__device__ double spline_peak(const double* y, int n) {
+__device__ __forceinline__ double spline_peak(const double* y, int n) {
     // Piecewise-cubic coefficients per unit interval, then Horner at q / INTERP; the sample
     // grid and the first-argmax rule are the reference's (interp1 on cells(1):1/INTERP:cells(end)).
     constexpr double dx = 1.0 / INTERP;   // 1/8, 1/4: exact
@@ -1218,15 +962,15 @@ __device__ double spline_peak(const double* y, int n) {
             c3[i] = (Mv[i + 1] - Mv[i]) * (1.0 / 6.0);
         }
     } else {          // n == 4: the single cubic through 4 points; n == 3: the parabola
-        const double d1 = y[1] - y[0], d2 = y[2] - 2.0 * y[1] + y[0];
+        const double d1 = y[1] - y[0], d2_ = y[2] - 2.0 * y[1] + y[0];
         const double d3 = (n == 4) ? y[3] - 3.0 * y[2] + 3.0 * y[1] - y[0] : 0.0;
         // Newton form about x = 0 expanded at each integer knot i
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const double x = i;
-            c0[i] = y[0] + x * d1 + x * (x - 1.0) * 0.5 * d2 + x * (x - 1.0) * (x - 2.0) * (1.0 / 6.0) * d3;
-            c1[i] = d1 + (2.0 * x - 1.0) * 0.5 * d2 + (3.0 * x * x - 6.0 * x + 2.0) * (1.0 / 6.0) * d3;
-            c2[i] = 0.5 * d2 + (3.0 * x - 3.0) * (1.0 / 6.0) * d3;
+            c0[i] = y[0] + x * d1 + x * (x - 1.0) * 0.5 * d2_ + x * (x - 1.0) * (x - 2.0) * (1.0 / 6.0) * d3;
+            c1[i] = d1 + (2.0 * x - 1.0) * 0.5 * d2_ + (3.0 * x * x - 6.0 * x + 2.0) * (1.0 / 6.0) * d3;
+            c2[i] = 0.5 * d2_ + (3.0 * x - 3.0) * (1.0 / 6.0) * d3;
             c3[i] = (1.0 / 6.0) * d3;
         }
     }
@@ -1258,9 +1002,10 @@ __device__ double spline_peak(const double* y, int n) {
 }
 
 // S9 of one detection from the workgroup's S tile (fsf:237-290).
-__device__ __forceinline__ void s9_estimate(const DevConsts& k, const float* S, int W, int c0, int P, int G, int Gp,
-                                            int v, int r, int pair, const float* __restrict__ MA,
-                                            const float* __restrict__ MB, DevDet* out) {
+template <class T>
+__device__ __forceinline__ void s9_estimate(const DevConsts& k, const T* S, int W, int c0, int P, int G, int Gp, int v,
+                                            int r, int pair, const T* __restrict__ MA, const T* __restrict__ MB,
+                                            DevDet* out) {
     const int c = r - c0;
     // the 5-cell windows clipped to the map (fsf:241-250): cells first .. first + n - 1
     const int rfirst = max(r - 2, 0), nrc = min(r + 2, G - 1) - rfirst + 1;
@@ -1289,25 +1034,33 @@ __device__ __forceinline__ void s9_estimate(const DevConsts& k, const float* S, 
     *out = d;
 }
 
-// Out-of-line copy for the queue-overflow path (pathological detection densities), so the
-// CFAR loops do not carry an inlined S9 body.
-__device__ __attribute__((noinline)) void s9_estimate_ool(const DevConsts& k, const float* S, int W, int c0, int P,
-                                                          int G, int Gp, int v, int r, int pair, const float* MA,
-                                                          const float* MB, DevDet* out) {
-    s9_estimate(k, S, W, c0, P, G, Gp, v, r, pair, MA, MB, out);
-}
-
 #define K3_QCAP 1024
-#define K3_VEC 12   // float4 loads per beam per thread in flight
+#define K3_VEC 12   // 16-B loads per beam per thread in flight
 
 constexpr int floor4(int x) { return x >= 0 ? (x & ~3) : -((-x + 3) & ~3); }
 
+// 4 consecutive cells of an S row from LDS (16-B aligned): one ds_read_b128 (float) or two
+// (double)
+__device__ __forceinline__ void ld4(const float* p, float (&o)[4]) {
+    const f32x4 t = *reinterpret_cast<const f32x4*>(p);
+    o[0] = t.x; o[1] = t.y; o[2] = t.z; o[3] = t.w;
+}
+__device__ __forceinline__ void ld4(const double* p, double (&o)[4]) {
+    const d2 a = *reinterpret_cast<const d2*>(p), b = *reinterpret_cast<const d2*>(p + 2);
+    o[0] = a.x; o[1] = a.y; o[2] = b.x; o[3] = b.y;
+}
+template <class T> struct U16;   // one 16-B unit of a map row
+template <> struct U16<float> { typedef f32x4 U; static constexpr int E = 4; };
+template <> struct U16<double> { typedef d2 U; static constexpr int E = 2; };
+
 // RR/RV/GR/GV = reference/guard cell counts when known at compile time (the reference's
 // 5/5/10/10, v8:45-46), 0 = runtime.  Tiles: RT range cells x all P Doppler cells of one beam
-// pair, tile starts aligned to 4 cells so that the magnitude rows load as float4.
-template <int RR, int RV, int GR, int GV>
+// pair, tile starts aligned to 4 cells so that the magnitude rows load as 16-B units.
+template <class T, int RR, int RV, int GR, int GV>
 __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts k, FramePtrs fp) {
-    extern __shared__ __attribute__((aligned(16))) float S[];   // [P][W] | queue[K3_QCAP] | qn, base
+    T* S = reinterpret_cast<T*>(rsp_lds);   // [P][W] | queue[K3_QCAP] | qn, base
+    typedef typename U16<T>::U U;
+    constexpr int EPU = U16<T>::E;
     constexpr bool FAST = RR > 0 && RV > 0 && GR > 0 && GV > 0;
     // XCD-aware order (bijective swizzle, cdna_hip_programming.md T1): the workgroups that
     // share an XCD take consecutive (tile, pair) ids with pairs fastest, so beam b's tile --
@@ -1329,70 +1082,74 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
     int* queue = reinterpret_cast<int*>(S + P * W);
     int* qn = queue + K3_QCAP;
     const int Gp = g.Gp;
-    const float* __restrict__ MA = fp.mag[f] + (size_t)pair * P * Gp;   // |RDM| of beams pair, pair+1
-    const float* __restrict__ MB = MA + (size_t)P * Gp;
-    trace_stamp(fp, 0);
+    const T* __restrict__ MA = static_cast<const T*>(fp.mag[f]) + (size_t)pair * P * Gp;   // |RDM| of beams pair, pair+1
+    const T* __restrict__ MB = MA + (size_t)P * Gp;
     if (threadIdx.x == 0) qn[0] = 0;
     // ---- load S = |A| + |B| (fsf:184-187) from the magnitude maps: 16 B per lane,
-    //      K3_VEC float4 of each beam in flight per thread
+    //      K3_VEC units of each beam in flight per thread
     {
-        const int W4 = W >> 2, n4 = P * W4;
-        for (int e0 = 0; e0 < n4; e0 += K3_VEC * RSP_THREADS) {
-            float4 xa[K3_VEC], xb[K3_VEC];
+        const int WU = W / EPU, nu = P * WU;
+        for (int e0 = 0; e0 < nu; e0 += K3_VEC * RSP_THREADS) {
+            U xa[K3_VEC], xb[K3_VEC];
 #pragma unroll
             for (int u = 0; u < K3_VEC; ++u) {
                 const int e = e0 + threadIdx.x + u * RSP_THREADS;
-                xa[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                xa[u] = U{};
                 xb[u] = xa[u];
-                if (e < n4) {
-                    const int v = e / W4, r = c0 + 4 * (e - v * W4);
-                    if (r >= 0 && r < G) {   // rows are padded to Gp (multiple of 4): r + 3 < Gp
-                        xa[u] = *reinterpret_cast<const float4*>(MA + (size_t)v * Gp + r);
-                        xb[u] = *reinterpret_cast<const float4*>(MB + (size_t)v * Gp + r);
-                        if (r + 1 >= G) { xa[u].y = 0.f; xb[u].y = 0.f; }
-                        if (r + 2 >= G) { xa[u].z = 0.f; xb[u].z = 0.f; }
-                        if (r + 3 >= G) { xa[u].w = 0.f; xb[u].w = 0.f; }
+                if (e < nu) {
+                    const int v = e / WU, r = c0 + EPU * (e - v * WU);
+                    if (r >= 0 && r < G) {   // rows are padded to Gp (multiple of 4): r + EPU - 1 < Gp
+                        xa[u] = *reinterpret_cast<const U*>(MA + (size_t)v * Gp + r);
+                        xb[u] = *reinterpret_cast<const U*>(MB + (size_t)v * Gp + r);
+#pragma unroll
+                        for (int q = 1; q < EPU; ++q)
+                            if (r + q >= G) { xa[u][q] = 0; xb[u][q] = 0; }
                     }
                 }
             }
 #pragma unroll
             for (int u = 0; u < K3_VEC; ++u) {
                 const int e = e0 + threadIdx.x + u * RSP_THREADS;
-                if (e < n4)
-                    reinterpret_cast<float4*>(S)[e] =
-                        make_float4(xa[u].x + xb[u].x, xa[u].y + xb[u].y, xa[u].z + xb[u].z, xa[u].w + xb[u].w);
+                if (e < nu) reinterpret_cast<U*>(S)[e] = xa[u] + xb[u];
             }
         }
     }
     __syncthreads();
-    trace_stamp(fp, 1);
+    if (fp.smap[f]) {   // on request: rdm_for_cfar_all as thresholded here, [pair][v][r]
+        T* sm = static_cast<T*>(fp.smap[f]) + (size_t)pair * P * G;
+        const int wlo = tile == 0 ? 0 : tstart, whi = tile == ntile - 1 ? G : min(tstart + RT, G);
+        const int nwc = whi - wlo;
+        for (int e = threadIdx.x; e < P * nwc; e += RSP_THREADS) {
+            const int v = e / nwc, r = wlo + (e - v * nwc);
+            sm[(size_t)v * G + r] = S[v * W + (r - c0)];
+        }
+    }
     const int v0 = rV + gV, v1 = P - rV - gV;
     if (v1 <= v0 || cut_hi <= cut_lo) return;
-    const float fR = (float)rR, fV = (float)rV;
-    // mean() = sum / n over the slices of fsf:197-203 (max(a/n, b/n) = max(a, b)/n); the
-    // division is a multiply by 1/n (<= 1 ulp from the quotient: only cells within that of the
-    // threshold can decide differently, the fp32-vs-fp64 band the parity tests allow)
-    const float iR = 1.0f / fR, iV = 1.0f / fV;
+    const double Tc = g.T;
+    // mean() = sum / n over the slices of fsf:197-203 (max(a/n, b/n) = max(a, b)/n).  double: the
+    // quotient, as MATLAB; float: a multiply by 1/n (<= 1 ulp from the quotient)
+    const T fR = (T)rR, fV = (T)rV;
+    const T iR = (T)1 / fR, iV = (T)1 / fV;
+    auto noise = [&](T a, T b, T fn, T in) -> T {
+        if constexpr (sizeof(T) == 8) return fmax(a, b) / fn;
+        else return fmaxf(a, b) * in;
+    };
+    bool overflow = false;
 #define K3_HIT(V, C, CUT, LR, TR, LV, TV)                                                               \
     do {                                                                                                \
-        const float nR_ = fmaxf(LR, TR) * iR, nV_ = fmaxf(LV, TV) * iV;                                 \
-        if ((CUT) > g.T * fmaxf(nR_, nV_)) {                                                            \
+        const T nR_ = noise(LR, TR, fR, iR), nV_ = noise(LV, TV, fV, iV);                               \
+        if ((CUT) > (T)Tc * (nR_ > nV_ ? nR_ : nV_)) {                                                  \
             const int qi = atomicAdd(qn, 1);                                                            \
-            if (qi < K3_QCAP) {                                                                         \
-                queue[qi] = ((V) << 16) | (C);                                                          \
-            } else { /* queue overflow (pathological): estimate in place */                             \
-                const int idx = atomicAdd(fp.count[f], 1);                                              \
-                if (idx < g.max_dets)                                                                   \
-                    s9_estimate_ool(k, S, W, c0, P, G, Gp, V, c0 + (C), pair, MA, MB, &fp.dets[f][idx]); \
-            }                                                                                           \
+            if (qi < K3_QCAP) queue[qi] = ((V) << 16) | (C);                                            \
+            else overflow = true;                                                                       \
         }                                                                                               \
     } while (0)
     // ---- cross GOCA-CFAR (fsf:192-213); hits go to an LDS queue so that the S9 work is
     //      spread over the whole workgroup instead of serialising in the lane that owns a range cell
-    if (FAST && (RT == 64 || RT == 32)) {   // RT = 32: long-P tiles (LDS cap in the plan)
+    if (FAST && (RT == 64 || RT == 32)) {   // RT = 32: long-P / double tiles (LDS cap in the plan)
         // a thread takes 4 adjacent range cells of one Doppler row: every window value comes
-        // from float4 LDS reads (17 per 4 cells instead of 20 scalar reads per cell); sums run
-        // left to right over each slice like mean()
+        // from 16-B LDS reads; sums run left to right over each slice like mean()
         constexpr int DL = -(GR + RR), DR = GR + 1;              // window starts rel. to the cell
         constexpr int BL = floor4(DL), BR = floor4(DR);
         constexpr int NL = (DL + 3 + RR - BL + 3) / 4, NR = (DR + 3 + RR - BR + 3) / 4;
@@ -1407,36 +1164,38 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
         const int rgp = lgT == 4 ? (rg & ~3) | ((rg & 1) << 1) | ((rg >> 1) & 1) : rg;
 #pragma unroll 1
         for (int v = v0 + rgp; v < v1; v += RSP_THREADS >> lgT) {
-            const float* row = S + v * W + c;
-            float xl[4 * NL], xr[4 * NR], cv[4];
-            f2 lv01 = {0.f, 0.f}, lv23 = {0.f, 0.f}, tv01 = {0.f, 0.f}, tv23 = {0.f, 0.f};   // packed column sums
+            const T* row = S + v * W + c;
+            T xl[4 * NL], xr[4 * NR], cv[4];
+            T lv[4] = {0, 0, 0, 0}, tv[4] = {0, 0, 0, 0};
 #pragma unroll
             for (int j = 0; j < NL; ++j) {
-                const float4 t = *reinterpret_cast<const float4*>(row + BL + 4 * j);
-                xl[4 * j] = t.x; xl[4 * j + 1] = t.y; xl[4 * j + 2] = t.z; xl[4 * j + 3] = t.w;
+                T t[4];
+                ld4(row + BL + 4 * j, t);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) xl[4 * j + i] = t[i];
             }
 #pragma unroll
             for (int j = 0; j < NR; ++j) {
-                const float4 t = *reinterpret_cast<const float4*>(row + BR + 4 * j);
-                xr[4 * j] = t.x; xr[4 * j + 1] = t.y; xr[4 * j + 2] = t.z; xr[4 * j + 3] = t.w;
+                T t[4];
+                ld4(row + BR + 4 * j, t);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) xr[4 * j + i] = t[i];
             }
-            {
-                const float4 t = *reinterpret_cast<const float4*>(row);
-                cv[0] = t.x; cv[1] = t.y; cv[2] = t.z; cv[3] = t.w;
-            }
+            ld4(row, cv);
 #pragma unroll
             for (int qq = 0; qq < RV; ++qq) {
-                const float4 a = *reinterpret_cast<const float4*>(row + (qq - GV - RV) * W);
-                const float4 b = *reinterpret_cast<const float4*>(row + (qq + GV + 1) * W);
-                lv01 += f2{a.x, a.y};
-                lv23 += f2{a.z, a.w};
-                tv01 += f2{b.x, b.y};
-                tv23 += f2{b.z, b.w};
+                T a[4], b[4];
+                ld4(row + (qq - GV - RV) * W, a);
+                ld4(row + (qq + GV + 1) * W, b);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    lv[i] += a[i];
+                    tv[i] += b[i];
+                }
             }
-            const float lv[4] = {lv01.x, lv01.y, lv23.x, lv23.y}, tv[4] = {tv01.x, tv01.y, tv23.x, tv23.y};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                float lr = 0.f, tr = 0.f;
+                T lr = 0, tr = 0;
 #pragma unroll
                 for (int qq = 0; qq < RR; ++qq) {
                     lr += xl[i + DL - BL + qq];
@@ -1453,12 +1212,12 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
             if (r >= cut_hi) continue;
             const int c = r - c0;
             for (int v = v0 + wv; v < v1; v += 4) {
-                const float* rowp = S + v * W;
-                float lr = 0.f, tr = 0.f, lv = 0.f, tv = 0.f;
-                const float* lrp = rowp + c - gR - rR;
-                const float* trp = rowp + c + gR + 1;
-                const float* lvp = S + (v - gV - rV) * W + c;
-                const float* tvp = S + (v + gV + 1) * W + c;
+                const T* rowp = S + v * W;
+                T lr = 0, tr = 0, lv = 0, tv = 0;
+                const T* lrp = rowp + c - gR - rR;
+                const T* trp = rowp + c + gR + 1;
+                const T* lvp = S + (v - gV - rV) * W + c;
+                const T* tvp = S + (v + gV + 1) * W + c;
                 for (int qq = 0; qq < rR; ++qq) {
                     lr += lrp[qq];
                     tr += trp[qq];
@@ -1472,13 +1231,12 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
         }
     }
 #undef K3_HIT
+    // queue overflow (> K3_QCAP hits in one tile, a pathological detection density): the frame's
+    // count is pushed past the plan capacity so that the host reports RSP_ERR_OVERFLOW
+    if (overflow) atomicAdd(fp.count[f], g.max_dets + 1);
     __syncthreads();
-    trace_stamp(fp, 2);
     const int n = min(qn[0], K3_QCAP);
-    if (n == 0) {
-        trace_stamp(fp, 3);
-        return;
-    }
+    if (n == 0) return;
     if (threadIdx.x == 0) qn[1] = atomicAdd(fp.count[f], n);   // one global reservation per workgroup
     __syncthreads();
     const int base = qn[1];
@@ -1487,43 +1245,37 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
         if (idx >= g.max_dets) break;
         const int e = queue[i];
         const int v = e >> 16, c = e & 0xFFFF;
-        s9_estimate(k, S, W, c0, P, G, Gp, v, c0 + c, pair, MA, MB, &fp.dets[f][idx]);
-    }
-    if (fp.trace) {
-        __syncthreads();
-        trace_stamp(fp, 3);
+        s9_estimate<T>(k, S, W, c0, P, G, Gp, v, c0 + c, pair, MA, MB, &fp.dets[f][idx]);
     }
 }
 
 // ======================================================================================
 // MTD over pulses of a pulse-compressed cube pc[B][P][G] -> rdm[B][P][G] (fsf:131-136)
 // ======================================================================================
-template <int LGP>
-__global__ __launch_bounds__(RSP_THREADS, 2) void k_mtd_cols(Geometry g, DevConsts k, const float2* __restrict__ pc,
-                                                        float2* __restrict__ rdm) {
-    extern __shared__ __attribute__((aligned(16))) float2 Y[];   // [GT][Ppad] + W_P table
+template <class T, int LGP>
+__global__ __launch_bounds__(RSP_THREADS, 2) void k_mtd_cols(Geometry g, DevConsts k, const cx<T>* __restrict__ pc,
+                                                        cx<T>* __restrict__ rdm) {
+    typedef cx<T> V;
+    V* Y = reinterpret_cast<V*>(rsp_lds);   // [GT][Ppad] + W_P table
     constexpr int GT = 16;
-    float2* twl = Y + GT * g.Ppad;
+    V* twl = Y + GT * g.Ppad;
+    const T* __restrict__ win = static_cast<const T*>(k.win);
     if constexpr (LGP > 0)
-        for (int i = threadIdx.x; i < tw_total(LGP); i += RSP_THREADS) twl[i] = k.twPp[i];
+        for (int i = threadIdx.x; i < tw_total(LGP); i += RSP_THREADS) twl[i] = static_cast<const V*>(k.twPp)[i];
     const int b = blockIdx.y, gt0 = blockIdx.x * GT;
     const int P = g.P, G = g.G, Ppad = g.Ppad;
     for (int e = threadIdx.x; e < P * GT; e += RSP_THREADS) {
         const int m = e / GT, gl = e - m * GT;
         const int gg = gt0 + gl;
-        float2 val = make_float2(0.f, 0.f);
-        if (gg < G) {
-            val = pc[((size_t)b * P + m) * G + gg];
-            val.x *= k.win[m];
-            val.y *= k.win[m];
-        }
+        V val = V{};
+        if (gg < G) val = pc[((size_t)b * P + m) * G + gg] * win[m];
         Y[gl * Ppad + m] = val;
     }
     __syncthreads();
     const int half = P >> 1;
     if constexpr (LGP > 0) {
-        StoreLds st{Y};
-        fft_passes<LGP, 0, 0, (16 << LGP) / RSP_THREADS, false, 0, RSP_THREADS>(Y, Ppad, GT, twl, st, st);
+        StoreLds<V> st{Y};
+        fft_passes<LGP, (16 << LGP) / RSP_THREADS, 0, RSP_THREADS>(Y, Ppad, GT, twl, st, st);
         for (int e = threadIdx.x; e < P * GT; e += RSP_THREADS) {
             const int v = e / GT, gl = e - v * GT;
             const int gg = gt0 + gl;
@@ -1532,15 +1284,16 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k_mtd_cols(Geometry g, DevCons
             if (gg < G) rdm[((size_t)b * P + v) * G + gg] = Y[gl * Ppad + src];
         }
     } else {
+        const V* __restrict__ twP = static_cast<const V*>(k.twP);
         for (int e = threadIdx.x; e < P * GT; e += RSP_THREADS) {
             const int v = e / GT, gl = e - v * GT;
             const int gg = gt0 + gl;
             int kk = v - half;
             if (kk < 0) kk += P;
-            float2 acc = make_float2(0.f, 0.f);
+            V acc = V{};
             int idx = 0;
             for (int p = 0; p < P; ++p) {
-                acc = cadd(acc, cmul(Y[gl * Ppad + p], k.twP[idx]));
+                acc += vmul(Y[gl * Ppad + p], twP[idx]);
                 idx += kk;
                 if (idx >= P) idx -= P;
             }
@@ -1552,9 +1305,10 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k_mtd_cols(Geometry g, DevCons
 // ======================================================================================
 // S4 + S4.1 on the device: echo synthesis + Philox noise (fsf:45-88)
 // ======================================================================================
+template <class T>
 __global__ __launch_bounds__(RSP_THREADS) void k_synth(Geometry g, const double* __restrict__ tx,
                                                      const SynthTarget* __restrict__ tg, int nt, int frame_idx,
-                                                     uint64_t seed, double nscale, float2* __restrict__ cube) {
+                                                     uint64_t seed, double nscale, cx<T>* __restrict__ cube) {
     const size_t total = (size_t)g.P * g.N * g.C;
     const size_t i = (size_t)blockIdx.x * RSP_THREADS + threadIdx.x;
     if (i >= total) return;
@@ -1590,7 +1344,7 @@ __global__ __launch_bounds__(RSP_THREADS) void k_synth(Geometry g, const double*
     sincos(2.0 * M_PI * ub, &sb, &cb);
     re += rr * cb * nscale;
     im += rr * sb * nscale;
-    cube[o] = make_float2((float)re, (float)im);
+    cube[o] = cx<T>{(T)re, (T)im};
 }
 
 }  // namespace
@@ -1604,21 +1358,34 @@ static hipError_t allow_lds(K kernel, size_t bytes) {
                                (int)bytes);
 }
 
-template <int BMAX, int CP>
+static size_t cplx_bytes(const Geometry& g) { return g.prec == RSP_PREC_F64 ? 16 : 8; }
+static int k1_tpw(const Geometry& g) {
+    const int cp = g.C <= 8 ? 8 : (g.C <= 16 ? 16 : 32), bmax = g.B <= 4 ? 4 : (g.B <= 8 ? 8 : 16);
+    const int nj = cp / 4, mb = bmax <= 8 ? 1 : 2;
+    return (16 / nj) / mb > 0 ? (16 / nj) / mb : 1;
+}
+static size_t k1p_lds(const Geometry& g) { return ((size_t)2 * g.B * g.NT * g.Ppad + g.P) * cplx_bytes(g); }
+
+bool k1_persistent_fits(const Geometry& g) {
+    const int pt = g.prec == RSP_PREC_F64 ? 16 : 32;   // pulses per MFMA sub-tile
+    const int pts = g.prec == RSP_PREC_F64 ? 8 : 16;   // FFT points per thread (k1p_pts)
+    return g.pow2P && g.logP >= 6 && g.logP <= 8 && g.NT * (g.P / pt) <= (K1_THREADS / 64) * k1_tpw(g) &&
+           k1p_lds(g) <= 160 * 1024 && g.B * g.NT * g.P <= pts * K1_THREADS && g.ncu > 0 && !g.k1_tiled;
+}
+
+template <class T, int BMAX, int CP>
 static hipError_t launch_k1_t(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int mode,
                               hipStream_t s) {
-    constexpr int NJ = CP / 4, MB = BMAX <= 8 ? 1 : 2, TPW = (16 / NJ) / MB > 0 ? (16 / NJ) / MB : 1;
-    const size_t ldsp = ((size_t)((g.dbg & 8192) ? 1 : 2) * g.B * g.NT * g.Ppad + g.P) * sizeof(float2);
-    if (mode == 3 && g.pow2P && g.NT * ((g.P + 31) >> 5) <= (K1_THREADS / 64) * TPW && ldsp <= 160 * 1024 &&
-        g.ncu > 0 && !(g.dbg & 4096)) {   // RSP_ABLATE=4096: the non-persistent kernel
+    if (mode == 3 && k1_persistent_fits(g)) {
         // one FFT size per instantiation keeps the prefetch registers + FFT under 256 VGPRs
+        const size_t ldsp = k1p_lds(g);
         const int grid = std::min(g.ncu, nf * g.ntiles);
-#define K1P_LAUNCH(LGP)                                                                                     \
-    do {                                                                                                    \
-        hipError_t e = allow_lds(k1p_dbf_mtd<BMAX, CP, LGP>, ldsp);                                         \
-        if (e != hipSuccess) return e;                                                                      \
-        hipLaunchKernelGGL((k1p_dbf_mtd<BMAX, CP, LGP>), dim3(grid), dim3(K1_THREADS), ldsp, s, g, k, fp, nf); \
-        return hipGetLastError();                                                                           \
+#define K1P_LAUNCH(LGP)                                                                                        \
+    do {                                                                                                       \
+        hipError_t e = allow_lds(k1p_dbf_mtd<T, BMAX, CP, LGP>, ldsp);                                         \
+        if (e != hipSuccess) return e;                                                                         \
+        hipLaunchKernelGGL((k1p_dbf_mtd<T, BMAX, CP, LGP>), dim3(grid), dim3(K1_THREADS), ldsp, s, g, k, fp, nf); \
+        return hipGetLastError();                                                                              \
     } while (0)
         switch (g.logP) {
             case 6: K1P_LAUNCH(6);
@@ -1628,109 +1395,105 @@ static hipError_t launch_k1_t(const Geometry& g, const DevConsts& k, const Frame
         }
 #undef K1P_LAUNCH
     }
-    const size_t lds = ((size_t)g.B * g.NT * g.Ppad + g.P) * sizeof(float2);
-    hipError_t e = allow_lds(k1_dbf_mtd<BMAX, CP>, lds);
+    const size_t lds = ((size_t)g.B * g.NT * g.Ppad + g.P) * sizeof(cx<T>);
+    hipError_t e = allow_lds(k1_dbf_mtd<T, BMAX, CP>, lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k1_dbf_mtd<BMAX, CP>), dim3(g.ntiles, nf), dim3(K1_THREADS), lds, s, g, k, fp, mode);
+    hipLaunchKernelGGL((k1_dbf_mtd<T, BMAX, CP>), dim3(g.ntiles, nf), dim3(K1_THREADS), lds, s, g, k, fp, mode);
     return hipGetLastError();
 }
 
-template <int BMAX>
+template <class T, int BMAX>
 static hipError_t launch_k1_b(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int mode,
-                              int ch, hipStream_t s) {
-    if (ch <= 8) return launch_k1_t<BMAX, 8>(g, k, fp, nf, mode, s);
-    if (ch <= 16) return launch_k1_t<BMAX, 16>(g, k, fp, nf, mode, s);
-    return launch_k1_t<BMAX, 32>(g, k, fp, nf, mode, s);
+                              hipStream_t s) {
+    if (g.C <= 8) return launch_k1_t<T, BMAX, 8>(g, k, fp, nf, mode, s);
+    if (g.C <= 16) return launch_k1_t<T, BMAX, 16>(g, k, fp, nf, mode, s);
+    return launch_k1_t<T, BMAX, 32>(g, k, fp, nf, mode, s);
 }
 
-hipError_t launch_k1(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int mode, int,
-                     hipStream_t s) {
-    if (g.B <= 4) return launch_k1_b<4>(g, k, fp, nf, mode, g.C, s);
-    if (g.B <= 8) return launch_k1_b<8>(g, k, fp, nf, mode, g.C, s);
-    return launch_k1_b<16>(g, k, fp, nf, mode, g.C, s);
+template <class T>
+static hipError_t launch_k1_p(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int mode,
+                              hipStream_t s) {
+    if (g.B <= 4) return launch_k1_b<T, 4>(g, k, fp, nf, mode, s);
+    if (g.B <= 8) return launch_k1_b<T, 8>(g, k, fp, nf, mode, s);
+    return launch_k1_b<T, 16>(g, k, fp, nf, mode, s);
 }
 
-hipError_t launch_k2(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int rows,
-                     hipStream_t s) {
+hipError_t launch_k1(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int mode, hipStream_t s) {
+    return g.prec == RSP_PREC_F64 ? launch_k1_p<double>(g, k, fp, nf, mode, s)
+                                  : launch_k1_p<float>(g, k, fp, nf, mode, s);
+}
+
+template <class T>
+static hipError_t launch_k2_p(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int rows,
+                              hipStream_t s) {
+    const size_t lds = (size_t)K2_LDS_DATA(k2_sh<T>()) * sizeof(cx<T>);
+    hipError_t e = allow_lds(k2_pc<T>, lds);
+    if (e != hipSuccess) return e;
+    if (g.nwg_k2 > 0) hipLaunchKernelGGL(k2_pc<T>, dim3(g.nwg_k2, nf), dim3(K2_THREADS), lds, s, g, k, fp, rows);
+    return hipGetLastError();
+}
+
+hipError_t launch_k2(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int rows, hipStream_t s) {
+    return g.prec == RSP_PREC_F64 ? launch_k2_p<double>(g, k, fp, nf, rows, s)
+                                  : launch_k2_p<float>(g, k, fp, nf, rows, s);
+}
+
+template <class T>
+static hipError_t launch_k3_p(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, hipStream_t s) {
+    const size_t lds = (size_t)g.P * g.cfar_W * sizeof(T) + (K3_QCAP + 4) * sizeof(int);
+    const dim3 grid(k3_ntiles(g) * (g.B - 1) * nf);   // 1-D; k3_cfar remaps it XCD-aware
     hipError_t e;
-    const size_t lds_g = (size_t)(RSP_K2_POINTS + RSP_K2_POINTS / 16) * sizeof(float2);
-    const size_t lds_l = (size_t)(K2_LDS_DATA + ((g.dbg & 256) ? K2_LDS_TW : K2_LDS_TW_CMP)) * sizeof(float2);
-    // twiddles read in place from global memory (L1/L2), or (dbg 64) copied to LDS; tables in
-    // compact rows, or (dbg 256, built so by the plan) full rows.  Default = the fastest
-    // measured (profiles/).
-#define K2_LAUNCH(TWG, CMP, LDS)                                                                     \
-    do {                                                                                             \
-        if ((e = allow_lds(k2_pc<TWG, CMP>, LDS)) != hipSuccess) return e;                           \
-        if (g.nwg_k2_pow2 > 0)                                                                       \
-            hipLaunchKernelGGL((k2_pc<TWG, CMP>), dim3(g.nwg_k2_pow2, nf), dim3(K2_THREADS), LDS, s, g, k, fp, rows); \
-    } while (0)
-    switch (g.dbg & (64 | 256)) {
-        case 0: K2_LAUNCH(true, true, lds_g); break;
-        case 64: K2_LAUNCH(false, true, lds_l); break;
-        case 256: K2_LAUNCH(true, false, lds_g); break;
-        default: K2_LAUNCH(false, false, lds_l); break;
-    }
-#undef K2_LAUNCH
-    if (g.nwg_k2 > g.nwg_k2_pow2) {   // mixed-radix jobs (RSP_K2_MIXED=2): their own 320-thread launch
-        const SegDesc& sd = g.segs[g.jobs[g.mix_job0].seg];
-        const size_t lds = (size_t)2 * (sd.mixM + (sd.mixM >> K2_SH)) * sizeof(float2);
-        const dim3 grid(g.nwg_k2 - g.nwg_k2_pow2, nf);
-#define K2M_LAUNCH(M, RA, RB, RC)                                                                    \
-    do {                                                                                             \
-        if ((e = allow_lds(k2m_pc<M, RA, RB, RC>, lds)) != hipSuccess) return e;                     \
-        hipLaunchKernelGGL((k2m_pc<M, RA, RB, RC>), grid, dim3(K2M_THREADS), lds, s, g, k, fp, rows); \
-    } while (0)
-        switch (sd.mixM) {
-            case 640: K2M_LAUNCH(640, 8, 8, 10); break;
-            case 1280: K2M_LAUNCH(1280, 16, 8, 10); break;
-            default: K2M_LAUNCH(2560, 16, 16, 10); break;
-        }
-#undef K2M_LAUNCH
+    if (g.refR == 5 && g.refV == 5 && g.guardR == 10 && g.guardV == 10) {   // the reference's cfar_params (v8:45-46)
+        if ((e = allow_lds(k3_cfar<T, 5, 5, 10, 10>, lds)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k3_cfar<T, 5, 5, 10, 10>), grid, dim3(RSP_THREADS), lds, s, g, k, fp);
+    } else {
+        if ((e = allow_lds(k3_cfar<T, 0, 0, 0, 0>, lds)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k3_cfar<T, 0, 0, 0, 0>), grid, dim3(RSP_THREADS), lds, s, g, k, fp);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_k3(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, hipStream_t s) {
     if (g.B < 2 || g.G - 2 * (g.refR + g.guardR) <= 0) return hipSuccess;
-    const size_t lds = (size_t)g.P * g.cfar_W * sizeof(float) + (K3_QCAP + 4) * sizeof(int);
-    const dim3 grid(k3_ntiles(g) * (g.B - 1) * nf);   // 1-D; k3_cfar remaps it XCD-aware
-    hipError_t e;
-    if (g.refR == 5 && g.refV == 5 && g.guardR == 10 && g.guardV == 10) {   // the reference's cfar_params (v8:45-46)
-        if ((e = allow_lds(k3_cfar<5, 5, 10, 10>, lds)) != hipSuccess) return e;
-        hipLaunchKernelGGL((k3_cfar<5, 5, 10, 10>), grid, dim3(RSP_THREADS), lds, s, g, k, fp);
-    } else {
-        if ((e = allow_lds(k3_cfar<0, 0, 0, 0>, lds)) != hipSuccess) return e;
-        hipLaunchKernelGGL((k3_cfar<0, 0, 0, 0>), grid, dim3(RSP_THREADS), lds, s, g, k, fp);
-    }
-    return hipGetLastError();
+    return g.prec == RSP_PREC_F64 ? launch_k3_p<double>(g, k, fp, nf, s) : launch_k3_p<float>(g, k, fp, nf, s);
 }
 
-template <int LGP>
-static hipError_t launch_mtd_t(const Geometry& g, const DevConsts& k, const float2* pc, float2* rdm, hipStream_t s) {
-    const size_t lds = ((size_t)16 * g.Ppad + g.P) * sizeof(float2);
-    hipError_t e = allow_lds(k_mtd_cols<LGP>, lds);
+template <class T, int LGP>
+static hipError_t launch_mtd_t(const Geometry& g, const DevConsts& k, const void* pc, void* rdm, hipStream_t s) {
+    const size_t lds = ((size_t)16 * g.Ppad + g.P) * sizeof(cx<T>);
+    hipError_t e = allow_lds(k_mtd_cols<T, LGP>, lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_mtd_cols<LGP>, dim3((g.G + 15) / 16, g.B), dim3(RSP_THREADS), lds, s, g, k, pc, rdm);
+    hipLaunchKernelGGL((k_mtd_cols<T, LGP>), dim3((g.G + 15) / 16, g.B), dim3(RSP_THREADS), lds, s, g, k,
+                       static_cast<const cx<T>*>(pc), static_cast<cx<T>*>(rdm));
     return hipGetLastError();
 }
 
-hipError_t launch_mtd_cols(const Geometry& g, const DevConsts& k, const float2* pc, float2* rdm, hipStream_t s) {
+template <class T>
+static hipError_t launch_mtd_p(const Geometry& g, const DevConsts& k, const void* pc, void* rdm, hipStream_t s) {
     switch (g.pow2P ? g.logP : 0) {
-        case 4: return launch_mtd_t<4>(g, k, pc, rdm, s);
-        case 5: return launch_mtd_t<5>(g, k, pc, rdm, s);
-        case 6: return launch_mtd_t<6>(g, k, pc, rdm, s);
-        case 7: return launch_mtd_t<7>(g, k, pc, rdm, s);
-        case 8: return launch_mtd_t<8>(g, k, pc, rdm, s);
-        case 9: return launch_mtd_t<9>(g, k, pc, rdm, s);
-        default: return launch_mtd_t<0>(g, k, pc, rdm, s);
+        case 4: return launch_mtd_t<T, 4>(g, k, pc, rdm, s);
+        case 5: return launch_mtd_t<T, 5>(g, k, pc, rdm, s);
+        case 6: return launch_mtd_t<T, 6>(g, k, pc, rdm, s);
+        case 7: return launch_mtd_t<T, 7>(g, k, pc, rdm, s);
+        case 8: return launch_mtd_t<T, 8>(g, k, pc, rdm, s);
+        case 9: return launch_mtd_t<T, 9>(g, k, pc, rdm, s);
+        default: return launch_mtd_t<T, 0>(g, k, pc, rdm, s);
     }
+}
+
+hipError_t launch_mtd_cols(const Geometry& g, const DevConsts& k, const void* pc, void* rdm, hipStream_t s) {
+    return g.prec == RSP_PREC_F64 ? launch_mtd_p<double>(g, k, pc, rdm, s) : launch_mtd_p<float>(g, k, pc, rdm, s);
 }
 
 hipError_t launch_synth(const Geometry& g, const double* tx, const SynthTarget* tg, int nt, int frame_idx,
-                        uint64_t seed, double nscale, float2* cube, hipStream_t s) {
+                        uint64_t seed, double nscale, void* cube, hipStream_t s) {
     const size_t total = (size_t)g.P * g.N * g.C;
     const unsigned blocks = (unsigned)((total + RSP_THREADS - 1) / RSP_THREADS);
-    hipLaunchKernelGGL(k_synth, dim3(blocks), dim3(RSP_THREADS), 0, s, g, tx, tg, nt, frame_idx, seed, nscale,
-                       cube);
+    if (g.prec == RSP_PREC_F64)
+        hipLaunchKernelGGL(k_synth<double>, dim3(blocks), dim3(RSP_THREADS), 0, s, g, tx, tg, nt, frame_idx, seed,
+                           nscale, static_cast<d2*>(cube));
+    else
+        hipLaunchKernelGGL(k_synth<float>, dim3(blocks), dim3(RSP_THREADS), 0, s, g, tx, tg, nt, frame_idx, seed,
+                           nscale, static_cast<f2*>(cube));
     return hipGetLastError();
 }

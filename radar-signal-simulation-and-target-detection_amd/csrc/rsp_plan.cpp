@@ -91,6 +91,14 @@ void fft_d(std::vector<cd>& a, int sign) {
     }
 }
 
+// exp(-2 pi i e / n) with e reduced mod n and the angle formed in long double
+cd root_of_unity(long long e, long long n) {
+    e %= n;
+    if (e < 0) e += n;
+    const long double a = -2.0L * 3.141592653589793238462643383279502884L * (long double)e / (long double)n;
+    return cd((double)std::cos(a), (double)std::sin(a));
+}
+
 // Radix sequence for a 2^m-point Stockham FFT: radix 16 passes, remainder as 8/4
 // (never a lone radix-2 pass unless m == 1).
 void radix_plan(int m, int* nrad, int* rad) {
@@ -104,8 +112,10 @@ void radix_plan(int m, int* nrad, int* rad) {
 
 // Per-pass Stockham twiddle tables of a 2^m-point FFT (radix order reversed if rev),
 // concatenated: pass q >= 1 owns Ns_q x (R_q - 1) entries T[k][r-1] = exp(-2 pi i k r / (Ns_q R_q))
-// (must match tw_pass_off() in rsp_kernels.hip).
-void build_pass_twiddles(int m, std::vector<float2>& out, bool rev = false, bool cmp = false) {
+// (must match tw_pass_off() in rsp_kernels.hip).  Compact rows (cmp): r = 1, 2, 4, 8 only.
+// The angle's numerator is reduced modulo the period first, so every entry is the correctly
+// rounded double of the exact root of unity's angle.
+void build_pass_twiddles(int m, std::vector<cd>& out, bool rev = false, bool cmp = false) {
     int nrad, rad[8];
     radix_plan(m, &nrad, rad);
     if (rev) std::reverse(rad, rad + nrad);
@@ -114,61 +124,21 @@ void build_pass_twiddles(int m, std::vector<float2>& out, bool rev = false, bool
         const int R = rad[q];
         if (q > 0)
             for (int k = 0; k < Ns; ++k)
-                for (int r = 1; r < R; r = cmp ? 2 * r : r + 1) {   // compact rows: r = 1, 2, 4, 8
-                    const double a = -2.0 * M_PI * (double)k * r / ((double)Ns * R);
-                    out.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
-                }
+                for (int r = 1; r < R; r = cmp ? 2 * r : r + 1) out.push_back(root_of_unity((long long)k * r, (long long)Ns * R));
         Ns *= R;
     }
-}
-
-// RSP_K2_MIXED: 0 (default) power-of-two blocks only; 1 = 5 * 2^k blocks inside k2_pc (256
-// threads, one 2560 row); 2 = those jobs in their own k2m_pc launch (320 threads, two rows).
-int k2_mixed_mode() {
-    const char* mx = getenv("RSP_K2_MIXED");
-    return mx ? std::max(0, std::min(2, atoi(mx))) : 0;
-}
-
-// Mixed-radix plans (k2m_fft_job): M -> forward radices (RA, RB, RC); inverse reversed.
-bool mixed_plan(int M, int* ra, int* rb, int* rc) {
-    switch (M) {
-        case 640: *ra = 8; *rb = 8; *rc = 10; return true;
-        case 1280: *ra = 16; *rb = 8; *rc = 10; return true;
-        case 2560: *ra = 16; *rb = 16; *rc = 10; return true;
-        default: return false;
-    }
-}
-
-// Compact twiddle tables of a mixed plan (must match twm_fwd() / k2m_fft_job in
-// rsp_kernels.hip): forward pass 1 (Ns = RA, R = RB), pass 2 (Ns = RA RB, R = RC), then inverse
-// pass 1 (Ns = RC, R = RB), pass 2 (Ns = RC RB, R = RA); row k holds W_{Ns R}^(k 2^i), 2^i < R.
-void build_mixed_twiddles(int M, std::vector<float2>& out) {
-    int ra, rb, rc;
-    mixed_plan(M, &ra, &rb, &rc);
-    const int ns[4] = {ra, ra * rb, rc, rc * rb}, rr[4] = {rb, rc, rb, ra};
-    for (int q = 0; q < 4; ++q)
-        for (int k = 0; k < ns[q]; ++k)
-            for (int r = 1; r < rr[q]; r *= 2) {
-                const long long e = ((long long)k * r) % ((long long)ns[q] * rr[q]);
-                const double a = -2.0 * M_PI * (double)e / ((double)ns[q] * rr[q]);
-                out.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
-            }
 }
 
 double mround(double x) { return x < 0 ? -std::floor(-x + 0.5) : std::floor(x + 0.5); }
 
 struct Lane {
-    hipStream_t stream = nullptr;   // the lane's own stream: detection read-back, synchronous paths
-    hipStream_t ks = nullptr;       // where the lane's K1-K3 run: the plan's shared kernel stream, or `stream`
-    hipEvent_t kdone = nullptr;     // K3 of the lane's batch done (on ks)
-    hipEvent_t ready = nullptr;     // work queued on `stream` before the batch (uploads), awaited by ks
-    hipEvent_t k1done = nullptr;    // K1 of the lane's batch done (pipelined queue: on the plan's K1 stream)
-    hipEvent_t tev[4] = {};         // live stage timing: before K1, after K1, K2, K3 (on ks)
+    hipStream_t stream = nullptr;   // the lane's stream: its batches' kernels and detection read-back
+    hipEvent_t tev[4] = {};         // live stage timing: before K1, after K1, K2, K3
     bool timed = false;
     hipEvent_t done = nullptr;
-    float2* z = nullptr;        // F frames
-    float2* rdm = nullptr;      // F frames
-    float* mag = nullptr;       // F frames
+    void* z = nullptr;          // F frames
+    void* rdm = nullptr;        // F frames
+    void* mag = nullptr;        // F frames
     DevDet* dets = nullptr;     // F x (1 + max_dets): record 0 of each frame holds its count
     DevDet* h_dets = nullptr;   // pinned F x (1 + async_cap), same layout
     int nf = 0;
@@ -194,51 +164,48 @@ struct rsp_plan {
     double p_signal_unscaled = 0, c = 0, fs = 0, wavelength = 0, d = 0, prt = 0;
     int F = 1;
     int async_cap = 512;
+    size_t esz = 16;   // bytes of one complex element (16: complex128, 8: complex64)
+    size_t rsz = 8;    // bytes of one real element
     size_t z_elems = 0, rdm_elems = 0, mag_elems = 0;
     std::vector<SegDesc> segs;
     std::vector<K2Job> jobs;
     std::vector<void*> dev_allocs;
     double* d_tx = nullptr;
     SynthTarget* d_tg = nullptr;
-    float2* d_cube = nullptr;     // staging cube for the synchronous paths
-    float2* d_aux = nullptr;      // second map for the stage-2 path
-    float2* h_stage = nullptr;    // pinned staging for uploads
+    void* d_cube = nullptr;       // staging cube for the synchronous paths
+    void* d_aux = nullptr;        // second map for the stage-2 path
+    void* d_smap = nullptr;       // rdm_for_cfar_all of the synchronous path (allocated on first request)
+    unsigned char* h_stage = nullptr;   // pinned staging for uploads
     size_t h_stage_bytes = 0;
     Lane lanes[RSP_LANES];
-    int nlanes = 3;   // lanes in use (RSP_NLANES, 1..RSP_LANES)
+    int nlanes = 3;   // lanes (streams) of the throughput queue
     int next_lane = 0;
-    // Throughput queue.  Default: each lane runs its batch (K1-K3 + read-back) on its own
-    // stream, so consecutive batches overlap on the device (one batch's kernel tail fills with
-    // the next batch's workgroups: 52 vs 59 us/frame at x2, F = 4, measured).  RSP_QUEUE=serial:
-    // all batches run back to back on ONE kernel stream (every kernel has the chip to itself)
-    // while the lanes' streams carry the read-back.
-    hipStream_t kstream = nullptr;
-    // RSP_QUEUE=pipe: every K1 runs on one K1 stream and each lane's K2/K3 wait for their K1, so
-    // K1 of batch i+1 (HBM-bound) runs beside K2/K3 of batch i (VALU-bound)
-    hipStream_t k1stream = nullptr;
-    // K1 + K2 run in sub-batches of this many frames inside a larger batch (RSP_K12_SUB; 0 = off)
-    int k12_sub = 0;
     // live stage timing of the queue (rsp_set_stage_timing): HIP events around K1/K2/K3 of
     // every batch, summed at harvest
     bool time_stages = false;
     double stage_ms[3] = {0, 0, 0};
     int64_t stage_launches = 0, stage_frames = 0;
     // pending batch of the queue
-    const float2* pend_in[RSP_MAX_F];
+    const void* pend_in[RSP_MAX_F];
     int pend_ids[RSP_MAX_F];
     int npend = 0;
     std::deque<FrameResult> results;
     bool overflow_seen = false;
 
     ~rsp_plan();
+    int dalloc_bytes(void** p, size_t bytes) {
+        void* q = nullptr;
+        if (hipMalloc(&q, bytes + 16) != hipSuccess) return fail(RSP_ERR_NOMEM, "hipMalloc(%zu bytes) failed", bytes);
+        dev_allocs.push_back(q);
+        *p = q;
+        return RSP_OK;
+    }
     template <class T>
     int dalloc(T** p, size_t n) {
         void* q = nullptr;
-        if (hipMalloc(&q, n * sizeof(T) + 16) != hipSuccess)
-            return fail(RSP_ERR_NOMEM, "hipMalloc(%zu bytes) failed", n * sizeof(T));
-        dev_allocs.push_back(q);
+        int rc = dalloc_bytes(&q, n * sizeof(T));
         *p = (T*)q;
-        return RSP_OK;
+        return rc;
     }
     template <class T>
     int upload(T** p, const std::vector<T>& h) {
@@ -247,25 +214,48 @@ struct rsp_plan {
         if (!h.empty()) HIPCHK(hipMemcpy(*p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
         return RSP_OK;
     }
+    // complex / real tables in the plan's precision
+    int upload_c(const void** p, const std::vector<cd>& h) {
+        if (g.prec == RSP_PREC_F64) {
+            double* q;
+            std::vector<double> v(2 * h.size());
+            for (size_t i = 0; i < h.size(); ++i) { v[2 * i] = h[i].real(); v[2 * i + 1] = h[i].imag(); }
+            int rc = upload(&q, v);
+            *p = q;
+            return rc;
+        }
+        float* q;
+        std::vector<float> v(2 * h.size());
+        for (size_t i = 0; i < h.size(); ++i) { v[2 * i] = (float)h[i].real(); v[2 * i + 1] = (float)h[i].imag(); }
+        int rc = upload(&q, v);
+        *p = q;
+        return rc;
+    }
+    int upload_r(const void** p, const std::vector<double>& h) {
+        if (g.prec == RSP_PREC_F64) {
+            double* q;
+            int rc = upload(&q, h);
+            *p = q;
+            return rc;
+        }
+        float* q;
+        std::vector<float> v(h.begin(), h.end());
+        int rc = upload(&q, v);
+        *p = q;
+        return rc;
+    }
 };
 
 rsp_plan::~rsp_plan() {
     (void)hipSetDevice(device);
-    if (kstream) (void)hipStreamSynchronize(kstream);
-    if (k1stream) (void)hipStreamSynchronize(k1stream);
     for (auto& L : lanes) {
         if (L.stream) (void)hipStreamSynchronize(L.stream);
         if (L.h_dets) (void)hipHostFree(L.h_dets);
         if (L.done) (void)hipEventDestroy(L.done);
-        if (L.kdone) (void)hipEventDestroy(L.kdone);
-        if (L.ready) (void)hipEventDestroy(L.ready);
-        if (L.k1done) (void)hipEventDestroy(L.k1done);
         for (auto& e : L.tev)
             if (e) (void)hipEventDestroy(e);
         if (L.stream) (void)hipStreamDestroy(L.stream);
     }
-    if (kstream) (void)hipStreamDestroy(kstream);
-    if (k1stream) (void)hipStreamDestroy(k1stream);
     if (h_stage) (void)hipHostFree(h_stage);
     for (void* p : dev_allocs) (void)hipFree(p);
 }
@@ -357,8 +347,8 @@ void cluster_frame(const rsp_cluster_params& cp, std::vector<rsp_detection>& det
 struct Interval { int lo, hi; };
 
 int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga, int gb, int seg_lo,
-                      std::vector<float2>& H, std::vector<float2>& twM, std::vector<int>& tw_sizes,
-                      std::vector<int>& tw_offs, const char* name, bool cmp) {
+                      std::vector<cd>& H, std::vector<cd>& twM, std::vector<int>& tw_sizes, std::vector<int>& tw_offs,
+                      const char* name) {
     std::vector<cd> h(Nfft);
     for (int i = 0; i < Nfft; ++i) h[i] = cd(mf_fft[2 * i], mf_fft[2 * i + 1]);
     fft_d(h, +1);
@@ -377,68 +367,36 @@ int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga,
     s.Lh = Lh;
     s.lo = std::max(seg_lo, seg_lo + ga - (Lh - 1));
     s.hi = std::min(seg_lo + Ls - 1, seg_lo + gb - 1);
-    // overlap-save block size: minimise blocks * M * (log2 M + 2), M <= 2048 so that a
-    // workgroup owns >= 2 adjacent rows (128 B contiguous loads of z)
+    // overlap-save block size M = 2^k <= 2048 (so that a workgroup owns >= 2 adjacent rows:
+    // 128 B contiguous loads of z); cost model blocks * M * (log2 M + 2)
     const int nout = gb - ga;
     double best = 1e300;
     int bestM = 0;
-    // candidates: 2^k (k2_fft_job) and, opt-in with RSP_K2_MIXED=1 (compact twiddles), 5 * 2^k
-    // (k2m_fft_job; 640 / 1280 / 2560, e.g. the x2 long segment: one 2560 block instead of two
-    // 2048 blocks, 37% fewer points).  Off by default: with 256 threads per workgroup the radix-16
-    // passes of a 2560 row keep 160 threads busy and the workgroup takes 12.5 us against 11.5 us
-    // for the 2 x 2048 rows it replaces (measured).  Cost model:
-    // blocks * M * (log2 M + 2).
-    const int mixed_mode = k2_mixed_mode();   // 0 off, 1 inside k2_pc, 2 own 320-thread launch
-    const bool allow_mixed = cmp && mixed_mode > 0;
-    const int cand[] = {64, 128, 256, 512, 640, 1024, 1280, 2048, 2560};
-    for (int M : cand) {
-        int ra, rb, rc;
-        const bool mixed = mixed_plan(M, &ra, &rb, &rc);
-        if (mixed && !allow_mixed) continue;
+    for (int M = 64; M <= 2048; M *= 2) {
         const int V = M - Lh + 1;
         if (V < 1) continue;
         const int nb = (nout + V - 1) / V;
         const double cost = (double)nb * M * (std::log2((double)M) + 2);
         if (cost < best * 0.999) { best = cost; bestM = M; }
     }
-    if (!bestM) return fail(RSP_ERR_UNSUPPORTED, "%s filter length %d exceeds the 2560-point block", name, Lh);
+    if (!bestM) return fail(RSP_ERR_UNSUPPORTED, "%s filter length %d exceeds the 2048-point block", name, Lh);
     const int M = bestM;
-    int ra, rb, rc;
-    const bool mixed = mixed_plan(M, &ra, &rb, &rc);
-    s.M = M; s.mixM = mixed ? M : 0; s.logM = mixed ? 0 : ilog2i(M); s.V = M - Lh + 1;
+    s.M = M; s.logM = ilog2i(M); s.V = M - Lh + 1;
     s.nblocks = (nout + s.V - 1) / s.V;
-    s.rows_per_wg = mixed ? (mixed_mode == 2 ? 2 : K2M_POINTS_HOST / M) : RSP_K2_POINTS / M;
-    if (!mixed) radix_plan(s.logM, &s.nrad, s.rad);
+    s.rows_per_wg = RSP_K2_POINTS / M;
     // spectrum of h zero-padded to M, natural order, 1/M folded in
     std::vector<cd> hm(M, 0.0);
     for (int i = 0; i < Lh; ++i) hm[i] = h[i];
-    if (mixed) {   // direct DFT (M not a power of two; Lh taps, once per plan)
-        std::vector<cd> out(M, 0.0);
-        for (int f = 0; f < M; ++f) {
-            cd acc = 0.0;
-            for (int i = 0; i < Lh; ++i) {
-                const long long e = ((long long)f * i) % M;
-                acc += hm[i] * std::polar(1.0, -2.0 * M_PI * (double)e / M);
-            }
-            out[f] = acc;
-        }
-        hm = out;
-    } else {
-        fft_d(hm, -1);
-    }
+    fft_d(hm, -1);
     s.H_off = (int)H.size();
-    for (auto& v : hm) { v /= (double)M; H.push_back(make_float2((float)v.real(), (float)v.imag())); }
+    for (auto& v : hm) H.push_back(v / (double)M);
     int ti = -1;
     for (size_t q = 0; q < tw_sizes.size(); ++q) if (tw_sizes[q] == M) ti = (int)q;
     if (ti < 0) {
         tw_sizes.push_back(M);
         tw_offs.push_back((int)twM.size());
-        if (mixed) {
-            build_mixed_twiddles(M, twM);
-        } else {
-            build_pass_twiddles(s.logM, twM, false, cmp);   // forward FFT
-            build_pass_twiddles(s.logM, twM, true, cmp);    // inverse FFT (reversed radices)
-        }
+        build_pass_twiddles(s.logM, twM, false, true);   // forward FFT, compact rows
+        build_pass_twiddles(s.logM, twM, true, true);    // inverse FFT (reversed radices)
         ti = (int)tw_sizes.size() - 1;
     }
     s.tw_off = tw_offs[ti];
@@ -448,27 +406,23 @@ int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga,
 int setup_lane(rsp_plan* p, Lane& L) {
     HIPCHK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&L.done, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&L.kdone, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&L.ready, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&L.k1done, hipEventDisableTiming));
     for (auto& e : L.tev) HIPCHK(hipEventCreate(&e));
-    L.ks = p->kstream ? p->kstream : L.stream;
     int rc;
-    if ((rc = p->dalloc(&L.z, p->z_elems * p->F))) return rc;
-    if ((rc = p->dalloc(&L.rdm, p->rdm_elems * p->F))) return rc;
-    if ((rc = p->dalloc(&L.mag, p->mag_elems * p->F))) return rc;
+    if ((rc = p->dalloc_bytes(&L.z, p->z_elems * p->F * p->esz))) return rc;
+    if ((rc = p->dalloc_bytes(&L.rdm, p->rdm_elems * p->F * p->esz))) return rc;
+    if ((rc = p->dalloc_bytes(&L.mag, p->mag_elems * p->F * p->rsz))) return rc;
     if ((rc = p->dalloc(&L.dets, (size_t)(p->g.max_dets + 1) * p->F))) return rc;
     HIPCHK(hipHostMalloc((void**)&L.h_dets, sizeof(DevDet) * (p->async_cap + 1) * p->F, hipHostMallocDefault));
     return RSP_OK;
 }
 
-FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const float2* const* in, int nf) {
+FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const void* const* in, int nf) {
     FramePtrs fp{};
     for (int f = 0; f < nf; ++f) {
         fp.in[f] = in[f];
-        fp.z[f] = L.z + p->z_elems * f;
-        fp.rdm[f] = L.rdm + p->rdm_elems * f;
-        fp.mag[f] = L.mag + p->mag_elems * f;
+        fp.z[f] = (char*)L.z + p->z_elems * p->esz * f;
+        fp.rdm[f] = (char*)L.rdm + p->rdm_elems * p->esz * f;
+        fp.mag[f] = (char*)L.mag + p->mag_elems * p->rsz * f;
         DevDet* rec = L.dets + (size_t)(p->g.max_dets + 1) * f;
         fp.count[f] = reinterpret_cast<int*>(rec);   // zeroed by K1, bumped by K3
         fp.dets[f] = rec + 1;
@@ -476,60 +430,19 @@ FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const float2* const* in, i
     return fp;
 }
 
-// Frames [off, off + n) of fp as a batch of their own.
-FramePtrs sub_ptrs(const FramePtrs& fp, int off, int n) {
-    FramePtrs s{};
-    s.trace = fp.trace;
-    for (int f = 0; f < n; ++f) {
-        s.in[f] = fp.in[off + f];
-        s.z[f] = fp.z[off + f];
-        s.rdm[f] = fp.rdm[off + f];
-        s.mag[f] = fp.mag[off + f];
-        s.dets[f] = fp.dets[off + f];
-        s.count[f] = fp.count[off + f];
-    }
-    return s;
-}
-
 // Enqueue K1 -> K2 -> K3 for nf frames on lane L, plus the async detection read-back.
-int launch_batch(rsp_plan* p, Lane& L, const float2* const* in, const int* ids, int nf, bool after_stream = false) {
-    const FramePtrs fp = lane_ptrs(p, L, in, nf);
-    if (after_stream && L.ks != L.stream) {   // kernels follow whatever the caller queued on the lane's stream
-        HIPCHK(hipEventRecord(L.ready, L.stream));
-        HIPCHK(hipStreamWaitEvent(L.ks, L.ready, 0));
-    }
+// smap (optional, one frame): K3 also writes rdm_for_cfar_all there.
+int launch_batch(rsp_plan* p, Lane& L, const void* const* in, const int* ids, int nf, void* smap = nullptr) {
+    FramePtrs fp = lane_ptrs(p, L, in, nf);
+    fp.smap[0] = smap;
     L.timed = p->time_stages;
-    if (L.timed) HIPCHK(hipEventRecord(L.tev[0], L.ks));
-    if (p->k1stream && !L.timed) {
-        // K1 on the plan's K1 stream after whatever the lane queued (the lane's previous batch
-        // was harvested before this launch, so its z buffer is free); K2 waits for this K1
-        HIPCHK(hipEventRecord(L.ready, L.stream));
-        HIPCHK(hipStreamWaitEvent(p->k1stream, L.ready, 0));
-        HIPCHK(launch_k1(p->g, p->k, fp, nf, 3, p->g.C, p->k1stream));
-        HIPCHK(hipEventRecord(L.k1done, p->k1stream));
-        HIPCHK(hipStreamWaitEvent(L.ks, L.k1done, 0));
-    } else if (!L.timed && p->k12_sub > 0 && nf > p->k12_sub) {
-        // K1 + K2 in sub-batches (each sub-batch's z is still in the Infinity Cache when K2 reads
-        // it), then one K3 over the whole batch (fewer tail rounds)
-        for (int f0 = 0; f0 < nf; f0 += p->k12_sub) {
-            const int n = std::min(p->k12_sub, nf - f0);
-            const FramePtrs sp = sub_ptrs(fp, f0, n);
-            HIPCHK(launch_k1(p->g, p->k, sp, n, 3, p->g.C, L.ks));
-            HIPCHK(launch_k2(p->g, p->k, sp, n, p->g.B * p->g.P, L.ks));
-        }
-    } else {
-        HIPCHK(launch_k1(p->g, p->k, fp, nf, 3, p->g.C, L.ks));
-    }
-    if (L.timed) HIPCHK(hipEventRecord(L.tev[1], L.ks));
-    if (L.timed || p->k1stream || p->k12_sub <= 0 || nf <= p->k12_sub)
-        HIPCHK(launch_k2(p->g, p->k, fp, nf, p->g.B * p->g.P, L.ks));
-    if (L.timed) HIPCHK(hipEventRecord(L.tev[2], L.ks));
-    HIPCHK(launch_k3(p->g, p->k, fp, nf, L.ks));
-    if (L.timed) HIPCHK(hipEventRecord(L.tev[3], L.ks));
-    if (L.ks != L.stream) {   // read-back on the lane's stream, off the kernel stream
-        HIPCHK(hipEventRecord(L.kdone, L.ks));
-        HIPCHK(hipStreamWaitEvent(L.stream, L.kdone, 0));
-    }
+    if (L.timed) HIPCHK(hipEventRecord(L.tev[0], L.stream));
+    HIPCHK(launch_k1(p->g, p->k, fp, nf, 3, L.stream));
+    if (L.timed) HIPCHK(hipEventRecord(L.tev[1], L.stream));
+    HIPCHK(launch_k2(p->g, p->k, fp, nf, p->g.B * p->g.P, L.stream));
+    if (L.timed) HIPCHK(hipEventRecord(L.tev[2], L.stream));
+    HIPCHK(launch_k3(p->g, p->k, fp, nf, L.stream));
+    if (L.timed) HIPCHK(hipEventRecord(L.tev[3], L.stream));
     // one copy: count record + the first async_cap detections of every frame
     HIPCHK(hipMemcpy2DAsync(L.h_dets, sizeof(DevDet) * (p->async_cap + 1), L.dets,
                             sizeof(DevDet) * (p->g.max_dets + 1), sizeof(DevDet) * (p->async_cap + 1), nf,
@@ -610,51 +523,94 @@ int ensure_stage(rsp_plan* p, size_t bytes) {
     return RSP_OK;
 }
 
-// Copy a host cube (any dtype) into d_dst as complex64.
-int upload_cube(rsp_plan* p, const void* cube, int dtype, int nch, float2* d_dst, hipStream_t s) {
+// Copy a host cube (complex64 or complex128, nch channel slabs of N x P) into d_dst in the
+// plan's precision (a converting copy only when the dtypes differ).
+int upload_cube(rsp_plan* p, const void* cube, int dtype, int nch, void* d_dst, hipStream_t s) {
+    if (dtype != RSP_C64 && dtype != RSP_C128) return fail(RSP_ERR_INVALID, "unknown dtype %d", dtype);
     const size_t slab = (size_t)p->g.N * p->g.P, elems = slab * nch;
-    int rc = ensure_stage(p, elems * sizeof(float2));
-    if (rc) return rc;
-    if (dtype == RSP_C64) {
-        memcpy(p->h_stage, cube, elems * sizeof(float2));
-    } else if (dtype == RSP_C128) {
-        const double* src = (const double*)cube;
-        for (size_t i = 0; i < elems; ++i) p->h_stage[i] = make_float2((float)src[2 * i], (float)src[2 * i + 1]);
-    } else {
-        return fail(RSP_ERR_INVALID, "unknown dtype %d", dtype);
+    const bool f64 = p->g.prec == RSP_PREC_F64;
+    const void* src = cube;
+    if ((dtype == RSP_C128) != f64) {
+        int rc = ensure_stage(p, elems * p->esz);
+        if (rc) return rc;
+        if (f64) {
+            const float* a = (const float*)cube;
+            double* o = (double*)p->h_stage;
+            for (size_t i = 0; i < 2 * elems; ++i) o[i] = a[i];
+        } else {
+            const double* a = (const double*)cube;
+            float* o = (float*)p->h_stage;
+            for (size_t i = 0; i < 2 * elems; ++i) o[i] = (float)a[i];
+        }
+        src = p->h_stage;
     }
-    HIPCHK(hipMemcpy2DAsync(d_dst, (size_t)p->g.cpitch * sizeof(float2), p->h_stage, slab * sizeof(float2),
-                            slab * sizeof(float2), nch, hipMemcpyHostToDevice, s));   // channel slabs at cpitch
+    HIPCHK(hipMemcpy2DAsync(d_dst, (size_t)p->g.cpitch * p->esz, src, slab * p->esz, slab * p->esz, nch,
+                            hipMemcpyHostToDevice, s));   // channel slabs at cpitch
+    HIPCHK(hipStreamSynchronize(s));   // the caller's buffer (or the staging buffer) is borrowed for the call
     return RSP_OK;
 }
 
-// [B][P][G] float maps -> MATLAB column-major [P x G x B] complex double
-void rdm_to_matlab(const rsp_plan* p, const std::vector<float2>& m, double* out) {
+// [B][P][G] complex device maps -> MATLAB column-major [P x G x B] complex double
+int rdm_to_matlab(rsp_plan* p, const void* d_map, double* out) {
     const int P = p->g.P, G = p->g.G, B = p->g.B;
+    const size_t n = p->rdm_elems;
+    std::vector<double> m(2 * n);
+    if (p->g.prec == RSP_PREC_F64) {
+        HIPCHK(hipMemcpy(m.data(), d_map, n * 16, hipMemcpyDeviceToHost));
+    } else {
+        std::vector<float> t(2 * n);
+        HIPCHK(hipMemcpy(t.data(), d_map, n * 8, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < 2 * n; ++i) m[i] = t[i];
+    }
     for (int b = 0; b < B; ++b)
         for (int v = 0; v < P; ++v)
             for (int r = 0; r < G; ++r) {
-                const float2 x = m[((size_t)b * P + v) * G + r];
+                const size_t i = ((size_t)b * P + v) * G + r;
                 const size_t o = (size_t)v + (size_t)P * ((size_t)r + (size_t)G * b);
-                out[2 * o] = x.x;
-                out[2 * o + 1] = x.y;
+                out[2 * o] = m[2 * i];
+                out[2 * o + 1] = m[2 * i + 1];
             }
+    return RSP_OK;
 }
 
-int run_sync_frame(rsp_plan* p, const float2* d_in, int frame_idx, rsp_frame_out* out) {
+// [B-1][P][G] real device maps (K3's S) -> MATLAB column-major [P x G x (B-1)] double
+int smap_to_matlab(rsp_plan* p, const void* d_map, double* out) {
+    const int P = p->g.P, G = p->g.G, NP = p->g.B - 1;
+    const size_t n = (size_t)NP * P * G;
+    std::vector<double> m(n);
+    if (p->g.prec == RSP_PREC_F64) {
+        HIPCHK(hipMemcpy(m.data(), d_map, n * 8, hipMemcpyDeviceToHost));
+    } else {
+        std::vector<float> t(n);
+        HIPCHK(hipMemcpy(t.data(), d_map, n * 4, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < n; ++i) m[i] = t[i];
+    }
+    for (int q = 0; q < NP; ++q)
+        for (int v = 0; v < P; ++v)
+            for (int r = 0; r < G; ++r)
+                out[(size_t)v + (size_t)P * ((size_t)r + (size_t)G * q)] = m[((size_t)q * P + v) * G + r];
+    return RSP_OK;
+}
+
+int run_sync_frame(rsp_plan* p, const void* d_in, int frame_idx, rsp_frame_out* out) {
     int rc = drain_all(p);
     if (rc) return rc;
     const size_t nres = p->results.size();
     Lane& L = p->lanes[0];
-    const float2* in[1] = {d_in};
+    const void* in[1] = {d_in};
     int ids[1] = {frame_idx};
     std::vector<std::vector<rsp_detection>> dets;
-    if ((rc = launch_batch(p, L, in, ids, 1, true))) return rc;
+    void* smap = nullptr;
+    if (out && out->cfar_maps && p->g.B > 1) {
+        if (!p->d_smap && (rc = p->dalloc_bytes(&p->d_smap, (size_t)(p->g.B - 1) * p->g.P * p->g.G * p->rsz))) return rc;
+        smap = p->d_smap;
+    }
+    if ((rc = launch_batch(p, L, in, ids, 1, smap))) return rc;
     if ((rc = harvest(p, L, &dets))) return rc;
     FrameResult fr = p->results.back();
     p->results.resize(nres);   // synchronous frames do not enter the queue's result list
-    if (fr.overflow) return fail(RSP_ERR_OVERFLOW, "frame %d: %d detections exceed capacity %d", frame_idx,
-                                 fr.n_dets, p->g.max_dets);
+    if (fr.overflow) return fail(RSP_ERR_OVERFLOW, "frame %d: detections exceed capacity %d (or > %d in one CFAR tile)",
+                                 frame_idx, p->g.max_dets, 1024);
     if (out) {
         std::vector<rsp_detection>& d = dets[0];
         out->n_dets = (int)d.size();
@@ -662,21 +618,8 @@ int run_sync_frame(rsp_plan* p, const float2* d_in, int frame_idx, rsp_frame_out
         out->n_targets = (int)fr.targets.size();
         if (out->targets)
             memcpy(out->targets, fr.targets.data(), sizeof(rsp_target) * std::min<int>(out->targets_cap, (int)fr.targets.size()));
-        if (out->rdm || out->cfar_maps) {
-            std::vector<float2> m(p->rdm_elems);
-            HIPCHK(hipMemcpy(m.data(), L.rdm, m.size() * sizeof(float2), hipMemcpyDeviceToHost));
-            if (out->rdm) rdm_to_matlab(p, m, out->rdm);
-            if (out->cfar_maps) {   // rdm_for_cfar_all (fsf:184-187)
-                const int P = p->g.P, G = p->g.G, B = p->g.B;
-                for (int b = 0; b + 1 < B; ++b)
-                    for (int v = 0; v < P; ++v)
-                        for (int r = 0; r < G; ++r) {
-                            const float2 a = m[((size_t)b * P + v) * G + r], c = m[((size_t)(b + 1) * P + v) * G + r];
-                            out->cfar_maps[(size_t)v + (size_t)P * ((size_t)r + (size_t)G * b)] =
-                                std::hypot((double)a.x, (double)a.y) + std::hypot((double)c.x, (double)c.y);
-                        }
-            }
-        }
+        if (out->rdm && (rc = rdm_to_matlab(p, L.rdm, out->rdm))) return rc;
+        if (smap && (rc = smap_to_matlab(p, smap, out->cfar_maps))) return rc;   // device-produced (fsf:184-187)
         if (out->dets && (int)d.size() > out->dets_cap)
             return fail(RSP_ERR_OVERFLOW, "%d detections exceed dets_cap %d", (int)d.size(), out->dets_cap);
         if (out->targets && (int)fr.targets.size() > out->targets_cap)
@@ -696,21 +639,48 @@ int32_t rsp_abi_version(void) { return RSP_ABI_VERSION; }
 const char* rsp_last_error(void) { return g_err.c_str(); }
 const char* rsp_stage_name(int32_t s) { return (s >= 0 && s < 3) ? kStageNames[s] : "?"; }
 
+int32_t rsp_plan_options_default(rsp_plan_options* o) {
+    if (!o) return fail(RSP_ERR_INVALID, "null argument");
+    o->device = 0;
+    o->frames_per_launch = 1;
+    o->precision = RSP_C128;
+    o->flags = 0;
+    return RSP_OK;
+}
+
 int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, const rsp_cluster_params* cluster,
                         const rsp_precomputed* pre, int32_t device, int32_t frames_per_launch, rsp_plan** out) {
-    if (!cfg || !cfar || !cluster || !pre || !out) return fail(RSP_ERR_INVALID, "null argument");
+    rsp_plan_options o;
+    rsp_plan_options_default(&o);
+    o.device = device;
+    o.frames_per_launch = frames_per_launch;
+    return rsp_plan_create_ex(cfg, cfar, cluster, pre, &o, out);
+}
+
+int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, const rsp_cluster_params* cluster,
+                           const rsp_precomputed* pre, const rsp_plan_options* opt, rsp_plan** out) {
+    if (!cfg || !cfar || !cluster || !pre || !opt || !out) return fail(RSP_ERR_INVALID, "null argument");
     *out = nullptr;
+    const int device = opt->device, frames_per_launch = opt->frames_per_launch;
+    if (opt->precision != RSP_C64 && opt->precision != RSP_C128)
+        return fail(RSP_ERR_INVALID, "precision must be RSP_C128 or RSP_C64, got %d", opt->precision);
+    if (opt->flags & ~RSP_PLAN_K1_TILED) return fail(RSP_ERR_INVALID, "unknown plan flags 0x%x", opt->flags);
     const int C = cfg->channel_num, B = cfg->beam_num, P = cfg->prtNum, N = cfg->point_PRT;
     const int g1 = pre->N_gate_narrow, g2 = pre->N_gate_medium, g3 = pre->N_gate_long, G = pre->N_total_gate;
     if (C < 1 || C > 32 || B < 1 || B > 16 || P < 2 || N < 2)
         return fail(RSP_ERR_INVALID, "bad sizes C=%d B=%d P=%d N=%d (1<=C<=32, 1<=B<=16)", C, B, P, N);
-    if (P % 2) return fail(RSP_ERR_UNSUPPORTED, "odd prtNum %d (pulse pairs are loaded as 16 B)", P);
+    if (P % 2) return fail(RSP_ERR_UNSUPPORTED, "odd prtNum %d (complex64 pulse pairs are loaded as 16 B)", P);
     if (g1 < 0 || g2 < 0 || g3 < 0 || G != g1 + g2 + g3 || G < 1) return fail(RSP_ERR_INVALID, "gate counts inconsistent");
     if (!pre->DBF_coeffs_data_C || !pre->MF_narrow || !pre->MF_medium_fft || !pre->MF_long_fft || !pre->MTD_win ||
         !pre->range_axis || !pre->velocity_axis || !pre->beam_angles_deg || (B > 1 && !pre->k_slopes_LUT))
         return fail(RSP_ERR_INVALID, "precomputed_data field missing");
     if (frames_per_launch < 1 || frames_per_launch > RSP_MAX_F)
         return fail(RSP_ERR_INVALID, "frames_per_launch must be 1..%d", RSP_MAX_F);
+    const bool f64 = opt->precision == RSP_C128;
+    const size_t esz = f64 ? 16 : 8;
+    if ((size_t)C * N * P * esz >= ((size_t)1 << 31))
+        return fail(RSP_ERR_UNSUPPORTED, "echo cube of %zu bytes: the kernels address one frame with 32-bit offsets (< 2 GB)",
+                    (size_t)C * N * P * esz);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RSP_ERR_DEVICE, "no HIP device available");
     if (device < 0 || device >= ndev) return fail(RSP_ERR_INVALID, "device %d out of range (%d devices)", device, ndev);
@@ -722,22 +692,24 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     p->cl = *cluster;
     p->c = cfg->c; p->fs = cfg->fs; p->wavelength = cfg->wavelength; p->d = cfg->element_spacing; p->prt = cfg->prt;
     p->p_signal_unscaled = pre->P_signal_unscaled;
+    p->esz = esz;
+    p->rsz = esz / 2;
     Geometry& g = p->g;
+    g.prec = f64 ? RSP_PREC_F64 : RSP_PREC_F32;
+    g.k1_tiled = (opt->flags & RSP_PLAN_K1_TILED) ? 1 : 0;
     g.C = C; g.B = B; g.P = P; g.N = N; g.G = G;
     g.cpitch = N * P;
-    if (const char* cp = getenv("RSP_CPAD")) g.cpitch += std::max(0, atoi(cp));   // timing experiments
     g.refR = cfar->refCells_R; g.guardR = cfar->guardCells_R; g.refV = cfar->refCells_V; g.guardV = cfar->guardCells_V;
-    g.T = (float)cfar->T_CFAR;
+    g.T = cfar->T_CFAR;
     g.max_dets = 1 << 16;
-    if (const char* ab = getenv("RSP_ABLATE")) g.dbg = atoi(ab);   // timing experiments only
     if (hipDeviceGetAttribute(&g.ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) g.ncu = 0;
     auto bail = [&](int rc) { delete p; return rc; };
     if (g.refR < 1 || g.refV < 1 || g.guardR < 0 || g.guardV < 0) return bail(fail(RSP_ERR_INVALID, "bad CFAR window"));
 
     // ---- pulse-compression segments (fsf:105-126)
-    std::vector<float2> H, twM;
+    std::vector<cd> H, twM;
     std::vector<int> tw_sizes, tw_offs;
-    std::vector<float> taps;
+    std::vector<double> taps;
     std::vector<Interval> need;
     if (g1 > 0) {
         SegDesc s{};
@@ -761,27 +733,27 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
         s.lo = lo; s.hi = hi;
         const int W = hi - lo + 1;
         const int WP = W + s.ntaps - 1;   // staged row: ntaps - 1 leading zeros (k2_pc narrow path)
-        // 8 rows per workgroup (measured best of 1/2/4/8 at x2)
-        int nrw = 8;
-        if (const char* e = getenv("RSP_NARROW_ROWS")) nrw = std::max(1, std::min(8, atoi(e)));   // timing experiments
-        s.rows_per_wg = std::max(1, std::min(nrw, (RSP_K2_POINTS + RSP_K2_POINTS / 16 - (s.ntaps + 1) / 2) / WP));
-        if (WP * s.rows_per_wg + (s.ntaps + 1) / 2 > RSP_K2_POINTS + RSP_K2_POINTS / 16)
+        // up to 8 rows per workgroup (measured best of 1/2/4/8 at x2), within the workgroup's LDS:
+        // rows * WP complex + the taps (ntaps reals = ntaps / 2 complex)
+        const int lds_c = RSP_K2_POINTS + (RSP_K2_POINTS >> (f64 ? 4 : 5));
+        s.rows_per_wg = std::max(1, std::min(8, (lds_c - (s.ntaps + 1) / 2) / WP));
+        if (WP * s.rows_per_wg + (s.ntaps + 1) / 2 > lds_c)
             return bail(fail(RSP_ERR_UNSUPPORTED, "narrow segment window %d samples too long", W));
         s.taps_off = (int)taps.size();
-        for (int j = 0; j < s.ntaps; ++j) taps.push_back((float)pre->MF_narrow[j]);
+        for (int j = 0; j < s.ntaps; ++j) taps.push_back(pre->MF_narrow[j]);
         p->segs.push_back(s);
     }
     if (g2 > 0) {
         SegDesc s{};
         int rc = build_fft_segment(s, pre->MF_medium_fft, pre->N_fft_med, N, g1, g1 + g2, pre->seg_start_medium - 1, H,
-                                   twM, tw_sizes, tw_offs, "medium", (g.dbg & 256) == 0);
+                                   twM, tw_sizes, tw_offs, "medium");
         if (rc) return bail(rc);
         p->segs.push_back(s);
     }
     if (g3 > 0) {
         SegDesc s{};
         int rc = build_fft_segment(s, pre->MF_long_fft, pre->N_fft_long, N, g1 + g2, G, pre->seg_start_long - 1, H, twM,
-                                   tw_sizes, tw_offs, "long", (g.dbg & 256) == 0);
+                                   tw_sizes, tw_offs, "long");
         if (rc) return bail(rc);
         p->segs.push_back(s);
     }
@@ -803,17 +775,18 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
         if (s.hi < s.lo) { s.off = 0; continue; }
         s.off = (int)(std::lower_bound(nof.begin(), nof.end(), s.lo) - nof.begin());
     }
-    // K1 tile: NT samples per [P][NT] slab; keep LDS <= 80 KB (2 workgroups per CU)
+    // K1 tile: NT samples per [P][NT] slab.  complex64: LDS tile <= 80 KB (2 workgroups per
+    // CU for the tiled K1; the persistent K1 double-buffers it) and B*NT*P <= 8192 (16 FFT
+    // points per thread); complex128: the same bytes (NT halved) and B*NT*P <= 4096
     g.pow2P = is_pow2(P) && P >= 16 && P <= 512;   // Stockham range of k1_fft; else direct DFT
     g.Ppad = g.pow2P ? P + P / 16 : P + 4;   // pow2: + one pad per 16 (K1_SH), see rsp_kernels.hip
+    const int max_pts = f64 ? 4096 : 8192;
+    const size_t tile_cap = f64 ? 72 * 1024 : 80 * 1024;
     g.NT = 8;
-    if (const char* nt = getenv("RSP_NT")) g.NT = std::max(1, std::min(8, atoi(nt)));   // timing experiments
-    while (g.NT > 1 && ((size_t)B * g.NT * g.Ppad * sizeof(float2) > 80 * 1024 || (g.pow2P && B * g.NT * P > 8192)))
-        g.NT >>= 1;
-    if ((size_t)B * g.NT * g.Ppad * sizeof(float2) > 160 * 1024 || (g.pow2P && B * g.NT * P > 8192))
+    while (g.NT > 1 && ((size_t)B * g.NT * g.Ppad * esz > tile_cap || (g.pow2P && B * g.NT * P > max_pts))) g.NT >>= 1;
+    if ((size_t)B * g.NT * g.Ppad * esz > 160 * 1024 || (g.pow2P && B * g.NT * P > 8192))
         return bail(fail(RSP_ERR_UNSUPPORTED, "B*P too large for the slow-time FFT tile"));
     g.ntiles = (g.nU + g.NT - 1) / g.NT;
-    nof.resize((size_t)g.ntiles * g.NT, -1);
     if ((int)U.size() > RSP_MAX_IVL) return bail(fail(RSP_ERR_UNSUPPORTED, "too many sample intervals"));
     g.nivl = (int)U.size();
     for (int q = 0, st = 0; q < g.nivl; ++q) {
@@ -821,30 +794,19 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
         g.ivl_start[q] = st;
         st += U[q].hi - U[q].lo + 1;
     }
-    if (g.pow2P) {
-        g.logP = ilog2i(P);
-        radix_plan(g.logP, &g.nradP, g.radP);
-    }
-    if (16 * (size_t)g.Ppad * sizeof(float2) > 160 * 1024 || (g.pow2P && 16 * P > 8192))
+    if (g.pow2P) g.logP = ilog2i(P);
+    if (16 * (size_t)g.Ppad * esz > 160 * 1024 || (g.pow2P && 16 * P > 8192))
         return bail(fail(RSP_ERR_UNSUPPORTED, "prtNum %d too large", P));
     // K2 jobs
     const int rows_total = B * P;
     int wg = 0;
-    const bool own_launch = k2_mixed_mode() == 2;
-    for (int pass = 0; pass < 2; ++pass) {   // k2m_pc's jobs (mixed, own launch) last
-        if (pass == 1) {
-            g.nwg_k2_pow2 = wg;
-            g.mix_job0 = (int)p->jobs.size();
-        }
-        for (size_t si = 0; si < p->segs.size(); ++si) {
-            const SegDesc& s = p->segs[si];
-            if ((own_launch && s.mixM) != (pass == 1)) continue;
-            const int nwg = (rows_total + s.rows_per_wg - 1) / s.rows_per_wg;
-            const int nbl = (s.type == 1) ? s.nblocks : 1;
-            for (int blk = 0; blk < nbl; ++blk) {
-                p->jobs.push_back(K2Job{(int)si, blk, wg, nwg});
-                wg += nwg;
-            }
+    for (size_t si = 0; si < p->segs.size(); ++si) {
+        const SegDesc& s = p->segs[si];
+        const int nwg = (rows_total + s.rows_per_wg - 1) / s.rows_per_wg;
+        const int nbl = (s.type == 1) ? s.nblocks : 1;
+        for (int blk = 0; blk < nbl; ++blk) {
+            p->jobs.push_back(K2Job{(int)si, blk, wg, nwg});
+            wg += nwg;
         }
     }
     g.nseg = (int)p->segs.size();
@@ -854,68 +816,57 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     for (int q = 0; q < g.nseg; ++q) g.segs[q] = p->segs[q];
     for (int q = 0; q < g.njobs; ++q) g.jobs[q] = p->jobs[q];
     g.nwg_k2 = wg;
-    if (getenv("RSP_PLAN_DEBUG"))
-        for (const SegDesc& s : p->segs)
-            fprintf(stderr, "rsp plan: segment type %d gates [%d,%d) lo %d hi %d Lh %d M %d (mixed %d) V %d blocks %d rows/wg %d\n",
-                    s.type, s.ga, s.gb, s.lo, s.hi, s.Lh, s.M, s.mixM, s.V, s.nblocks, s.rows_per_wg);
-    // K3 tile
-    g.cfar_hR = (std::max(g.refR + g.guardR, 2) + 3) & ~3;   // halo, multiple of 4 (float4 tile loads)
+    // K3 tile: <= 64 KB of S per tile (>= 2 workgroups per CU); the fast path covers RT 32/64
+    g.cfar_hR = (std::max(g.refR + g.guardR, 2) + 3) & ~3;   // halo, multiple of 4 (16-B tile loads)
     g.cfar_RT = 64;
-    // <= 64 KB per tile: >= 2 workgroups per CU (P = 256: RT 32, 64 KB; k3_cfar fast path covers RT 32/64)
-    while (g.cfar_RT > 8 && (size_t)P * (g.cfar_RT + 2 * g.cfar_hR) * 4 > 64 * 1024) g.cfar_RT >>= 1;
-    g.cfar_W = (g.cfar_RT + 2 * g.cfar_hR + 3) & ~3;   // LDS row stride, float4 aligned
-    if ((size_t)P * g.cfar_W * 4 > 160 * 1024) return bail(fail(RSP_ERR_UNSUPPORTED, "CFAR tile exceeds LDS"));
+    while (g.cfar_RT > 8 && (size_t)P * (g.cfar_RT + 2 * g.cfar_hR) * p->rsz > 64 * 1024) g.cfar_RT >>= 1;
+    g.cfar_W = (g.cfar_RT + 2 * g.cfar_hR + 3) & ~3;   // LDS row stride, 16-B aligned
+    if ((size_t)P * g.cfar_W * p->rsz > 150 * 1024) return bail(fail(RSP_ERR_UNSUPPORTED, "CFAR tile exceeds LDS"));
 
-    // ---- constants to the device
+    // ---- constants to the device, in the plan's precision
     int rc;
-    // conj(W) laid out [C][BMAX] (BMAX = the K1 instantiation's beam count, zero padded) so
-    // that one channel's beam weights are one contiguous scalar load in k1_dbf_mtd
     const int bmax = B <= 4 ? 4 : (B <= 8 ? 8 : 16);
-    const int cpad = C <= 8 ? 8 : (C <= 16 ? 16 : 32);   // CP of k1_dbf_mtd<BMAX, CP>
-    std::vector<float2> Wc((size_t)bmax * cpad, make_float2(0.f, 0.f)), twP(P), twPp;
-    for (int b = 0; b < B; ++b)
-        for (int c = 0; c < C; ++c) {   // column-major B x C; y = x * W' uses conj(W)  (fsf:95)
-            const size_t i = (size_t)b + (size_t)B * c;
-            Wc[(size_t)c * bmax + b] = make_float2((float)pre->DBF_coeffs_data_C[2 * i], -(float)pre->DBF_coeffs_data_C[2 * i + 1]);
-        }
-    if (g.pow2P) build_pass_twiddles(g.logP, twPp);
-    g.wc_elems = (int)Wc.size();
+    const int cpad = C <= 8 ? 8 : (C <= 16 ? 16 : 32);   // CP of k1_dbf_mtd<T, BMAX, CP>
+    // conj(W): y = x * W' (fsf:95), W column-major B x C
+    auto wconj = [&](int b, int c) {
+        const size_t i = (size_t)b + (size_t)B * c;
+        return cd(pre->DBF_coeffs_data_C[2 * i], -pre->DBF_coeffs_data_C[2 * i + 1]);
+    };
     // per-lane A operands of the DBF MFMA (k1_dbf_mtd): lane l holds A[row l&15][channel 4j + l>>4];
     // row m: beam mb*8 + (m&7), m<8 -> Re(y), m>=8 -> Im(y); y = sum_c conj(W[b][c]) x_c (fsf:95)
     const int mblk = bmax <= 8 ? 1 : 2, nj = cpad / 4;
-    std::vector<float> atab((size_t)mblk * nj * 2 * 64, 0.f);
+    std::vector<double> atab((size_t)mblk * nj * 2 * 64, 0.0);
     for (int mb = 0; mb < mblk; ++mb)
         for (int j = 0; j < nj; ++j)
             for (int lane = 0; lane < 64; ++lane) {
                 const int m = lane & 15, c = 4 * j + (lane >> 4), b = mb * 8 + (m & 7);
-                float wr = 0.f, wi = 0.f;
+                double wr = 0, wi = 0;
                 if (b < B && c < C) {
-                    wr = Wc[(size_t)c * bmax + b].x;
-                    wi = Wc[(size_t)c * bmax + b].y;
+                    wr = wconj(b, c).real();
+                    wi = wconj(b, c).imag();
                 }
                 const bool im = m >= 8;
                 atab[((mb * nj + j) * 2 + 0) * 64 + lane] = im ? wi : wr;    // coefficient of Re(x_c)
                 atab[((mb * nj + j) * 2 + 1) * 64 + lane] = im ? wr : -wi;   // coefficient of Im(x_c)
             }
+    std::vector<cd> twPp, twP(P);
+    if (g.pow2P) build_pass_twiddles(g.logP, twPp);
     g.twPp_elems = (int)twPp.size();
-    for (int i = 0; i < P; ++i) {
-        const double a = -2.0 * M_PI * i / P;
-        twP[i] = make_float2((float)std::cos(a), (float)std::sin(a));
-    }
-    std::vector<float> win(pre->MTD_win, pre->MTD_win + P);
+    for (int i = 0; i < P; ++i) twP[i] = root_of_unity(i, P);
+    std::vector<double> win(pre->MTD_win, pre->MTD_win + P);
     std::vector<double> ra(pre->range_axis, pre->range_axis + G), va(pre->velocity_axis, pre->velocity_axis + P);
     std::vector<double> ang(pre->beam_angles_deg, pre->beam_angles_deg + B);
     std::vector<double> kl(std::max(B - 1, 1), 0.0);
     for (int i = 0; i + 1 < B; ++i) kl[i] = pre->k_slopes_LUT[i];
-    float2 *dWc, *dtwP, *dtwPp, *dH, *dtwM; float *dwin, *dtaps, *datab; int* dnof; SegDesc* dsegs; K2Job* djobs;
+    DevConsts& k = p->k;
     double *dra, *dva, *dang, *dkl;
-    if ((rc = p->upload(&dWc, Wc)) || (rc = p->upload(&datab, atab)) || (rc = p->upload(&dtwP, twP)) || (rc = p->upload(&dtwPp, twPp)) || (rc = p->upload(&dwin, win)) ||
-        (rc = p->upload(&dnof, nof)) || (rc = p->upload(&dsegs, p->segs)) || (rc = p->upload(&djobs, p->jobs)) ||
-        (rc = p->upload(&dtaps, taps)) || (rc = p->upload(&dH, H)) || (rc = p->upload(&dtwM, twM)) ||
-        (rc = p->upload(&dra, ra)) || (rc = p->upload(&dva, va)) || (rc = p->upload(&dang, ang)) ||
-        (rc = p->upload(&dkl, kl)))
+    if ((rc = p->upload_r(&k.Atab, atab)) || (rc = p->upload_c(&k.twP, twP)) || (rc = p->upload_c(&k.twPp, twPp)) ||
+        (rc = p->upload_r(&k.win, win)) || (rc = p->upload_r(&k.taps, taps)) || (rc = p->upload_c(&k.H, H)) ||
+        (rc = p->upload_c(&k.twM, twM)) || (rc = p->upload(&dra, ra)) || (rc = p->upload(&dva, va)) ||
+        (rc = p->upload(&dang, ang)) || (rc = p->upload(&dkl, kl)))
         return bail(rc);
-    p->k = DevConsts{dWc, datab, dwin, dtwP, dtwPp, dnof, dsegs, djobs, dtaps, dH, dtwM, dra, dva, dang, dkl, pre->deltaR, pre->deltaV};
+    k.range_axis = dra; k.velocity_axis = dva; k.beam_angles = dang; k.klut = dkl;
+    k.deltaR = pre->deltaR; k.deltaV = pre->deltaV;
     if (pre->tx_pulse) {
         std::vector<double> tx(pre->tx_pulse, pre->tx_pulse + 2 * (size_t)N);
         if ((rc = p->upload(&p->d_tx, tx))) return bail(rc);
@@ -925,17 +876,7 @@ int32_t rsp_plan_create(const rsp_sig_config* cfg, const rsp_cfar_params* cfar, 
     p->rdm_elems = (size_t)B * P * G;
     g.Gp = (G + 3) & ~3;
     p->mag_elems = (size_t)B * P * g.Gp;
-    if ((rc = p->dalloc(&p->d_cube, (size_t)std::max(C, B) * g.cpitch))) return bail(rc);
-    {
-        const char* nl = getenv("RSP_NLANES");
-        if (nl) p->nlanes = std::max(1, std::min(RSP_LANES, atoi(nl)));
-        if (const char* ks = getenv("RSP_K12_SUB")) p->k12_sub = std::max(0, atoi(ks));
-        const char* q = getenv("RSP_QUEUE");
-        if (q && !strcmp(q, "serial") && hipStreamCreateWithFlags(&p->kstream, hipStreamNonBlocking) != hipSuccess)
-            return bail(fail(RSP_ERR_DEVICE, "hipStreamCreateWithFlags failed"));
-        if (q && !strcmp(q, "pipe") && hipStreamCreateWithFlags(&p->k1stream, hipStreamNonBlocking) != hipSuccess)
-            return bail(fail(RSP_ERR_DEVICE, "hipStreamCreateWithFlags failed"));
-    }
+    if ((rc = p->dalloc_bytes(&p->d_cube, (size_t)std::max(C, B) * g.cpitch * esz))) return bail(rc);
     for (auto& L : p->lanes)
         if ((rc = setup_lane(p, L))) return bail(rc);
     *out = p;
@@ -1033,6 +974,8 @@ int32_t rsp_query_sizes(const rsp_plan* p, rsp_sizes* s) {
     s->used_samples = g.nU;
     s->max_detections = g.max_dets;
     s->n_stages = 3;
+    s->precision = g.prec == RSP_PREC_F64 ? RSP_C128 : RSP_C64;
+    s->elem_bytes = (int32_t)p->esz;
     return RSP_OK;
 }
 
@@ -1048,7 +991,7 @@ int32_t rsp_process_cube(rsp_plan* p, const void* cube, int32_t dtype, int32_t l
 }
 
 static int synth_into(rsp_plan* p, const rsp_target_in* t, int nt, int frame_idx, uint64_t seed, double p_noise,
-                      float2* d_cube, hipStream_t s) {
+                      void* d_cube, hipStream_t s) {
     if (!p->d_tx) return fail(RSP_ERR_INVALID, "plan has no tx_pulse (synthesis path needs precomputed_data.tx_pulse)");
     if (nt < 0 || nt > 64) return fail(RSP_ERR_INVALID, "1..64 targets supported, got %d", nt);
     std::vector<SynthTarget> tg(nt);
@@ -1069,7 +1012,7 @@ int32_t rsp_synthesize_device(rsp_plan* p, const rsp_target_in* t, int32_t nt, i
                               double p_noise, void* d_cube) {
     if (!p || (!t && nt) || !d_cube) return fail(RSP_ERR_INVALID, "null argument");
     HIPCHK(hipSetDevice(p->device));
-    return synth_into(p, t, nt, frame_idx, seed, p_noise, (float2*)d_cube, p->lanes[0].stream);
+    return synth_into(p, t, nt, frame_idx, seed, p_noise, d_cube, p->lanes[0].stream);
 }
 
 int32_t rsp_process_targets(rsp_plan* p, const rsp_target_in* t, int32_t nt, int32_t frame_idx, uint64_t seed,
@@ -1084,7 +1027,8 @@ int32_t rsp_process_targets(rsp_plan* p, const rsp_target_in* t, int32_t nt, int
 
 int32_t rsp_enqueue_device(rsp_plan* p, const void* d_cube, int32_t frame_idx) {
     if (!p || !d_cube) return fail(RSP_ERR_INVALID, "null argument");
-    p->pend_in[p->npend] = (const float2*)d_cube;
+    HIPCHK(hipSetDevice(p->device));   // a host thread may drive plans on several devices
+    p->pend_in[p->npend] = d_cube;
     p->pend_ids[p->npend] = frame_idx;
     if (++p->npend == p->F) return flush_pending(p);
     return RSP_OK;
@@ -1138,22 +1082,15 @@ int32_t rsp_process_stage2(rsp_plan* p, const void* iq, int32_t dtype, double* m
     Geometry gs = p->g;
     gs.C = gs.B;   // input channels are the beams; K1 transposes only (no DBF, no MTD)
     if ((rc = upload_cube(p, iq, dtype, gs.B, p->d_cube, L.stream))) return rc;
-    if (!p->d_aux && (rc = p->dalloc(&p->d_aux, p->rdm_elems))) return rc;
-    const float2* in[1] = {p->d_cube};
+    if (!p->d_aux && (rc = p->dalloc_bytes(&p->d_aux, p->rdm_elems * p->esz))) return rc;
+    const void* in[1] = {p->d_cube};
     const FramePtrs fp = lane_ptrs(p, L, in, 1);
-    HIPCHK(launch_k1(gs, p->k, fp, 1, 0, gs.C, L.stream));
+    HIPCHK(launch_k1(gs, p->k, fp, 1, 0, L.stream));
     HIPCHK(launch_k2(gs, p->k, fp, 1, gs.B * gs.P, L.stream));      // PC rows (b, m) -> L.rdm
     HIPCHK(launch_mtd_cols(gs, p->k, L.rdm, p->d_aux, L.stream));  // S7 over pulses
     HIPCHK(hipStreamSynchronize(L.stream));
-    std::vector<float2> m(p->rdm_elems);
-    if (pc_out) {
-        HIPCHK(hipMemcpy(m.data(), L.rdm, m.size() * sizeof(float2), hipMemcpyDeviceToHost));
-        rdm_to_matlab(p, m, pc_out);
-    }
-    if (mtd_out) {
-        HIPCHK(hipMemcpy(m.data(), p->d_aux, m.size() * sizeof(float2), hipMemcpyDeviceToHost));
-        rdm_to_matlab(p, m, mtd_out);
-    }
+    if (pc_out && (rc = rdm_to_matlab(p, L.rdm, pc_out))) return rc;
+    if (mtd_out && (rc = rdm_to_matlab(p, p->d_aux, mtd_out))) return rc;
     return RSP_OK;
 }
 
@@ -1170,11 +1107,10 @@ int32_t rsp_profile_stages(rsp_plan* p, const void* const* d_cubes, int32_t n_cu
     const int nsets = (n_cubes + nf - 1) / nf;
     std::vector<FramePtrs> fps(nsets);
     for (int j = 0; j < nsets; ++j) {
-        const float2* in[RSP_MAX_F];
-        for (int f = 0; f < nf; ++f) in[f] = (const float2*)d_cubes[(j * nf + f) % n_cubes];
+        const void* in[RSP_MAX_F];
+        for (int f = 0; f < nf; ++f) in[f] = d_cubes[(j * nf + f) % n_cubes];
         fps[j] = lane_ptrs(p, L, in, nf);
     }
-    const FramePtrs& fp = fps[0];
     const Geometry& g = p->g;
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
@@ -1183,7 +1119,7 @@ int32_t rsp_profile_stages(rsp_plan* p, const void* const* d_cubes, int32_t n_cu
         int it = 0;
         auto run = [&]() -> hipError_t {
             const FramePtrs& fj = fps[it++ % nsets];
-            if (s == 0) return launch_k1(g, p->k, fj, nf, 3, g.C, L.stream);
+            if (s == 0) return launch_k1(g, p->k, fj, nf, 3, L.stream);
             if (s == 1) return launch_k2(g, p->k, fj, nf, g.B * g.P, L.stream);
             // counts are zeroed by K1 in the pipeline; here by a tiny 2-D memset per launch
             hipError_t e = hipMemset2DAsync(L.dets, sizeof(DevDet) * (g.max_dets + 1), 0, sizeof(int), nf, L.stream);
@@ -1199,37 +1135,14 @@ int32_t rsp_profile_stages(rsp_plan* p, const void* const* d_cubes, int32_t n_cu
         if (ms_out) ms_out[s] = ms / iters;
     }
     if (frames_out) *frames_out = nf;
-    if (const char* tf = getenv("RSP_TRACE_FILE")) {   // diagnostic per-workgroup phase stamps
-        size_t nwg[3] = {(size_t)g.ntiles * nf, (size_t)g.nwg_k2 * nf, (size_t)k3_ntiles(g) * (g.B - 1) * nf};
-        size_t mx = std::max(nwg[0], std::max(nwg[1], nwg[2]));
-        unsigned long long* dt = nullptr;
-        HIPCHK(hipMalloc(&dt, mx * 4 * sizeof(unsigned long long)));
-        FramePtrs tp = fp;
-        tp.trace = dt;
-        FILE* fo = fopen(tf, "a");
-        std::vector<unsigned long long> h(mx * 4);
-        for (int s = 0; s < 3; ++s) {
-            HIPCHK(hipMemsetAsync(dt, 0, mx * 4 * sizeof(unsigned long long), L.stream));
-            HIPCHK(hipMemset2DAsync(L.dets, sizeof(DevDet) * (g.max_dets + 1), 0, sizeof(int), nf, L.stream));
-            if (s == 0) HIPCHK(launch_k1(g, p->k, tp, nf, 3, g.C, L.stream));
-            if (s == 1) HIPCHK(launch_k2(g, p->k, tp, nf, g.B * g.P, L.stream));
-            if (s == 2) HIPCHK(launch_k3(g, p->k, tp, nf, L.stream));
-            HIPCHK(hipStreamSynchronize(L.stream));
-            HIPCHK(hipMemcpy(h.data(), dt, nwg[s] * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-            for (size_t w = 0; fo && w < nwg[s]; ++w)
-                fprintf(fo, "%s,%zu,%llu,%llu,%llu,%llu\n", kStageNames[s], w, h[4 * w], h[4 * w + 1], h[4 * w + 2],
-                        h[4 * w + 3]);
-        }
-        if (fo) fclose(fo);
-        (void)hipFree(dt);
-    }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     if (bytes_out) {   // algorithmic bytes per launch (nf frames); DESIGN.md "Measurement"
-        const int64_t cube = (int64_t)g.C * g.nU * g.P * 8;        // used fast-time samples, complex64
-        const int64_t z = (int64_t)g.B * g.nU * g.P * 8;           // Doppler-domain rows
-        const int64_t rdm = (int64_t)g.B * g.P * g.G * 8;          // complex RD map
-        const int64_t mag = (int64_t)g.B * g.P * g.G * 4;          // |RD| map
+        const int64_t es = (int64_t)p->esz, rs = (int64_t)p->rsz;   // complex / real element bytes
+        const int64_t cube = (int64_t)g.C * g.nU * g.P * es;       // used fast-time samples
+        const int64_t z = (int64_t)g.B * g.nU * g.P * es;          // Doppler-domain rows
+        const int64_t rdm = (int64_t)g.B * g.P * g.G * es;         // complex RD map
+        const int64_t mag = (int64_t)g.B * g.P * g.G * rs;         // |RD| map
         if (cap > 0) bytes_out[0] = nf * (cube + z);
         if (cap > 1) bytes_out[1] = nf * (z + rdm + mag);
         if (cap > 2) bytes_out[2] = nf * mag;

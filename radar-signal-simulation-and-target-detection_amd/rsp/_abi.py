@@ -8,7 +8,7 @@ the GPU.  There is no CPU fallback: if the library is missing, ``lib()`` raises.
 import ctypes as ct
 import os
 
-LIB_PATH = os.environ.get('RSP_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'librsp.so')   # RSP_LIB: timing experiments
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'librsp.so')
 
 RSP_OK, RSP_ERR_INVALID, RSP_ERR_UNSUPPORTED, RSP_ERR_DEVICE, RSP_ERR_NOMEM, RSP_ERR_OVERFLOW = 0, -1, -2, -3, -4, -5
 RSP_C64, RSP_C128 = 1, 2
@@ -66,7 +66,16 @@ class FrameOut(ct.Structure):
 class Sizes(ct.Structure):
     _fields_ = [('cube_elems', ct.c_int64), ('rdm_elems', ct.c_int64), ('cfar_map_elems', ct.c_int64),
                 ('P', ct.c_int32), ('N', ct.c_int32), ('C', ct.c_int32), ('B', ct.c_int32), ('G', ct.c_int32),
-                ('used_samples', ct.c_int32), ('max_detections', ct.c_int32), ('n_stages', ct.c_int32)]
+                ('used_samples', ct.c_int32), ('max_detections', ct.c_int32), ('n_stages', ct.c_int32),
+                ('precision', ct.c_int32), ('elem_bytes', ct.c_int32)]
+
+
+RSP_PLAN_K1_TILED = 1
+
+
+class PlanOptions(ct.Structure):
+    _fields_ = [('device', ct.c_int32), ('frames_per_launch', ct.c_int32), ('precision', ct.c_int32),
+                ('flags', ct.c_int32)]
 
 
 RSP_MAT_CHAR, RSP_MAT_DOUBLE, RSP_MAT_SINGLE = 4, 6, 7
@@ -122,6 +131,9 @@ PROTOTYPES = {
     'rsp_last_error': (ct.c_char_p, []),
     'rsp_plan_create': (ct.c_int32, [ct.POINTER(SigConfig), ct.POINTER(CfarParams), ct.POINTER(ClusterParams),
                                      ct.POINTER(Precomputed), ct.c_int32, ct.c_int32, ct.POINTER(_P)]),
+    'rsp_plan_create_ex': (ct.c_int32, [ct.POINTER(SigConfig), ct.POINTER(CfarParams), ct.POINTER(ClusterParams),
+                                        ct.POINTER(Precomputed), ct.POINTER(PlanOptions), ct.POINTER(_P)]),
+    'rsp_plan_options_default': (ct.c_int32, [ct.POINTER(PlanOptions)]),
     'rsp_plan_destroy': (ct.c_int32, [_P]),
     'rsp_query_sizes': (ct.c_int32, [_P, ct.POINTER(Sizes)]),
     'rsp_process_cube': (ct.c_int32, [_P, _P, ct.c_int32, ct.c_int32, ct.c_int32, ct.POINTER(FrameOut)]),

@@ -30,9 +30,13 @@ class Plan:
 
     Parameters mirror ``fun_process_single_frame(targets, config, cfar_params,
     cluster_params, precomputed_data, frame_idx)`` (fun_process_single_frame.m:13).
+    ``precision``: 'c128' (complex double, MATLAB's arithmetic; default) or 'c64'.
+    ``k1_tiled``: force the one-tile-per-workgroup K1 (parity tests compare it with the
+    persistent K1 the plan otherwise picks).
     """
 
-    def __init__(self, config, cfar_params, cluster_params, precomputed_data, device=0, frames_per_launch=1):
+    def __init__(self, config, cfar_params, cluster_params, precomputed_data, device=0, frames_per_launch=1,
+                 precision='c128', k1_tiled=False):
         sc = config['Sig_Config']
         pre = precomputed_data
         self.config = config
@@ -70,14 +74,24 @@ class Plan:
             MTD_win=arr(pre['MTD_win']), range_axis=arr(pre['range_axis']), velocity_axis=arr(pre['velocity_axis']),
             deltaR=float(pre['deltaR']), deltaV=float(pre['deltaV']), beam_angles_deg=arr(pre['beam_angles_deg']),
             k_slopes_LUT=arr(klut if klut.size else np.zeros(1)))
+        if precision not in ('c128', 'c64'):
+            raise ValueError("precision must be 'c128' or 'c64'")
+        opt = _abi.PlanOptions()
+        check(lib().rsp_plan_options_default(ct.byref(opt)))
+        opt.device, opt.frames_per_launch = int(device), int(frames_per_launch)
+        opt.precision = _abi.RSP_C128 if precision == 'c128' else _abi.RSP_C64
+        opt.flags = _abi.RSP_PLAN_K1_TILED if k1_tiled else 0
         h = ct.c_void_p()
-        check(lib().rsp_plan_create(ct.byref(self.cfg), ct.byref(self.cfar), ct.byref(self.cluster),
-                                    ct.byref(self.pre), int(device), int(frames_per_launch), ct.byref(h)))
+        check(lib().rsp_plan_create_ex(ct.byref(self.cfg), ct.byref(self.cfar), ct.byref(self.cluster),
+                                       ct.byref(self.pre), ct.byref(opt), ct.byref(h)))
         self.h = h
         s = _abi.Sizes()
         check(lib().rsp_query_sizes(self.h, ct.byref(s)))
         self.sizes = s
         self.P, self.N, self.C, self.B, self.G = s.P, s.N, s.C, s.B, s.G
+        self.precision = precision
+        self.cdtype = np.complex128 if precision == 'c128' else np.complex64   # device cube / map element
+        self.cube_bytes = s.cube_elems * s.elem_bytes
 
     def close(self):
         if getattr(self, 'h', None):
@@ -116,7 +130,8 @@ class Plan:
         return res
 
     def process_cube(self, cube, frame_idx=1, want_rdm=False, want_cfar=False):
-        """S5..S11 on a noisy echo cube ``cube[m, n, c]`` (MATLAB [P x N x C])."""
+        """S5..S11 on a noisy echo cube ``cube[m, n, c]`` (MATLAB [P x N x C]).  ``cfar_maps``
+        (want_cfar) is rdm_for_cfar_all as the device's K3 thresholds it (fsf:184-187)."""
         cube = np.asarray(cube)
         if cube.shape != (self.P, self.N, self.C):
             raise ValueError('cube shape %r != (P, N, C) = %r' % (cube.shape, (self.P, self.N, self.C)))
@@ -179,8 +194,8 @@ class Plan:
         return out
 
     def upload_cube(self, ptr, cube):
-        """Upload a [P, N, C] cube as complex64 column-major to device pointer ``ptr``."""
-        a = np.asfortranarray(np.asarray(cube).astype(np.complex64))
+        """Upload a [P, N, C] cube column-major, in the plan's precision, to device pointer ``ptr``."""
+        a = np.asfortranarray(np.asarray(cube).astype(self.cdtype))
         check(lib().rsp_device_upload(self.h, ct.c_void_p(ptr), a.ctypes.data_as(ct.c_void_p), a.nbytes))
 
     def synthesize_device(self, ptr, targets, frame_idx, seed=20250101, p_noise=1.0):

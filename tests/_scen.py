@@ -38,3 +38,15 @@ def noisy_cube(s, targets, frame_idx=1, seed=SEED, dtype=np.complex64):
 
 def det_key_set(dets):
     return {(int(d[0]), int(d[1]), int(d[2])) for d in dets}
+
+
+def device_cube(plan, targets, frame_idx=1, seed=SEED):
+    """S4 + S4.1 synthesised on the device in the plan's precision, downloaded as [P, N, C]."""
+    ptr = plan.device_alloc(plan.cube_bytes)
+    try:
+        plan.synthesize_device(ptr, targets, frame_idx=frame_idx, seed=seed)
+        plan.sync()
+        flat = plan.device_download(ptr, plan.sizes.cube_elems, plan.cdtype)
+    finally:
+        plan.device_free(ptr)
+    return flat.reshape((plan.P, plan.N, plan.C), order='F').astype(np.complex128)

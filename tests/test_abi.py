@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert _abi.lib().rsp_abi_version() == 1
+    assert _abi.lib().rsp_abi_version() == 2
 
 
 STRUCTS = {'rsp_sig_config': _abi.SigConfig, 'rsp_cfar_params': _abi.CfarParams,
@@ -45,7 +45,8 @@ STRUCTS = {'rsp_sig_config': _abi.SigConfig, 'rsp_cfar_params': _abi.CfarParams,
            'rsp_target_in': _abi.TargetIn, 'rsp_target': _abi.Target, 'rsp_detection': _abi.Detection,
            'rsp_frame_out': _abi.FrameOut, 'rsp_sizes': _abi.Sizes, 'rsp_music_config': _abi.MusicConfig,
            'rsp_music_scene': _abi.MusicScene, 'rsp_music_out': _abi.MusicOut, 'rsp_track_point': _abi.TrackPoint,
-           'rsp_inter_frame_params': _abi.InterFrameParams, 'rsp_track': _abi.Track}
+           'rsp_inter_frame_params': _abi.InterFrameParams, 'rsp_track': _abi.Track,
+           'rsp_plan_options': _abi.PlanOptions}
 
 
 def test_struct_layouts_match_header():
@@ -77,6 +78,18 @@ def test_null_arguments_are_rejected():
     assert lib.rsp_drain(None) == _abi.RSP_ERR_INVALID
     assert lib.rsp_process_cube(None, None, 1, 0, 0, None) == _abi.RSP_ERR_INVALID
     assert lib.rsp_stage_name(99) == b'?'
+    assert lib.rsp_plan_create_ex(None, None, None, None, None, None) == _abi.RSP_ERR_INVALID
+
+
+def test_plan_options_defaults_and_validation():
+    lib = _abi.lib()
+    o = _abi.PlanOptions()
+    assert lib.rsp_plan_options_default(ct.byref(o)) == _abi.RSP_OK
+    assert (o.device, o.frames_per_launch, o.precision, o.flags) == (0, 1, _abi.RSP_C128, 0)
+    from rsp.plan import Plan
+    s = scenario('small')
+    with pytest.raises(ValueError):
+        Plan(s['cfg'], s['cfar'], s['clus'], s['pre_p'], precision='c32')
 
 
 def test_bad_config_is_rejected_before_touching_the_device():

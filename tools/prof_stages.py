@@ -21,9 +21,10 @@ def main():
     nf = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     cfg, cfar, clus, W, ang, k = C.named_config(name)
     pre = precompute(cfg, W, ang, k, C.V8_FIR)
-    plan = Plan(cfg, cfar, clus, pre, frames_per_launch=nf)
+    prec = sys.argv[4] if len(sys.argv) > 4 else 'c128'
+    plan = Plan(cfg, cfar, clus, pre, frames_per_launch=nf, precision=prec)
     # a ring of >= 8 cubes (> the 256 MiB Infinity Cache at x2), rotated over by the launches
-    cubes = [plan.device_alloc(plan.sizes.cube_elems * 8) for _ in range(max(nf, 8))]
+    cubes = [plan.device_alloc(plan.cube_bytes) for _ in range(max(nf, 8))]
     tg = C.v8_2_targets()
     for i, p in enumerate(cubes):
         plan.synthesize_device(p, tg, 1 + i)
