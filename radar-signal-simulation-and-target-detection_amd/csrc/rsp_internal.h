@@ -8,6 +8,18 @@
 #define RSP_K2_POINTS 4096   // complex points per pulse-compression workgroup
 #define K2_THREADS 256       // threads per pulse-compression workgroup (16 points each)
 #define RSP_THREADS 256
+// Compile-time kernel choices (defaults = the shipped library; other values only for A/B
+// timing builds, `make ab`): overlap-save radix plan palindromic (1) or standard (0); compact
+// (1) or full (0) twiddle rows; LDS pad shift of complex-double overlap-save rows.
+#ifndef RSP_K2_PAL
+#define RSP_K2_PAL 1
+#endif
+#ifndef RSP_K2_CMP
+#define RSP_K2_CMP 1
+#endif
+#ifndef RSP_K2_SH64
+#define RSP_K2_SH64 5
+#endif
 
 // Arithmetic of a plan: every device buffer, table and operation of the chain is in one of
 // these.  PREC_F64 is MATLAB's complex double (the reference's arithmetic, fsf:47,92,101,131);

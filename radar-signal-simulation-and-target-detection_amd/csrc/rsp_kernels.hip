@@ -59,10 +59,25 @@ __device__ __forceinline__ V vtw(double c, double s) {   // exp(-+ i theta)
     typedef scal<V> S;
     return V{(S)c, (S)(INV ? s : -s)};
 }
-// |x| (fsf:184-185 abs): hardware square root for float (v_sqrt_f32, 1 ulp); the correctly
-// rounded square root for double
+// |x| (fsf:184-185 abs): hardware square root for float (v_sqrt_f32, 1 ulp); for double the
+// compiler's own refinement of v_rsq_f64 (Goldschmidt step + two Newton corrections) without
+// its ldexp scaling and class checks, which guard only denormal / infinite inputs -- not the
+// magnitudes of a radar map; 0 stays 0.
 __device__ __forceinline__ float cmag(f2 x) { return __builtin_amdgcn_sqrtf(x.x * x.x + x.y * x.y); }
-__device__ __forceinline__ double cmag(d2 x) { return __builtin_sqrt(x.x * x.x + x.y * x.y); }
+__device__ __forceinline__ double cmag(d2 x) {
+#if defined(RSP_CMAG_EXACT)
+    return __builtin_sqrt(x.x * x.x + x.y * x.y);
+#endif
+    const double q = x.x * x.x + x.y * x.y;
+    const double r = __builtin_amdgcn_rsq(q);           // v_rsq_f64
+    double g = q * r, h = 0.5 * r;
+    const double r0 = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r0, g);
+    h = __builtin_fma(h, r0, h);
+    g = __builtin_fma(__builtin_fma(-g, g, q), h, g);
+    g = __builtin_fma(__builtin_fma(-g, g, q), h, g);
+    return q > 0.0 ? g : 0.0;
+}
 
 // Raw buffer resources (SRSRC): 32-bit byte offsets and hardware range checking.  An offset at
 // or past num_records reads 0 / drops the store, so masked lanes need no branch or select.
@@ -213,21 +228,34 @@ constexpr int n_passes(int m) {
     }
     return n;
 }
-constexpr int rad_bits_p(int m, int q, bool rev) { return rev ? rad_bits(m, n_passes(m) - 1 - q) : rad_bits(m, q); }
+// PAL: the overlap-save blocks' plan puts the smallest radix in the middle of a 3-pass plan
+// (2048 = 16 x 8 x 16, 1024 = 16 x 4 x 16): a palindrome, so the inverse FFT runs the same
+// radices, and both Ns = 1 passes -- the forward first pass and the inverse first pass fused
+// into the forward last one -- are radix 16, whose stride-16 stores are at most 2-way
+// conflicted (tools/lds_conflicts64.py).  Must match radix_plan() in rsp_plan.cpp.
+constexpr int rad_bits_pal(int m, int q) {
+    return n_passes(m) == 3 && q >= 1 ? rad_bits(m, 3 - q) : rad_bits(m, q);
+}
+constexpr int rad_bits_p(int m, int q, bool rev, bool pal = false) {
+    return pal ? (rev ? rad_bits_pal(m, n_passes(m) - 1 - q) : rad_bits_pal(m, q))
+               : (rev ? rad_bits(m, n_passes(m) - 1 - q) : rad_bits(m, q));
+}
 
 // Offset of pass q's twiddle table inside the concatenated per-pass tables of a 2^LG FFT:
 // pass i >= 1 owns Ns_i rows of tw_row(R_i) entries (pass 0: Ns = 1, no twiddles).  Must
 // match build_pass_twiddles() in rsp_plan.cpp.
-constexpr int tw_pass_off(int LG, int q, bool rev = false, bool cmp = false) {
+constexpr int tw_pass_off(int LG, int q, bool rev = false, bool cmp = false, bool pal = false) {
     int off = 0, lgns = 0;
     for (int i = 0; i < q; ++i) {
-        const int rb = rad_bits_p(LG, i, rev);
+        const int rb = rad_bits_p(LG, i, rev, pal);
         if (i > 0) off += (1 << lgns) * tw_row(1 << rb, cmp);
         lgns += rb;
     }
     return off;
 }
-constexpr int tw_total(int LG, bool rev = false, bool cmp = false) { return tw_pass_off(LG, n_passes(LG), rev, cmp); }
+constexpr int tw_total(int LG, bool rev = false, bool cmp = false, bool pal = false) {
+    return tw_pass_off(LG, n_passes(LG), rev, cmp, pal);
+}
 
 // One Stockham radix-R pass (Govindaraju et al. formulation) over `nrows` rows of
 // length L = 2^LGL held in LDS (row stride rs).  Ns = 2^LGNS = product of the earlier
@@ -300,20 +328,20 @@ __device__ __forceinline__ void sh_pass(V* buf, int rs, int nrows, const V* tw, 
 // Passes Q..QEND-1 of a 2^LG-point FFT (radix order reversed if REV) over `nrows` rows;
 // pass n_passes - 1 stores through `last`, the others through `mid`.  tw = this plan's
 // concatenated tables.  PTS = complex points per thread (nrows * L / NTHR).
-template <int LG, int Q, int QEND, int LGNS, int PTS, bool INV, bool REV, int SH, int NTHR, bool CMP, class V,
-          class StMid, class StLast>
+template <int LG, int Q, int QEND, int LGNS, int PTS, bool INV, bool REV, int SH, int NTHR, bool CMP, bool PAL = false,
+          class V, class StMid, class StLast>
 __device__ __forceinline__ void fft_range(V* buf, int rs, int nrows, const V* tw, const StMid& mid, const StLast& last) {
     constexpr int NP = n_passes(LG);
     if constexpr (Q < QEND) {
-        constexpr int RB = rad_bits_p(LG, Q, REV);
+        constexpr int RB = rad_bits_p(LG, Q, REV, PAL);
         constexpr int R = 1 << RB;
         constexpr int NB = (PTS + R - 1) / R;
-        const V* twq = tw + tw_pass_off(LG, Q, REV, CMP);
+        const V* twq = tw + tw_pass_off(LG, Q, REV, CMP, PAL);
         if constexpr (Q == NP - 1)
             sh_pass<R, INV, NB, SH, NTHR, LG, LGNS, CMP>(buf, rs, nrows, twq, last);
         else
             sh_pass<R, INV, NB, SH, NTHR, LG, LGNS, CMP>(buf, rs, nrows, twq, mid);
-        fft_range<LG, Q + 1, QEND, LGNS + RB, PTS, INV, REV, SH, NTHR, CMP>(buf, rs, nrows, tw, mid, last);
+        fft_range<LG, Q + 1, QEND, LGNS + RB, PTS, INV, REV, SH, NTHR, CMP, PAL>(buf, rs, nrows, tw, mid, last);
     }
 }
 
@@ -723,10 +751,11 @@ struct StoreRdm {   // last inverse pass: keep outputs i in [Lh-1, Lh-1+V) that 
     }
 };
 
-// LDS pad of the overlap-save rows: one complex per 32 (float) / 16 (double, 16-B elements:
-// a stride-16 first-pass store then walks 17 x 16 B, distinct 16-B slots of the 128-B
-// ds_write_b128 lane groups)
-template <class T> constexpr int k2_sh() { return sizeof(T) == 4 ? 5 : 4; }
+// LDS pad of the overlap-save rows: one complex per 32.  For 16-B elements this keeps every
+// ds_read_b128 of a pass conflict-free (a pad per 16 would shift lanes 20-27 of a lane group
+// onto lane 12's bank), and the stride-16 stores of the two radix-16 Ns = 1 passes 2-way
+// (tools/lds_conflicts64.py)
+template <class T> constexpr int k2_sh() { return sizeof(T) == 4 ? 5 : RSP_K2_SH64; }
 #define K2_LDS_DATA(SH) (RSP_K2_POINTS + (RSP_K2_POINTS >> (SH)))
 
 // One overlap-save block of one FFT segment for RSP_K2_POINTS / 2^LGM adjacent rows.
@@ -747,8 +776,9 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     constexpr int rs = M + (M >> SH);
     constexpr int NP = n_passes(LGM);
     static_assert(NP >= 2, "overlap-save block needs >= 2 FFT passes");
-    constexpr int RB0 = rad_bits(LGM, 0), R0 = 1 << RB0, NB0 = 16 / R0, nb0 = M / R0;
-    constexpr int RBL = rad_bits(LGM, NP - 1), RL = 1 << RBL, NBL = 16 / RL;   // last forward pass
+    constexpr bool PAL = RSP_K2_PAL, CMP = RSP_K2_CMP;
+    constexpr int RB0 = rad_bits_p(LGM, 0, false, PAL), R0 = 1 << RB0, NB0 = 16 / R0, nb0 = M / R0;
+    constexpr int RBL = rad_bits_p(LGM, NP - 1, false, PAL), RL = 1 << RBL, NBL = 16 / RL;   // last forward pass
     const int P = g.P, G = g.G;
     const int lo = sd.lo, hi = sd.hi, off = sd.off;
     const int tid = threadIdx.x;
@@ -799,18 +829,18 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
 #pragma unroll
         for (int r = 0; r < RL; ++r) hreg[t * RL + r] = H[sd.H_off + j + r * (M / RL)];
     }
-    constexpr int NTWF = tw_total(LGM, false, true);
+    constexpr int NTWF = tw_total(LGM, false, CMP, PAL);
     // forward pass 0 (Ns = 1, no twiddles) straight from the loaded samples
     sh_store<R0, false, NB0, SH, K2_THREADS, LGM, 0>(v0, rs, rows, StoreLds<V>{L});
     __syncthreads();
     // forward passes 1 .. NP-2
-    fft_range<LGM, 1, NP - 1, RB0, 16, false, false, SH, K2_THREADS, true>(L, rs, rows, twl, StoreLds<V>{L},
-                                                                          StoreLds<V>{L});
+    fft_range<LGM, 1, NP - 1, RB0, 16, false, false, SH, K2_THREADS, CMP, PAL>(L, rs, rows, twl, StoreLds<V>{L},
+                                                                               StoreLds<V>{L});
     // fused: forward last pass, x H (1/M folded in), inverse pass 0 of the reversed plan
     {
         V v[NBL][RL];
-        sh_load<RL, false, NBL, SH, K2_THREADS, LGM, LGM - RBL, true>(L, rs, rows,
-                                                                       twl + tw_pass_off(LGM, NP - 1, false, true), v);
+        sh_load<RL, false, NBL, SH, K2_THREADS, LGM, LGM - RBL, CMP>(L, rs, rows,
+                                                                      twl + tw_pass_off(LGM, NP - 1, false, CMP, PAL), v);
         __syncthreads();
 #pragma unroll
         for (int t = 0; t < NBL; ++t) {
@@ -824,7 +854,7 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     // inverse passes 1 .. NP-1 (reversed radices); the last keeps the valid overlap-save
     // outputs = stitched gates
     const int gend = min(sd.gb, g0 + sd.V);
-    fft_range<LGM, 1, NP, RBL, 16, true, true, SH, K2_THREADS, true>(
+    fft_range<LGM, 1, NP, RBL, 16, true, true, SH, K2_THREADS, CMP, PAL>(
         L, rs, rows, twl + NTWF, StoreLds<V>{L},
         StoreRdm<V>{buf_rsrc(rdm, (unsigned)(rows_total * G * sizeof(V))),
                     buf_rsrc(mag, (unsigned)(rows_total * g.Gp * sizeof(T))), G, g.Gp, row0, rows_total, Lh1, g0,

@@ -141,6 +141,7 @@ struct Reader {
             small = true;
             type = t & 0xFFFF;
             nbytes = t >> 16;
+            if (nbytes > 4) return false;   // the small form holds at most 4 bytes inline (malformed file)
             memcpy(inl, &w[1], 4);
         } else {
             small = false;

@@ -9,6 +9,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'radar-signal-simulation-and-target-detection_amd'))
+if os.environ.get('AB_LIB'):   # timing experiments only (tools/ab.sh): an A/B variant of librsp.so
+    from rsp import _abi  # noqa: E402
+    _abi.LIB_PATH = os.environ['AB_LIB']
 
 from rsp import config as C  # noqa: E402
 from rsp.precompute import precompute  # noqa: E402

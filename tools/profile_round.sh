@@ -1,10 +1,11 @@
 #!/bin/bash
 # GPU profiling pass for the round's evidence (run on the GPU box through gpurun):
-#   kernel trace + stats of the bench command, FETCH_SIZE / WRITE_SIZE passes -> traffic json,
-#   and SQ counter passes of the stage driver.  Everything lands in gpurun_out/prof_<tag>/.
-# usage: tools/profile_round.sh TAG [bench args...]
+#   the bench line, a kernel trace + stats of the same bench command, FETCH_SIZE / WRITE_SIZE
+#   passes -> traffic json, and SQ counter passes of the stage driver.  Everything lands in
+#   gpurun_out/prof_<tag>/.
+# usage: tools/profile_round.sh TAG CONFIG PREC [bench args...]     (PREC = c128 | c64)
 set -o pipefail
-tag=$1; shift
+tag=$1; cfg=$2; prec=$3; shift 3
 out=gpurun_out/prof_$tag
 mkdir -p $out
 export TMPDIR=/tmp
@@ -16,14 +17,14 @@ step() {  # name timeout cmd...
   echo "=== $name rc=$rc"; tail -n 4 $out/$name.log
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
-step bench 240 python3 bench.py "$@"
+step bench 240 python3 bench.py --config $cfg --precision $prec "$@"
 cp $out/bench.log $out/bench.json
-step trace 240 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o run -- python3 bench.py --no-cpu-baseline "$@"
-step fetch 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/fetch -o run -- python3 tools/prof_stages.py x2 10 8
-step write 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/write -o run -- python3 tools/prof_stages.py x2 10 8
-python3 tools/pmc_traffic.py $out/fetch $out/write $out/pmc_traffic_x2.json x2 10 8 > /dev/null
-step sqa 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d $out/sqa -o run -- python3 tools/prof_stages.py x2 10 8
-step sqb 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d $out/sqb -o run -- python3 tools/prof_stages.py x2 10 8
+step trace 240 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o run -- python3 bench.py --config $cfg --precision $prec --no-cpu-baseline "$@"
+step fetch 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/fetch -o run -- python3 tools/prof_stages.py $cfg 10 8 $prec
+step write 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/write -o run -- python3 tools/prof_stages.py $cfg 10 8 $prec
+python3 tools/pmc_traffic.py $out/fetch $out/write $out/pmc_traffic_${cfg}_${prec}.json $cfg 10 8 > /dev/null
+step sqa 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d $out/sqa -o run -- python3 tools/prof_stages.py $cfg 10 8 $prec
+step sqb 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d $out/sqb -o run -- python3 tools/prof_stages.py $cfg 10 8 $prec
 python3 tools/pmc_summary.py $out/sqa $out/sqb > $out/sq_summary.txt
 cat $out/sq_summary.txt
 find $out/trace -name '*kernel_stats.csv' -exec cp {} $out/kernel_stats.csv \;
