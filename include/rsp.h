@@ -215,6 +215,13 @@ int32_t rsp_results_clear(rsp_plan* plan);
  * fun_MTD_produce is un-vendored; this backs it with fsf S6 + S7. */
 int32_t rsp_process_stage2(rsp_plan* plan, const void* iq_beams, int32_t dtype,
                            double* mtd_out, double* pc_out);
+/* Gated stage-2 input, as the v2 `.mat` frames store it (main_simulate_echoes_with_array_v2.m:
+ * 256-267): iq_gated [P x n_gated x B] holds, for segment k = narrow, medium, long, the PRT
+ * columns cols[2k] .. cols[2k+1] (1-based, inclusive) side by side.  They are put back at
+ * their PRT positions (zeros elsewhere) and processed like rsp_process_stage2.
+ * cols = NULL: the reference gating 83:310, 311:1033, 1034:3486 (n_gated = 3404). */
+int32_t rsp_process_stage2_gated(rsp_plan* plan, const void* iq_gated, int32_t dtype, int32_t n_gated,
+                                 const int32_t* cols, double* mtd_out, double* pc_out);
 
 /* ---- measurement ----
  * Time each device stage `iters` times on the plan's stream with HIP events.  Each launch

@@ -936,6 +936,34 @@ int32_t rsp_process_stage2(rsp_plan* p, const void* iq, int32_t dtype, double* m
     return RSP_OK;
 }
 
+int32_t rsp_process_stage2_gated(rsp_plan* p, const void* iq, int32_t dtype, int32_t n_gated, const int32_t* cols,
+                                 double* mtd_out, double* pc_out) {
+    if (!p || !iq) return fail(RSP_ERR_INVALID, "null argument");
+    if (dtype != RSP_C64 && dtype != RSP_C128) return fail(RSP_ERR_INVALID, "unknown dtype %d", dtype);
+    static const int32_t kRefCols[6] = {83, 310, 311, 1033, 1034, 3486};   // main_simulate_echoes_with_array_v2.m:257-264
+    const int32_t* c = cols ? cols : kRefCols;
+    const int P = p->g.P, N = p->g.N, B = p->g.B;
+    int total = 0;
+    for (int k = 0; k < 3; ++k) {
+        if (c[2 * k] < 1 || c[2 * k + 1] < c[2 * k] || c[2 * k + 1] > N)
+            return fail(RSP_ERR_INVALID, "gate columns %d..%d of segment %d outside the %d-sample PRT", c[2 * k],
+                        c[2 * k + 1], k, N);
+        total += c[2 * k + 1] - c[2 * k] + 1;
+    }
+    if (total != n_gated) return fail(RSP_ERR_INVALID, "gated input has %d columns, the gate columns cover %d", n_gated, total);
+    // put the gated columns back at their PRT positions (zeros elsewhere): [P x N x B]
+    const size_t es = dtype == RSP_C128 ? 16 : 8, colb = (size_t)P * es;
+    std::vector<unsigned char> full((size_t)N * B * colb, 0);
+    const unsigned char* src = static_cast<const unsigned char*>(iq);
+    for (int b = 0; b < B; ++b) {
+        int ng = 0;
+        for (int k = 0; k < 3; ++k)
+            for (int col = c[2 * k] - 1; col < c[2 * k + 1]; ++col, ++ng)
+                memcpy(&full[((size_t)b * N + col) * colb], src + ((size_t)b * n_gated + ng) * colb, colb);
+    }
+    return rsp_process_stage2(p, full.data(), dtype, mtd_out, pc_out);
+}
+
 int32_t rsp_profile_stages(rsp_plan* p, const void* const* d_cubes, int32_t n_cubes, int32_t iters, float* ms_out,
                            int64_t* bytes_out, int32_t cap, int32_t* frames_out) {
     if (!p || !d_cubes || n_cubes < 1 || iters < 1) return fail(RSP_ERR_INVALID, "bad argument");

@@ -13,6 +13,11 @@ Drop-in for the MATLAB reference's per-frame chain
 All compute runs in librsp.so (HIP kernels for gfx950 behind the C-ABI in
 include/rsp.h).  There is no CPU fallback.
 """
+import collections
+import hashlib
+
+import numpy as np
+
 from .config import (named_config, make_config, default_cfar_params, default_cluster_params,
                      v8_2_targets, evolve_targets, V8_FIR)
 from .precompute import precompute
@@ -23,35 +28,94 @@ from .music import MusicPlan, MUSIC_1D
 from .tracks import inter_frame_cluster, default_inter_frame_params
 from . import matio
 
-_PLANS = {}
+# main_simulate_echoes_with_array_v2.m:257-264: PRT columns of the three gated segments
+REFERENCE_GATE_COLS = ((83, 310), (311, 1033), (1034, 3486))
+
+_PLANS = collections.OrderedDict()   # content fingerprint -> Plan (most recently used last)
+_MAX_PLANS = 4
 
 
-def _plan_for(config, cfar_params, cluster_params, precomputed_data, device=0):
-    key = (id(config), id(cfar_params), id(cluster_params), id(precomputed_data), device)
-    p = _PLANS.get(key)
+def _fingerprint(*objs):
+    """SHA-1 over the contents of nested dicts / lists / scalars / numpy arrays, so that a plan
+    is reused only for equal inputs (an in-place edit or a new dict with other values makes a
+    new plan; a garbage-collected dict's reused id() cannot alias an old one)."""
+    h = hashlib.sha1()
+
+    def feed(o):
+        if isinstance(o, dict):
+            h.update(b'{')
+            for k in sorted(o, key=str):
+                feed(str(k))
+                feed(o[k])
+            h.update(b'}')
+        elif isinstance(o, (list, tuple)):
+            h.update(b'[')
+            for x in o:
+                feed(x)
+            h.update(b']')
+        elif isinstance(o, np.ndarray):
+            h.update(b'A' + str(o.dtype).encode() + str(o.shape).encode())
+            h.update(np.ascontiguousarray(o).tobytes())
+        else:
+            h.update(b'S' + type(o).__name__.encode() + repr(o).encode())
+    for o in objs:
+        feed(o)
+    return h.hexdigest()
+
+
+def _plan_for(config, cfar_params, cluster_params, precomputed_data, device=0, precision='c128'):
+    key = _fingerprint(config, cfar_params, cluster_params, precomputed_data, device, precision)
+    p = _PLANS.pop(key, None)
     if p is None:
-        p = Plan(config, cfar_params, cluster_params, precomputed_data, device=device)
-        _PLANS[key] = p
+        p = Plan(config, cfar_params, cluster_params, precomputed_data, device=device, precision=precision)
+        while len(_PLANS) >= _MAX_PLANS:
+            _PLANS.popitem(last=False)[1].close()
+    _PLANS[key] = p
     return p
 
 
 def fun_process_single_frame(targets, config, cfar_params, cluster_params, precomputed_data, frame_idx,
-                             seed=20250101, device=0):
+                             seed=20250101, device=0, precision='c128'):
     """fun_process_single_frame.m:13 -- returns ``final_targets`` (list of dicts with
     Range, Velocity, Angle, Power).  Echo synthesis (S4) and noise (S4.1) run on the
-    device; MATLAB ``randn`` is replaced by the documented Philox stream (seed, frame_idx)."""
-    p = _plan_for(config, cfar_params, cluster_params, precomputed_data, device)
+    device; MATLAB ``randn`` is replaced by the documented Philox stream (seed, frame_idx).
+    Complex double by default, like MATLAB."""
+    p = _plan_for(config, cfar_params, cluster_params, precomputed_data, device, precision)
     return p.process_targets(targets, frame_idx=frame_idx, seed=seed)['final_targets']
 
 
-def process_stage2_mtd(iq_data, angle, config, cfar_params=None, cluster_params=None, precomputed_data=None,
-                       device=0):
-    """process_stage2_mtd.m:1 -- ``[MTD_results, PC_results]`` for beamformed data
-    ``iq_data[m, n, b]``.  ``angle`` (servo angle) is unused, as in the reference.
-    The reference's fun_MTD_produce is un-vendored; this backs it with fsf S6 + S7
-    using ``precomputed_data`` (built from ``config`` when omitted)."""
-    from .config import default_cfar_params as _dc, default_cluster_params as _dl
+def _stage2_precompute(config):
+    """precomputed_data for the stage-2 path built from ``config`` alone (the 3-argument call):
+    waveform, matched filters, segment geometry and MTD window of v8:79-135; the DBF weights,
+    beam angles and K-LUT are not used by stage 2 and are zero."""
+    sc = config['Sig_Config']
+    B = int(config.get('mtd', {}).get('beam_num', sc['beam_num']))
+    C = int(sc['channel_num'])
+    return precompute(config, np.zeros((B, C), complex), np.zeros(B), np.zeros(max(B - 1, 0)), V8_FIR)
+
+
+def process_stage2_mtd(iq_data, angle, config, precomputed_data=None, gate_cols=None, device=0, precision='c128'):
+    """process_stage2_mtd.m:1 -- ``[MTD_results, PC_results] = process_stage2_mtd(iq_data, angle, config)``.
+
+    ``iq_data[m, n, b]`` is beamformed fast-time data (the DBF of
+    debug_simulated_data_processing_v3.m:146-152), either the full PRT (``n`` = point_PRT) or
+    gated like the v2 ``.mat`` frames (main_simulate_echoes_with_array_v2.m:256-267: PRT columns
+    83:310, 311:1033, 1034:3486 side by side, n = 3404; other gatings via ``gate_cols``, 1-based
+    inclusive (first, last) per segment).  Gated columns are put back at their PRT positions
+    (zeros elsewhere).  ``angle`` (servo angle) is unused, as in the reference.  Returns
+    complex [P, G, B] arrays, G = N_total_gate (process_stage2_mtd.m:29-30 pre-sizes 332 x 3404
+    x 13 for the reference config).
+
+    The reference's arithmetic (fun_MTD_produce -> fun_lss_pulse_compression / fun_Process_MTD,
+    debug_simulated_data_processing_v2.m:259-405) is un-vendored; this backs it with the
+    per-frame chain's own S6 pulse compression + S7 MTD (fsf:99-136).  ``precomputed_data``
+    defaults to the one v8:79-135 builds from ``config``."""
     if precomputed_data is None:
-        raise ValueError('precomputed_data is required (fun_MTD_produce is not in the reference)')
-    p = _plan_for(config, cfar_params or _dc(), cluster_params or _dl(), precomputed_data, device)
-    return p.process_stage2(iq_data)
+        precomputed_data = _stage2_precompute(config)
+    p = _plan_for(config, default_cfar_params(), default_cluster_params(), precomputed_data, device, precision)
+    iq = np.asarray(iq_data)
+    if iq.ndim == 2:
+        iq = iq[:, :, None]
+    if iq.shape[1] == p.N:
+        return p.process_stage2(iq)
+    return p.process_stage2(iq, gate_cols=gate_cols if gate_cols is not None else REFERENCE_GATE_COLS)

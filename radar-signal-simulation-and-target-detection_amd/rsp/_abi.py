@@ -148,6 +148,7 @@ PROTOTYPES = {
                                      ct.POINTER(ct.c_int32), ct.POINTER(ct.c_int32)]),
     'rsp_results_clear': (ct.c_int32, [_P]),
     'rsp_process_stage2': (ct.c_int32, [_P, _P, ct.c_int32, _dp, _dp]),
+    'rsp_process_stage2_gated': (ct.c_int32, [_P, _P, ct.c_int32, ct.c_int32, ct.POINTER(ct.c_int32), _dp, _dp]),
     'rsp_profile_stages': (ct.c_int32, [_P, ct.POINTER(_P), ct.c_int32, ct.c_int32, ct.POINTER(ct.c_float),
                                         ct.POINTER(ct.c_int64), ct.c_int32, ct.POINTER(ct.c_int32)]),
     'rsp_stage_name': (ct.c_char_p, [ct.c_int32]),

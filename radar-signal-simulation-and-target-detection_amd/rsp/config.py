@@ -74,15 +74,43 @@ def steering_weights(angles_deg, C, d, wl, taper=None):
     return W * t[None, :] / t.sum()
 
 
-def calibrate_k_slopes(W, beam_angles_deg, d, wl):
-    """Restatement of calibrate_all_monopulse_slopes.m:35-73 for arbitrary B x C weights.
+def calibrate_all_monopulse_slopes(dbf_coeffs_C, beam_angles_deg, fc=9450e6, d=0.0138, c=C_LIGHT):
+    """Literal restatement of calibrate_all_monopulse_slopes.m:24-73.
 
-    For each adjacent pair: scan 501 angles over +-|dtheta| around the crossover,
-    responses w * a(theta) with a = exp(j 2 pi d n sin(theta)/wl), n = 0..C-1,
-    ratio (A-B)/(A+B), and the slope of polyfit(real(ratio), angle_offset, 1) over
-    the 11 points nearest the crossover.  Used for synthetic-weight configs; the
-    amplitude monopulse of fsf:280-290 is what consumes it.
-    """
+    ``dbf_coeffs_C`` is the B x C complex DBF table as read from the CSV (:24-25); the script
+    flips its channel order (:26, ``fliplr``).  For each adjacent pair (:35-72): 501 angles over
+    +-|dtheta| around the crossover (:44-47), steering vectors exp(j 2 pi d n sind(theta)/lambda),
+    n = 0..C-1 (:50-53), complex responses w * a (no conjugate, :56-57), the complex ratio
+    (A-B)/(A+B) (:58), and the slope p(1) of polyfit(real(ratio), angle - crossover, 1) over the
+    11 points around the crossover (:63-72).  Returns k_slopes_LUT (1 x B-1).
+
+    On the reference CSV this does NOT give the LUT hard-coded in v8:138 (SURVEY section 4,
+    negative KAT: about -2.54 ... -21.49), which is why the reference configs take the LUT as
+    input data."""
+    W = np.fliplr(np.asarray(dbf_coeffs_C, complex))                          # :26
+    B, C = W.shape
+    wl = c / fc                                                               # :17
+    n = np.arange(C)[:, None]                                                 # :50
+    k = np.zeros(B - 1)
+    for p in range(B - 1):                                                    # :35
+        xo = (beam_angles_deg[p] + beam_angles_deg[p + 1]) / 2                # :44
+        wdt = abs(beam_angles_deg[p] - beam_angles_deg[p + 1])                # :46
+        ang = np.linspace(xo - wdt, xo + wdt, 501)                            # :47
+        sv = np.exp(1j * 2 * np.pi * d * n * np.sin(np.deg2rad(ang))[None, :] / wl)   # :53
+        rA, rB = W[p] @ sv, W[p + 1] @ sv                                     # :56-57
+        ratio = (rA - rB) / (rA + rB)                                         # :58
+        ci = int(np.argmin(np.abs(ang - xo)))                                 # :63
+        sl = slice(ci - 5, ci + 6)                                            # :64-68
+        k[p] = np.polyfit(np.real(ratio[sl]), ang[sl] - xo, 1)[0]             # :71-72
+    return k
+
+
+def calibrate_k_slopes_amplitude(W, beam_angles_deg, d, wl):
+    """NOT the reference's calibration: the amplitude variant used for synthetic-weight configs
+    (BASELINE #4).  Same scan and fit as calibrate_all_monopulse_slopes.m:35-73, but with the
+    kernel's own beam outputs -- y = x * W' (fsf:95), i.e. responses conj(W) a(theta) -- and the
+    amplitude ratio (|A|-|B|)/(|A|+|B|) that the amplitude monopulse of fsf:280-290 forms, so that
+    K * ratio maps the kernel's ratio back to the angle offset for these weights."""
     B, C = W.shape
     n = np.arange(C)[:, None]
     k = np.zeros(B - 1)
@@ -92,7 +120,6 @@ def calibrate_k_slopes(W, beam_angles_deg, d, wl):
         wdt = abs(a0 - a1)
         ang = np.linspace(xo - wdt, xo + wdt, 501)
         sv = np.exp(1j * 2 * np.pi * d * n * np.sin(np.deg2rad(ang))[None, :] / wl)
-        # amplitude responses, consistent with the kernel's |.| monopulse (fsf:282-285)
         rA = np.abs(np.conj(W[p]) @ sv)
         rB = np.abs(np.conj(W[p + 1]) @ sv)
         ratio = (rA - rB) / (rA + rB)
@@ -140,7 +167,7 @@ def named_config(name):
         s = np.linspace(np.sin(np.deg2rad(-48.6)), np.sin(np.deg2rad(48.6)), 16)
         ang = np.rad2deg(np.arcsin(s))
         W = steering_weights(ang, 32, d, wl, taper=sw.taylor(32, nbar=4, sll=30, norm=False))
-        k = calibrate_k_slopes(W, ang, d, wl)
+        k = calibrate_k_slopes_amplitude(W, ang, d, wl)
         return cfg, cfar, clus, W, list(ang), list(k)
     raise KeyError(name)
 

@@ -159,20 +159,27 @@ class Plan:
             arr[i] = _abi.TargetIn(t['Range'], t['Velocity'], t['ElevationAngle'], t['SNR_dB'])
         return arr
 
-    def process_stage2(self, iq_beams):
-        """process_stage2_mtd backing: beams ``iq[m, n, b]`` -> (MTD [P,G,B], PC [P,G,B])."""
+    def process_stage2(self, iq_beams, gate_cols=None):
+        """process_stage2_mtd backing: beams ``iq[m, n, b]`` -> (MTD [P,G,B], PC [P,G,B]).
+        ``gate_cols``: ((first, last), ...) 1-based PRT columns of the segments of a gated
+        input (rsp_process_stage2_gated); None: ``n`` is the full PRT."""
         iq = np.asarray(iq_beams)
-        if iq.shape != (self.P, self.N, self.B):
-            raise ValueError('iq shape %r != (P, N, B) = %r' % (iq.shape, (self.P, self.N, self.B)))
         if iq.dtype == np.complex64:
             a, dt = np.asfortranarray(iq), _abi.RSP_C64
         else:
             a, dt = np.asfortranarray(iq, np.complex128), _abi.RSP_C128
         mtd = np.empty((self.P, self.G, self.B), np.complex128, order='F')
         pc = np.empty((self.P, self.G, self.B), np.complex128, order='F')
-        check(lib().rsp_process_stage2(self.h, a.ctypes.data_as(ct.c_void_p), dt,
-                                       mtd.ctypes.data_as(ct.POINTER(ct.c_double)),
-                                       pc.ctypes.data_as(ct.POINTER(ct.c_double))))
+        mo, po = mtd.ctypes.data_as(ct.POINTER(ct.c_double)), pc.ctypes.data_as(ct.POINTER(ct.c_double))
+        if gate_cols is None:
+            if iq.shape != (self.P, self.N, self.B):
+                raise ValueError('iq shape %r != (P, N, B) = %r' % (iq.shape, (self.P, self.N, self.B)))
+            check(lib().rsp_process_stage2(self.h, a.ctypes.data_as(ct.c_void_p), dt, mo, po))
+        else:
+            cols = (ct.c_int32 * 6)(*[int(x) for fl in gate_cols for x in fl])
+            if iq.shape[0] != self.P or iq.shape[2] != self.B:
+                raise ValueError('iq shape %r: expected (P, n, B) with P=%d B=%d' % (iq.shape, self.P, self.B))
+            check(lib().rsp_process_stage2_gated(self.h, a.ctypes.data_as(ct.c_void_p), dt, iq.shape[1], cols, mo, po))
         return mtd, pc
 
     # ---- device-resident queue -------------------------------------------------------------

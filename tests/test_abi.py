@@ -189,3 +189,19 @@ def test_plain_c_host_links_and_calls():
     assert int(out[0]) == 2
     assert float(out[1]) == pytest.approx((5 * 1000.0 + 7 * 1010.0) / 12, abs=1e-6)
     assert float(out[2]) == pytest.approx(12.0)
+
+
+def test_plan_cache_is_keyed_on_content():
+    """rsp._plan_for reuses a plan only for equal inputs (round-1 review: id()-keyed cache)."""
+    import numpy as np
+    import rsp
+    s = scenario('small')
+    a = rsp._fingerprint(s['cfg'], s['cfar'], s['clus'], s['pre_p'])
+    cf = dict(s['cfar'])
+    assert rsp._fingerprint(s['cfg'], cf, s['clus'], s['pre_p']) == a      # equal copy: same key
+    cf['T_CFAR'] = 9.0
+    assert rsp._fingerprint(s['cfg'], cf, s['clus'], s['pre_p']) != a      # other threshold: new key
+    pre = dict(s['pre_p'])
+    pre['MTD_win'] = np.array(pre['MTD_win'])
+    pre['MTD_win'][3] += 1e-12
+    assert rsp._fingerprint(s['cfg'], s['cfar'], s['clus'], pre) != a      # array contents count

@@ -172,6 +172,29 @@ def test_targets_found(case):
         assert any(abs(f['Range'] - t['Range']) < 15 for f in fg), 'target at %g m missed' % t['Range']
 
 
+def test_process_stage2_mtd_dropin_reference_gated():
+    """process_stage2_mtd(iq_data, angle, config) -- the literal 3-argument call of
+    debug_simulated_data_processing_v3.m:189 -- on the reference frame's DBF output gated like
+    the v2 .mat frames ([332 x 3404 x 13], main_simulate_echoes_with_array_v2.m:256-267): the
+    [332 x 3404 x 13] MTD and PC results (process_stage2_mtd.m:29-30) equal the oracle's S6 + S7
+    of the same columns put back at their PRT positions, to 1e-12 of the map maximum."""
+    import rsp
+    s = scenario('reference')
+    tg = targets_for('reference')
+    iq = chain.dbf(_input_cube('reference', s, tg), s['pre_o']['DBF_coeffs_data_C'])
+    cols = rsp.REFERENCE_GATE_COLS
+    gated = np.concatenate([iq[:, a - 1:b, :] for a, b in cols], axis=1)
+    assert gated.shape == (332, 3404, 13)
+    mtd, pc = rsp.process_stage2_mtd(gated, np.zeros(332), s['cfg'])
+    assert mtd.shape == pc.shape == (332, 3404, 13)
+    full = np.zeros_like(iq)
+    for a, b in cols:
+        full[:, a - 1:b, :] = iq[:, a - 1:b, :]
+    pc_o = chain.pulse_compress(full, s['pre_o'])
+    _map_close(pc, pc_o, MAP_TOL['c128'])
+    _map_close(mtd, chain.mtd(pc_o, s['pre_o']), MAP_TOL['c128'])
+
+
 @pytest.mark.parametrize('prec', ['c128', 'c64'])
 def test_synthesis_path_matches_oracle_cube(prec):
     s = scenario('small')

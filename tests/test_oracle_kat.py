@@ -195,3 +195,37 @@ def test_empty_paths():
     raw = chain.synthesize_echo([], cfg, pre) + chain.philox_noise(cfg, 1, 1)
     fin, st = chain.process_cube(raw, cfg, cfar, clus, pre, keep=True)
     assert fin == [] and st['dets'].shape == (0, 4) and st['par'] == []
+
+
+def test_k_calibration_literal_reproduces_negative_kat():
+    """calibrate_all_monopulse_slopes.m:24-73 restated literally (fliplr'd CSV weights, complex
+    w*a responses, real() of the complex ratio, 11-point polyfit) on the reference CSV gives the
+    SURVEY section-4 negative KAT K = [-2.54, -2.33, ..., -21.49] -- not the LUT hard-coded at
+    v8:138, which therefore stays input data."""
+    from rsp import config as C
+    k = C.calibrate_all_monopulse_slopes(C.load_reference_dbf(), C.V8_BEAM_ANGLES)
+    assert k.shape == (12,)
+    np.testing.assert_allclose(k[[0, 1, 5, 9, 11]], [-2.5448, -2.3314, -2.9340, -8.4438, -21.4863], atol=5e-4)
+    assert np.all(k < 0)
+    assert np.abs(k - np.asarray(C.V8_K_LUT)).max() > 1.0   # the hard-coded LUT is not reproducible
+
+
+def test_k_calibration_amplitude_variant_inverts_the_kernel_ratio():
+    """The amplitude variant (synthetic configs, BASELINE #4) is a different, named function: for
+    the x4 Taylor-tapered beams, K is the slope d(angle)/d(ratio) of the amplitude ratio
+    (|A|-|B|)/(|A|+|B|) of conj(W) a(theta) near the crossover (the ratio the amplitude monopulse
+    of fsf:280-290 computes), so K times a ratio change recovers the angle change."""
+    from rsp import config as C
+    cfg, _, _, W, ang, k = C.named_config('x4')
+    d, wl = cfg['Array']['element_spacing'], cfg['Sig_Config']['wavelength']
+    k2 = C.calibrate_k_slopes_amplitude(W, ang, d, wl)
+    np.testing.assert_array_equal(k, k2)
+    n = np.arange(W.shape[1])
+    def ratio(p, th):
+        a = np.exp(1j * 2 * np.pi * d * n * np.sin(np.deg2rad(th)) / wl)
+        A, B = abs(np.conj(W[p]) @ a), abs(np.conj(W[p + 1]) @ a)
+        return (A - B) / (A + B)
+    for p in (0, 7, 14):
+        xo = 0.5 * (ang[p] + ang[p + 1])
+        for off in (-0.05, 0.04):
+            assert k[p] * (ratio(p, xo + off) - ratio(p, xo)) == pytest.approx(off, rel=0.05)
