@@ -758,13 +758,32 @@ struct StoreRdm {   // last inverse pass: keep outputs i in [Lh-1, Lh-1+V) that 
 template <class T> constexpr int k2_sh() { return sizeof(T) == 4 ? 5 : RSP_K2_SH64; }
 #define K2_LDS_DATA(SH) (RSP_K2_POINTS + (RSP_K2_POINTS >> (SH)))
 
+// The block's twiddle tables are staged in LDS next to the rows: a pass's twiddles then arrive
+// with its LDS data reads instead of after an L2 round trip (-6% for k2_pc in complex double).
+// When the radix plan is a palindrome the inverse plan's table equals the forward one (the
+// conjugation happens in load_tw), so one copy serves both.
+constexpr bool k2_tw_sym(int LGM) {
+    for (int q = 0; q < n_passes(LGM); ++q)
+        if (rad_bits_p(LGM, q, false, RSP_K2_PAL) != rad_bits_p(LGM, n_passes(LGM) - 1 - q, false, RSP_K2_PAL))
+            return false;
+    return true;
+}
+constexpr int k2_tw_lds(int LGM) {
+    return tw_total(LGM, false, RSP_K2_CMP, RSP_K2_PAL) +
+           (k2_tw_sym(LGM) ? 0 : tw_total(LGM, true, RSP_K2_CMP, RSP_K2_PAL));
+}
+constexpr int k2_tw_lds_max() {
+    int m = 0;
+    for (int lg = 6; lg <= 11; ++lg) m = k2_tw_lds(lg) > m ? k2_tw_lds(lg) : m;
+    return m;
+}
+
 // One overlap-save block of one FFT segment for RSP_K2_POINTS / 2^LGM adjacent rows.
 // LDS round trips: forward pass 0 runs on the samples as loaded from z; the forward FFT's
 // last pass, the filter-spectrum product and the inverse FFT's first pass (radices in
 // reverse order, so that pass has the same butterflies) run in registers back to back;
 // the inverse FFT's last pass stores the kept gates to HBM.  2 (log2 M / 4) round trips
-// instead of 2 (log2 M / 4) + 3.  Twiddles are compact rows read in place from global
-// memory (L1/L2 resident).
+// instead of 2 (log2 M / 4) + 3.  Twiddles are compact rows, staged in LDS.
 template <class T, int LGM>
 __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k, const SegDesc& sd, const K2Job& job,
                                            const cx<T>* __restrict__ z, cx<T>* __restrict__ rdm, T* __restrict__ mag,
@@ -830,17 +849,21 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
         for (int r = 0; r < RL; ++r) hreg[t * RL + r] = H[sd.H_off + j + r * (M / RL)];
     }
     constexpr int NTWF = tw_total(LGM, false, CMP, PAL);
+    V* twL = L + K2_LDS_DATA(SH);
+    for (int e = tid; e < k2_tw_lds(LGM); e += K2_THREADS) twL[e] = twl[e];   // visible after the pass-0 barrier
+    const V* twF = twL;
+    const V* twI = k2_tw_sym(LGM) ? twL : twL + NTWF;
     // forward pass 0 (Ns = 1, no twiddles) straight from the loaded samples
     sh_store<R0, false, NB0, SH, K2_THREADS, LGM, 0>(v0, rs, rows, StoreLds<V>{L});
     __syncthreads();
     // forward passes 1 .. NP-2
-    fft_range<LGM, 1, NP - 1, RB0, 16, false, false, SH, K2_THREADS, CMP, PAL>(L, rs, rows, twl, StoreLds<V>{L},
+    fft_range<LGM, 1, NP - 1, RB0, 16, false, false, SH, K2_THREADS, CMP, PAL>(L, rs, rows, twF, StoreLds<V>{L},
                                                                                StoreLds<V>{L});
     // fused: forward last pass, x H (1/M folded in), inverse pass 0 of the reversed plan
     {
         V v[NBL][RL];
         sh_load<RL, false, NBL, SH, K2_THREADS, LGM, LGM - RBL, CMP>(L, rs, rows,
-                                                                      twl + tw_pass_off(LGM, NP - 1, false, CMP, PAL), v);
+                                                                      twF + tw_pass_off(LGM, NP - 1, false, CMP, PAL), v);
         __syncthreads();
 #pragma unroll
         for (int t = 0; t < NBL; ++t) {
@@ -855,7 +878,7 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     // outputs = stitched gates
     const int gend = min(sd.gb, g0 + sd.V);
     fft_range<LGM, 1, NP, RBL, 16, true, true, SH, K2_THREADS, CMP, PAL>(
-        L, rs, rows, twl + NTWF, StoreLds<V>{L},
+        L, rs, rows, twI, StoreLds<V>{L},
         StoreRdm<V>{buf_rsrc(rdm, (unsigned)(rows_total * G * sizeof(V))),
                     buf_rsrc(mag, (unsigned)(rows_total * g.Gp * sizeof(T))), G, g.Gp, row0, rows_total, Lh1, g0,
                     gend});
@@ -1158,18 +1181,30 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
     if (v1 <= v0 || cut_hi <= cut_lo) return;
     const double Tc = g.T;
     // mean() = sum / n over the slices of fsf:197-203 (max(a/n, b/n) = max(a, b)/n).  double: the
-    // quotient, as MATLAB; float: a multiply by 1/n (<= 1 ulp from the quotient)
+    // correctly rounded quotient, as MATLAB, without a division: q0 = x * RN(1/n), r = x - q0 n
+    // (exact, one FMA), q = RN(q0 + r RN(1/n)) is RN(x/n) (Markstein's theorem: RN(1/n) within half
+    // an ulp, q0 within one ulp of x/n; no underflow for these sums).  float: a multiply by 1/n
+    // (<= 1 ulp from the quotient).  With n_R = n_V (the reference's 5/5) max(nR, nV) is one
+    // quotient of the largest slice sum.
     const T fR = (T)rR, fV = (T)rV;
     const T iR = (T)1 / fR, iV = (T)1 / fV;
-    auto noise = [&](T a, T b, T fn, T in) -> T {
-        if constexpr (sizeof(T) == 8) return fmax(a, b) / fn;
-        else return fmaxf(a, b) * in;
+    auto quot = [&](T x, T fn, T in) -> T {
+        if constexpr (sizeof(T) == 8) {
+            const T q0 = x * in;
+            return __builtin_fma(__builtin_fma(-q0, fn, x), in, q0);
+        } else {
+            return x * in;
+        }
+    };
+    auto noise2 = [&](T lr, T tr, T lv, T tv) -> T {
+        if (FAST && RR == RV) return quot(fmax(fmax(lr, tr), fmax(lv, tv)), fR, iR);
+        const T nR = quot(fmax(lr, tr), fR, iR), nV = quot(fmax(lv, tv), fV, iV);
+        return nR > nV ? nR : nV;
     };
     bool overflow = false;
 #define K3_HIT(V, C, CUT, LR, TR, LV, TV)                                                               \
     do {                                                                                                \
-        const T nR_ = noise(LR, TR, fR, iR), nV_ = noise(LV, TV, fV, iV);                               \
-        if ((CUT) > (T)Tc * (nR_ > nV_ ? nR_ : nV_)) {                                                  \
+        if ((CUT) > (T)Tc * noise2(LR, TR, LV, TV)) {                                                   \
             const int qi = atomicAdd(qn, 1);                                                            \
             if (qi < K3_QCAP) queue[qi] = ((V) << 16) | (C);                                            \
             else overflow = true;                                                                       \
@@ -1456,7 +1491,7 @@ hipError_t launch_k1(const Geometry& g, const DevConsts& k, const FramePtrs& fp,
 template <class T>
 static hipError_t launch_k2_p(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int rows,
                               hipStream_t s) {
-    const size_t lds = (size_t)K2_LDS_DATA(k2_sh<T>()) * sizeof(cx<T>);
+    const size_t lds = (size_t)(K2_LDS_DATA(k2_sh<T>()) + k2_tw_lds_max()) * sizeof(cx<T>);
     hipError_t e = allow_lds(k2_pc<T>, lds);
     if (e != hipSuccess) return e;
     if (g.nwg_k2 > 0) hipLaunchKernelGGL(k2_pc<T>, dim3(g.nwg_k2, nf), dim3(K2_THREADS), lds, s, g, k, fp, rows);
