@@ -17,6 +17,10 @@
 #ifndef RSP_K2_CMP
 #define RSP_K2_CMP 1
 #endif
+// 2560-point mixed-radix overlap-save blocks (1) or powers of two only (0)
+#ifndef RSP_K2_MIX
+#define RSP_K2_MIX 1
+#endif
 #ifndef RSP_K2_SH64
 #define RSP_K2_SH64 5
 #endif

@@ -167,6 +167,69 @@ template <bool INV, class V> struct Dft<16, INV, V> {
     }
 };
 
+// Odd radices of the mixed-radix overlap-save blocks (M = 5 * 2^k, 3 * 2^k).
+template <bool INV, class V> struct Dft<3, INV, V> {
+    static __device__ __forceinline__ void run(V* a) {
+        typedef scal<V> S;
+        constexpr double h = 0.86602540378443864676;   // sin(2 pi / 3)
+        const V s = a[1] + a[2], d = a[1] - a[2];
+        const V t = a[0] - s * (S)0.5;
+        const V u = vrot<INV>(d) * (S)h;                // -+ i sin(2pi/3) (x1 - x2)
+        a[0] = a[0] + s;
+        a[1] = t + u;
+        a[2] = t - u;
+    }
+};
+template <bool INV, class V> struct Dft<5, INV, V> {
+    static __device__ __forceinline__ void run(V* a) {
+        typedef scal<V> S;
+        constexpr double c1 = 0.30901699437494742410, c2 = -0.80901699437494742410;   // cos(2pi/5), cos(4pi/5)
+        constexpr double s1 = 0.95105651629515357212, s2 = 0.58778525229247312917;    // sin(2pi/5), sin(4pi/5)
+        const V a1 = a[1] + a[4], b1 = a[1] - a[4], a2 = a[2] + a[3], b2 = a[2] - a[3];
+        const V r1 = a[0] + a1 * (S)c1 + a2 * (S)c2, r2 = a[0] + a1 * (S)c2 + a2 * (S)c1;
+        const V u1 = vrot<INV>(b1 * (S)s1 + b2 * (S)s2), u2 = vrot<INV>(b1 * (S)s2 - b2 * (S)s1);
+        a[0] = a[0] + a1 + a2;
+        a[1] = r1 + u1;
+        a[4] = r1 - u1;
+        a[2] = r2 + u2;
+        a[3] = r2 - u2;
+    }
+};
+// Good-Thomas prime-factor DFT of N = N1 N2 (coprime), no internal twiddles: input n =
+// (N2 n1 + N1 n2) mod N, output k = (N2 (N2^-1 mod N1) k1 + N1 (N1^-1 mod N2) k2) mod N.
+constexpr int inv_mod(int a, int m) {
+    for (int x = 1; x < m; ++x)
+        if ((a * x) % m == 1) return x;
+    return 1;
+}
+template <int N1, int N2, bool INV, class V>
+__device__ __forceinline__ void dft_pfa(V* a) {
+    constexpr int N = N1 * N2;
+    V y[N1][N2];
+#pragma unroll
+    for (int n1 = 0; n1 < N1; ++n1) {
+#pragma unroll
+        for (int n2 = 0; n2 < N2; ++n2) y[n1][n2] = a[(N2 * n1 + N1 * n2) % N];
+        Dft<N2, INV, V>::run(y[n1]);
+    }
+#pragma unroll
+    for (int k2 = 0; k2 < N2; ++k2) {
+        V c[N1];
+#pragma unroll
+        for (int n1 = 0; n1 < N1; ++n1) c[n1] = y[n1][k2];
+        Dft<N1, INV, V>::run(c);
+#pragma unroll
+        for (int k1 = 0; k1 < N1; ++k1)
+            a[(N2 * inv_mod(N2 % N1, N1) * k1 + N1 * inv_mod(N1 % N2, N2) * k2) % N] = c[k1];
+    }
+}
+template <bool INV, class V> struct Dft<10, INV, V> {
+    static __device__ __forceinline__ void run(V* a) { dft_pfa<2, 5, INV>(a); }
+};
+template <bool INV, class V> struct Dft<12, INV, V> {
+    static __device__ __forceinline__ void run(V* a) { dft_pfa<4, 3, INV>(a); }
+};
+
 constexpr int clog2(int x) { return x <= 1 ? 0 : 1 + clog2(x >> 1); }
 
 // LDS index inside a row: SH > 0 inserts one complex every 2^SH to break power-of-two
@@ -350,6 +413,56 @@ template <int LG, int PTS, int SH, int NTHR, class V, class StMid, class StLast>
 __device__ __forceinline__ void fft_passes(V* buf, int rs, int nrows, const V* tw, const StMid& mid,
                                            const StLast& last) {
     fft_range<LG, 0, n_passes(LG), 0, PTS, false, false, SH, NTHR, false>(buf, rs, nrows, tw, mid, last);
+}
+
+// ---- Stockham passes of any length L and radix R (mixed-radix overlap-save blocks) ----------
+// Same formulation as sh_load / sh_store with L, R, Ns compile-time constants that need not be
+// powers of two: divisions by them become multiply-shifts, and every LDS index is padded per
+// element (lidx of the full position).
+template <int R, bool INV, int NB, int SH, int NTHR, int L, int NS, bool CMP, class V>
+__device__ __forceinline__ void shg_load(const V* buf, int rs, int nrows, const V* tw, V (&v)[NB][R]) {
+    constexpr int nb = L / R;
+    const int total = nb * nrows;
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+        const int beta = threadIdx.x + t * NTHR;
+        if (beta < total) {
+            const int row = beta / nb, j = beta - row * nb;
+            const V* src = buf + row * rs;
+            V w[R];
+            if (NS > 1) load_tw<R, INV, CMP>(tw + (j % NS) * tw_row(R, CMP), w);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                V x = src[lidx<SH>(j + r * nb)];
+                if (r > 0 && NS > 1) x = vmul(x, w[r]);
+                v[t][r] = x;
+            }
+        }
+    }
+}
+template <int R, bool INV, int NB, int SH, int NTHR, int L, int NS, class V, class St>
+__device__ __forceinline__ void shg_store(V (&v)[NB][R], int rs, int nrows, const St& st) {
+    constexpr int nb = L / R;
+    const int total = nb * nrows;
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+        const int beta = threadIdx.x + t * NTHR;
+        if (beta < total) {
+            const int row = beta / nb, j = beta - row * nb;
+            Dft<R, INV, V>::run(v[t]);
+            const int idxD = (j / NS) * (NS * R) + j % NS;
+#pragma unroll
+            for (int r = 0; r < R; ++r) st.put(t * R + r, row, idxD + r * NS, row * rs + lidx<SH>(idxD + r * NS), v[t][r]);
+        }
+    }
+}
+template <int R, bool INV, int NB, int SH, int NTHR, int L, int NS, bool CMP, class V, class St>
+__device__ __forceinline__ void shg_pass(V* buf, int rs, int nrows, const V* tw, const St& st) {
+    V v[NB][R];
+    shg_load<R, INV, NB, SH, NTHR, L, NS, CMP>(buf, rs, nrows, tw, v);
+    __syncthreads();
+    shg_store<R, INV, NB, SH, NTHR, L, NS>(v, rs, nrows, st);
+    __syncthreads();
 }
 
 __device__ __forceinline__ int ilog2(int x) { return 31 - __clz(x); }
@@ -773,7 +886,7 @@ constexpr int k2_tw_lds(int LGM) {
            (k2_tw_sym(LGM) ? 0 : tw_total(LGM, true, RSP_K2_CMP, RSP_K2_PAL));
 }
 constexpr int k2_tw_lds_max() {
-    int m = 0;
+    int m = 16 * tw_row(10, RSP_K2_CMP) + 160 * tw_row(16, RSP_K2_CMP);   // k2_fft_job_mix<2560>
     for (int lg = 6; lg <= 11; ++lg) m = k2_tw_lds(lg) > m ? k2_tw_lds(lg) : m;
     return m;
 }
@@ -884,6 +997,96 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
                     gend});
 }
 
+
+// Mixed-radix overlap-save block M = 16 x R1 x 16 (2560 = 16 x 10 x 16): one block of M = 2560
+// covers x2's long segment (Lh = 700, 1860 gates), which takes two 2048-point blocks in powers of
+// two -- 37.5% fewer points.  One row per workgroup: the radix-16 passes run 160 butterflies
+// (waves 0-2, the fourth wave skips them), the radix-10 passes 256.  The plan is a palindrome,
+// so the inverse FFT runs the same radices, the fused middle pass (forward radix-16 pass, x H,
+// inverse radix-16 pass 0) has the same butterflies on both sides as in k2_fft_job, and the
+// inverse twiddle table equals the forward one (conjugated in load_tw).
+template <class T, int M, int R1>
+__device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConsts& k, const SegDesc& sd, const K2Job& job,
+                                               const cx<T>* __restrict__ z, cx<T>* __restrict__ rdm, T* __restrict__ mag,
+                                               int row0, int rows_total, cx<T>* L) {
+    typedef cx<T> V;
+    constexpr int SH = k2_sh<T>();
+    constexpr int R0 = 16;
+    static_assert(M == R0 * R1 * R0, "palindromic 3-pass plan");
+    constexpr int rows = RSP_K2_POINTS / M;
+    static_assert(rows >= 1, "block larger than the workgroup");
+    constexpr int rs = M + (M >> SH);
+    constexpr bool CMP = RSP_K2_CMP;
+    constexpr int nb0 = M / R0;                                          // radix-16 butterflies per row
+    constexpr int NB0 = (nb0 * rows + K2_THREADS - 1) / K2_THREADS;
+    constexpr int NB1 = ((M / R1) * rows + K2_THREADS - 1) / K2_THREADS;
+    constexpr int NS1 = R0, NS2 = R0 * R1;                               // Ns of passes 1 and 2
+    constexpr int TW2 = NS1 * tw_row(R1, CMP);                           // offset of pass 2's table
+    constexpr int NTWF = TW2 + NS2 * tw_row(R0, CMP);
+    const int P = g.P, G = g.G;
+    const int lo = sd.lo, hi = sd.hi, off = sd.off;
+    const int tid = threadIdx.x;
+    const int Lh1 = sd.Lh - 1;
+    const int g0 = sd.ga + job.blk * sd.V;
+    const int a = sd.seg_lo + g0 - Lh1;
+    const V* twl = static_cast<const V*>(k.twM) + sd.tw_off;
+    const V* __restrict__ H = static_cast<const V*>(k.H);
+    V v0[NB0][R0];
+    V hreg[NB0][R0];
+    const int lgNT = ilog2(g.NT);
+    const __amdgpu_buffer_rsrc_t zr = buf_rsrc(z, (unsigned)(g.B * g.ntiles * P * g.NT * sizeof(V)));
+#pragma unroll
+    for (int t = 0; t < NB0; ++t) {
+        const int beta = tid + t * K2_THREADS;
+        const int rl = beta / nb0, j = beta - rl * nb0;
+        const int rho = row0 + rl;
+        const bool live = beta < nb0 * rows && rho < rows_total;
+        const int b = rho / P, v = rho - b * P;
+        const int np0 = a + j - lo + off;
+        const int zb = ((b * g.ntiles + (np0 >> lgNT)) * P + v) * g.NT + (np0 & (g.NT - 1));
+#pragma unroll
+        for (int r = 0; r < R0; ++r) {
+            const int n = a + j + r * nb0;
+            const bool ok = live && n >= lo && n <= hi;
+            const unsigned e = ((nb0 & (g.NT - 1)) == 0) ? (unsigned)(zb + r * nb0 * P) : (unsigned)zaddr(g, b, v, n - lo + off);
+            v0[t][r] = buf_ld<V>(zr, ok ? e * (unsigned)sizeof(V) : RSP_OOB);
+        }
+#pragma unroll
+        for (int r = 0; r < R0; ++r) hreg[t][r] = H[sd.H_off + j + r * nb0];   // fused pass outputs j + r M/16
+    }
+    V* twL = L + K2_LDS_DATA(SH);
+    for (int e = tid; e < NTWF; e += K2_THREADS) twL[e] = twl[e];
+    const V* twF = twL;
+    const V* twI = twF;   // palindrome: the reversed plan's table is the forward one
+    shg_store<R0, false, NB0, SH, K2_THREADS, M, 1>(v0, rs, rows, StoreLds<V>{L});
+    __syncthreads();
+    shg_pass<R1, false, NB1, SH, K2_THREADS, M, NS1, CMP>(L, rs, rows, twF, StoreLds<V>{L});
+    {
+        V v[NB0][R0];
+        shg_load<R0, false, NB0, SH, K2_THREADS, M, NS2, CMP>(L, rs, rows, twF + TW2, v);
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < NB0; ++t) {
+            Dft<R0, false, V>::run(v[t]);
+#pragma unroll
+            for (int r = 0; r < R0; ++r) v[t][r] = vmul(v[t][r], hreg[t][r]);
+        }
+        shg_store<R0, true, NB0, SH, K2_THREADS, M, 1>(v, rs, rows, StoreLds<V>{L});
+        __syncthreads();
+    }
+    shg_pass<R1, true, NB1, SH, K2_THREADS, M, NS1, CMP>(L, rs, rows, twI, StoreLds<V>{L});
+    const int gend = min(sd.gb, g0 + sd.V);
+    {
+        V v[NB0][R0];
+        shg_load<R0, true, NB0, SH, K2_THREADS, M, NS2, CMP>(L, rs, rows, twI + TW2, v);
+        shg_store<R0, true, NB0, SH, K2_THREADS, M, NS2>(
+            v, rs, rows,
+            StoreRdm<V>{buf_rsrc(rdm, (unsigned)(rows_total * G * sizeof(V))),
+                        buf_rsrc(mag, (unsigned)(rows_total * g.Gp * sizeof(T))), G, g.Gp, row0, rows_total, Lh1, g0,
+                        gend});
+    }
+}
+
 template <class T>
 __global__ __launch_bounds__(K2_THREADS, 512 / K2_THREADS) void k2_pc(Geometry g, DevConsts k, FramePtrs fp, int rows_total) {
     typedef cx<T> V;
@@ -903,7 +1106,9 @@ __global__ __launch_bounds__(K2_THREADS, 512 / K2_THREADS) void k2_pc(Geometry g
     const int lo = sd.lo, hi = sd.hi, off = sd.off;
     const int tid = threadIdx.x;
 
-    if (sd.type == 1) {
+    if (sd.type == 1 && sd.logM == 0) {   // mixed-radix block
+        k2_fft_job_mix<T, 2560, 10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L);
+    } else if (sd.type == 1) {
         switch (sd.logM) {
             case 6: k2_fft_job<T, 6>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
             case 7: k2_fft_job<T, 7>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
@@ -1107,14 +1312,18 @@ template <> struct U16<float> { typedef f32x4 U; static constexpr int E = 4; };
 template <> struct U16<double> { typedef d2 U; static constexpr int E = 2; };
 
 // RR/RV/GR/GV = reference/guard cell counts when known at compile time (the reference's
-// 5/5/10/10, v8:45-46), 0 = runtime.  Tiles: RT range cells x all P Doppler cells of one beam
-// pair, tile starts aligned to 4 cells so that the magnitude rows load as 16-B units.
-template <class T, int RR, int RV, int GR, int GV>
+// 5/5/10/10, v8:45-46), 0 = runtime; RTC = the tile width g.cfar_RT when they are (32 or 64),
+// so that the LDS row stride and every window offset are compile-time constants.  Tiles: RT
+// range cells x all P Doppler cells of one beam pair, tile starts aligned to 4 cells so that
+// the magnitude rows load as 16-B units.
+template <class T, int RR, int RV, int GR, int GV, int RTC>
 __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts k, FramePtrs fp) {
     T* S = reinterpret_cast<T*>(rsp_lds);   // [P][W] | queue[K3_QCAP] | qn, base
     typedef typename U16<T>::U U;
     constexpr int EPU = U16<T>::E;
-    constexpr bool FAST = RR > 0 && RV > 0 && GR > 0 && GV > 0;
+    constexpr bool FAST = RR > 0 && RV > 0 && GR > 0 && GV > 0 && (RTC == 32 || RTC == 64);
+    constexpr int HRC = ((RR + GR > 2 ? RR + GR : 2) + 3) & ~3;   // = g.cfar_hR (rsp_plan.cpp)
+    constexpr int WC = (RTC + 2 * HRC + 3) & ~3;                 // = g.cfar_W
     // XCD-aware order (bijective swizzle, cdna_hip_programming.md T1): the workgroups that
     // share an XCD take consecutive (tile, pair) ids with pairs fastest, so beam b's tile --
     // read by pairs b-1 and b -- and the range halos of neighbouring tiles are L2 hits
@@ -1126,7 +1335,7 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
     }
     const int pair = wg % npair, col = wg / npair;
     const int tile = col % ntile, f = col / ntile;
-    const int P = g.P, G = g.G, W = g.cfar_W, hR = g.cfar_hR, RT = g.cfar_RT;
+    const int P = g.P, G = g.G, W = FAST ? WC : g.cfar_W, hR = FAST ? HRC : g.cfar_hR, RT = FAST ? RTC : g.cfar_RT;
     const int rR = RR ? RR : g.refR, gR = GR ? GR : g.guardR, rV = RV ? RV : g.refV, gV = GV ? GV : g.guardV;
     const int rc0 = rR + gR;                           // first cell under test (0-based)
     const int tstart = (rc0 & ~3) + tile * RT;         // multiple of 4
@@ -1140,7 +1349,34 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
     if (threadIdx.x == 0) qn[0] = 0;
     // ---- load S = |A| + |B| (fsf:184-187) from the magnitude maps: 16 B per lane,
     //      K3_VEC units of each beam in flight per thread
-    {
+    if constexpr (FAST) {
+        // a thread keeps one 16-B column unit and walks the rows: one address add per load
+        constexpr int WU = WC / EPU, NTR = RSP_THREADS / WU;
+        const int u = threadIdx.x % WU, rr = threadIdx.x / WU;
+        const int r = c0 + EPU * u;
+        const bool colok = rr < NTR && r >= 0 && r < G;   // rows are padded to Gp: r + EPU - 1 < Gp
+        const T* pa = MA + (size_t)rr * Gp + r;
+        const T* pb = MB + (size_t)rr * Gp + r;
+        U* sd = reinterpret_cast<U*>(S + rr * WC) + u;
+        for (int vb = 0; vb < P; vb += K3_VEC * NTR) {
+            U xa[K3_VEC], xb[K3_VEC];
+#pragma unroll
+            for (int q = 0; q < K3_VEC; ++q) {
+                xa[q] = U{};
+                xb[q] = xa[q];
+                if (colok && vb + rr + q * NTR < P) {
+                    xa[q] = *reinterpret_cast<const U*>(pa + (size_t)(vb + q * NTR) * Gp);
+                    xb[q] = *reinterpret_cast<const U*>(pb + (size_t)(vb + q * NTR) * Gp);
+#pragma unroll
+                    for (int e = 1; e < EPU; ++e)
+                        if (r + e >= G) { xa[q][e] = 0; xb[q][e] = 0; }
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < K3_VEC; ++q)
+                if (rr < NTR && vb + rr + q * NTR < P) sd[(vb + q * NTR) * WU] = xa[q] + xb[q];
+        }
+    } else {
         const int WU = W / EPU, nu = P * WU;
         for (int e0 = 0; e0 < nu; e0 += K3_VEC * RSP_THREADS) {
             U xa[K3_VEC], xb[K3_VEC];
@@ -1212,13 +1448,13 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
     } while (0)
     // ---- cross GOCA-CFAR (fsf:192-213); hits go to an LDS queue so that the S9 work is
     //      spread over the whole workgroup instead of serialising in the lane that owns a range cell
-    if (FAST && (RT == 64 || RT == 32)) {   // RT = 32: long-P / double tiles (LDS cap in the plan)
+    if constexpr (FAST) {   // RT = 32: long-P / double tiles (LDS cap in the plan)
         // a thread takes 4 adjacent range cells of one Doppler row: every window value comes
         // from 16-B LDS reads; sums run left to right over each slice like mean()
         constexpr int DL = -(GR + RR), DR = GR + 1;              // window starts rel. to the cell
         constexpr int BL = floor4(DL), BR = floor4(DR);
         constexpr int NL = (DL + 3 + RR - BL + 3) / 4, NR = (DR + 3 + RR - BR + 3) / 4;
-        const int lgT = RT == 64 ? 4 : 3;                         // log2 threads per row (RT / 4)
+        constexpr int lgT = RTC == 64 ? 4 : 3;                    // log2 threads per row (RT / 4)
         const int q = threadIdx.x & ((1 << lgT) - 1);
         const int c = hR + 4 * q;                                 // first tile column of the group
         const int r = c0 + c;
@@ -1229,7 +1465,7 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
         const int rgp = lgT == 4 ? (rg & ~3) | ((rg & 1) << 1) | ((rg >> 1) & 1) : rg;
 #pragma unroll 1
         for (int v = v0 + rgp; v < v1; v += RSP_THREADS >> lgT) {
-            const T* row = S + v * W + c;
+            const T* row = S + v * WC + c;
             T xl[4 * NL], xr[4 * NR], cv[4];
             T lv[4] = {0, 0, 0, 0}, tv[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -1250,8 +1486,8 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
 #pragma unroll
             for (int qq = 0; qq < RV; ++qq) {
                 T a[4], b[4];
-                ld4(row + (qq - GV - RV) * W, a);
-                ld4(row + (qq + GV + 1) * W, b);
+                ld4(row + (qq - GV - RV) * WC, a);
+                ld4(row + (qq + GV + 1) * WC, b);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     lv[i] += a[i];
@@ -1508,12 +1744,16 @@ static hipError_t launch_k3_p(const Geometry& g, const DevConsts& k, const Frame
     const size_t lds = (size_t)g.P * g.cfar_W * sizeof(T) + (K3_QCAP + 4) * sizeof(int);
     const dim3 grid(k3_ntiles(g) * (g.B - 1) * nf);   // 1-D; k3_cfar remaps it XCD-aware
     hipError_t e;
-    if (g.refR == 5 && g.refV == 5 && g.guardR == 10 && g.guardV == 10) {   // the reference's cfar_params (v8:45-46)
-        if ((e = allow_lds(k3_cfar<T, 5, 5, 10, 10>, lds)) != hipSuccess) return e;
-        hipLaunchKernelGGL((k3_cfar<T, 5, 5, 10, 10>), grid, dim3(RSP_THREADS), lds, s, g, k, fp);
+    const bool ref = g.refR == 5 && g.refV == 5 && g.guardR == 10 && g.guardV == 10;   // the reference's cfar_params (v8:45-46)
+    if (ref && g.cfar_RT == 64) {
+        if ((e = allow_lds(k3_cfar<T, 5, 5, 10, 10, 64>, lds)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k3_cfar<T, 5, 5, 10, 10, 64>), grid, dim3(RSP_THREADS), lds, s, g, k, fp);
+    } else if (ref && g.cfar_RT == 32) {
+        if ((e = allow_lds(k3_cfar<T, 5, 5, 10, 10, 32>, lds)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k3_cfar<T, 5, 5, 10, 10, 32>), grid, dim3(RSP_THREADS), lds, s, g, k, fp);
     } else {
-        if ((e = allow_lds(k3_cfar<T, 0, 0, 0, 0>, lds)) != hipSuccess) return e;
-        hipLaunchKernelGGL((k3_cfar<T, 0, 0, 0, 0>), grid, dim3(RSP_THREADS), lds, s, g, k, fp);
+        if ((e = allow_lds(k3_cfar<T, 0, 0, 0, 0, 0>, lds)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k3_cfar<T, 0, 0, 0, 0, 0>), grid, dim3(RSP_THREADS), lds, s, g, k, fp);
     }
     return hipGetLastError();
 }

@@ -114,6 +114,20 @@ void build_pass_twiddles(int m, std::vector<cd>& out, bool rev = false, bool cmp
     }
 }
 
+// Mixed-radix overlap-save block M = 16 x R1 x 16 (k2_fft_job_mix): a palindrome, so the
+// inverse table (reversed radices) is the forward one and only the forward table is stored.
+void build_mix_twiddles(int R1, std::vector<cd>& out, bool cmp) {
+    const int rad[3] = {16, R1, 16};
+    int Ns = 1;
+    for (int q = 0; q < 3; ++q) {
+        const int R = rad[q];
+        if (q > 0)
+            for (int k = 0; k < Ns; ++k)
+                for (int r = 1; r < R; r = cmp ? 2 * r : r + 1) out.push_back(root_of_unity((long long)k * r, (long long)Ns * R));
+        Ns *= R;
+    }
+}
+
 double mround(double x) { return x < 0 ? -std::floor(-x + 0.5) : std::floor(x + 0.5); }
 
 struct Lane {
@@ -272,20 +286,23 @@ int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga,
     s.lo = std::max(seg_lo, seg_lo + ga - (Lh - 1));
     s.hi = std::min(seg_lo + Ls - 1, seg_lo + gb - 1);
     // overlap-save block size M = 2^k <= 2048 (so that a workgroup owns >= 2 adjacent rows:
-    // 128 B contiguous loads of z); cost model blocks * M * (log2 M + 2)
+    // 128 B contiguous loads of z) or the mixed-radix 2560 = 16 x 10 x 16 (one row per workgroup,
+    // RSP_K2_MIX); cost model blocks * M * (log2 M + 2)
     const int nout = gb - ga;
     double best = 1e300;
     int bestM = 0;
-    for (int M = 64; M <= 2048; M *= 2) {
+    const int cand[] = {64, 128, 256, 512, 1024, 2048, RSP_K2_MIX ? 2560 : 0};
+    for (int M : cand) {
         const int V = M - Lh + 1;
-        if (V < 1) continue;
+        if (M == 0 || V < 1) continue;
         const int nb = (nout + V - 1) / V;
         const double cost = (double)nb * M * (std::log2((double)M) + 2);
         if (cost < best * 0.999) { best = cost; bestM = M; }
     }
     if (!bestM) return fail(RSP_ERR_UNSUPPORTED, "%s filter length %d exceeds the 2048-point block", name, Lh);
     const int M = bestM;
-    s.M = M; s.logM = ilog2i(M); s.V = M - Lh + 1;
+    const bool mix = !is_pow2(M);
+    s.M = M; s.logM = mix ? 0 : ilog2i(M); s.V = M - Lh + 1;
     s.nblocks = (nout + s.V - 1) / s.V;
     s.rows_per_wg = RSP_K2_POINTS / M;
     // spectrum of h zero-padded to M, natural order, 1/M folded in
@@ -299,8 +316,12 @@ int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga,
     if (ti < 0) {
         tw_sizes.push_back(M);
         tw_offs.push_back((int)twM.size());
-        build_pass_twiddles(s.logM, twM, false, RSP_K2_CMP, RSP_K2_PAL);   // forward FFT (compact rows, palindromic plan)
-        build_pass_twiddles(s.logM, twM, true, RSP_K2_CMP, RSP_K2_PAL);    // inverse FFT (reversed radices)
+        if (mix) {
+            build_mix_twiddles(M / 256, twM, RSP_K2_CMP);
+        } else {
+            build_pass_twiddles(s.logM, twM, false, RSP_K2_CMP, RSP_K2_PAL);   // forward FFT (compact rows, palindromic plan)
+            build_pass_twiddles(s.logM, twM, true, RSP_K2_CMP, RSP_K2_PAL);    // inverse FFT (reversed radices)
+        }
         ti = (int)tw_sizes.size() - 1;
     }
     s.tw_off = tw_offs[ti];
