@@ -74,6 +74,12 @@ def parse():
     ap.add_argument('--cpu-frames', type=int, default=0, help='oracle frames for cpu_baseline (0 = auto ~15 s)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--batch', type=int, default=1024, help='MUSIC instances per launch (--config music5)')
+    ap.add_argument('--frames-total', type=int, default=0,
+                    help='BASELINE config #3 mode: this many distinct frames (e.g. 512), sharded over the ranks, '
+                         'each processed once (the default mode times --steps batches over a ring)')
+    ap.add_argument('--e2e', action='store_true',
+                    help='end-to-end mode: frames enter as host cubes in pinned memory (rsp_enqueue_host: '
+                         'async H2D of the used samples overlapping the kernels), not the headline')
     ap.add_argument('--stage-timing', action='store_true',
                     help='HIP events around every kernel in the timed region (diagnostic: overlapped durations)')
     return ap.parse_args()
@@ -239,16 +245,39 @@ def main():
     sz = plan.sizes
     targets = scene(cfg)
     cube_bytes = plan.cube_bytes
-    ring = [plan.device_alloc(cube_bytes) for _ in range(a.ring)]
+    if a.frames_total:   # config #3: every frame distinct, frame ids global across the ranks
+        share = [(a.frames_total * r // world, a.frames_total * (r + 1) // world) for r in range(world)]
+        f0, f1 = share[rank]
+        nring = f1 - f0
+    else:
+        f0, nring = 1000 * rank, a.ring
+    ring = [plan.device_alloc(cube_bytes) for _ in range(nring)]
     tg = targets
+    for _ in range(f0 if a.frames_total else 0):   # the scene evolved to this rank's first frame
+        tg = C.evolve_targets(tg, cfg)
     for i, p in enumerate(ring):
-        plan.synthesize_device(p, tg, frame_idx=1 + i + 1000 * rank, seed=20250101 + rank)
+        plan.synthesize_device(p, tg, frame_idx=1 + i + f0, seed=20250101 + (0 if a.frames_total else rank))
         tg = C.evolve_targets(tg, cfg)
     plan.sync()
+    hring = []
+    if a.e2e:   # host copies of the ring cubes in pinned memory
+        for p in ring[:4]:
+            h = plan.host_alloc(cube_bytes)
+            cube = plan.host_cube(h)
+            cube[...] = plan.device_download(p, cube.size, plan.cdtype).reshape(cube.shape, order='F')
+            hring.append(h)
 
     def run(nbatches, base):   # nbatches full batches of fpl frames
         for i in range(nbatches * a.fpl):
-            plan.enqueue(ring[i % a.ring], base + i)
+            if a.e2e:
+                plan.enqueue_host(hring[i % len(hring)], base + i)
+            else:
+                plan.enqueue(ring[i % len(ring)], base + i)
+        plan.drain()
+
+    def run_all():   # config #3: each of this rank's frames once
+        for i, p in enumerate(ring):
+            plan.enqueue(p, 1 + f0 + i)
         plan.drain()
 
     run(max(a.warmup, 2 * NLANES), 0)   # every lane (stream) warmed with full batches
@@ -259,7 +288,10 @@ def main():
     plan.sync()
     plan.set_stage_timing(a.stage_timing)   # optional live HIP events around K1/K2/K3 of every batch
     t0 = time.perf_counter()
-    run(a.steps, 1)
+    if a.frames_total:
+        run_all()
+    else:
+        run(a.steps, 1)
     res = plan.results(clear=True)
     n_targets_local = sum(len(r['final_targets']) for r in res)
     if dist is not None:
@@ -282,7 +314,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
-    frames = a.steps * a.fpl * world
+    frames = a.frames_total if a.frames_total else a.steps * a.fpl * world
     fps = frames / el
     cells = sz.B * sz.G * sz.P
     out = None
@@ -314,17 +346,27 @@ def main():
                 dom['pmc_traffic_bytes'] = traffic
         esz = sz.elem_bytes
         frame_alg_bytes = sz.C * sz.N * sz.P * esz + cells * esz   # cube read + RD map write
+        metric = 'frames/sec + range-Doppler cells/sec, %dch×%dbeam×%dsamp×%dpulse' % (sz.C, sz.B, sz.N, sz.P)
+        cfg_no = {'x2': '2', 'x4': '4', 'plumbing': '1'}.get(a.config, '-')
+        if a.frames_total:
+            metric += ', batch of %d independent frames sharded over %d GPU(s)' % (a.frames_total, world)
+            cfg_no = '3'
+        if a.e2e:
+            metric += ', end to end (host cubes in pinned memory -> H2D of the used samples -> chain)'
+        steps = (a.frames_total + a.fpl - 1) // a.fpl if a.frames_total else a.steps
         out = {
-            'metric': 'frames/sec + range-Doppler cells/sec, %dch×%dbeam×%dsamp×%dpulse' % (sz.C, sz.B, sz.N, sz.P),
-            'value': fps, 'unit': 'frames/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
-            'ms_per_step': el / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
+            'metric': metric,
+            'value': fps, 'unit': 'frames/s', 'n_gpus': world, 'steps': steps, 'warmup': a.warmup,
+            'ms_per_step': el / steps * 1e3, 'higher_is_better': True,
+            'scaling': 'strong' if a.frames_total else 'weak',
             'vs_baseline': None,
             'dtype': 'fp64 (complex128)' if a.precision == 'c128' else 'fp32 (complex64)',
             'data': 'synthetic (device Philox noise + v8_2 targets)',
             'cells_per_s': fps * cells,
             'achieved_GBps_frame': fps * frame_alg_bytes / 1e9,
             'config': {'workload': 'BASELINE config #%s: %s C=%d B=%d N=%d P=%d G=%d' % (
-                {'x2': '2', 'x4': '4', 'plumbing': '1'}.get(a.config, '-'), a.config, sz.C, sz.B, sz.N, sz.P, sz.G), 'frames_per_launch': a.fpl, 'frames_per_step': a.fpl, 'ring': a.ring,
+                cfg_no, a.config, sz.C, sz.B, sz.N, sz.P, sz.G), 'frames_per_launch': a.fpl, 'frames_per_step': a.fpl,
+                'ring': len(hring) if a.e2e else len(ring),
                 'parallelism': 'frame-sharded x%d' % world, 'used_samples': sz.used_samples,
                 'targets_reported': n_targets_all},
             'roofline': {'bound': 'hbm', 'kernel': dom['stage'], 'achieved': achieved, 'peak': HBM_PEAK_GBS,
@@ -336,12 +378,17 @@ def main():
                                    'trace)' % a.profile_iters,
                          'stages': stages},
         }
+        if a.e2e:
+            out['e2e_h2d_bytes_per_frame'] = sz.C * sz.used_samples * sz.P * esz
+            out['e2e_h2d_GBps'] = fps * out['e2e_h2d_bytes_per_frame'] / 1e9
         if world == 1 and not a.no_cpu_baseline:
             out['cpu_baseline'] = cpu_baseline(cfg, cfar, clus, W, ang, k, targets, nframes=a.cpu_frames, name=a.config)
         else:
             out['cpu_baseline'] = None
     for p in ring:
         plan.device_free(p)
+    for h in hring:
+        plan.host_free(h)
     plan.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -203,11 +203,31 @@ int32_t rsp_synthesize_device(rsp_plan* plan, const rsp_target_in* targets, int3
  * on the host.  rsp_drain waits for everything queued.  Results are kept in
  * enqueue order until rsp_results_clear. */
 int32_t rsp_enqueue_device(rsp_plan* plan, const void* d_cube, int32_t frame_idx);
+/* End-to-end form of rsp_enqueue_device: a host PNC cube in the plan's precision (no conversion;
+ * rsp_process_cube converts).  Only the fast-time samples the chain reads (rsp_sizes.used_samples)
+ * are copied, asynchronously on the plan's upload stream into a plan-owned device ring, so
+ * uploads overlap the kernels of earlier batches; with pinned memory (rsp_host_alloc) the copy
+ * runs at full PCIe rate.  The host cube must stay unchanged until rsp_drain returns. */
+int32_t rsp_enqueue_host(rsp_plan* plan, const void* h_cube, int32_t dtype, int32_t frame_idx);
+int32_t rsp_host_alloc(rsp_plan* plan, int64_t bytes, void** h_ptr);   /* pinned host memory */
+int32_t rsp_host_free(rsp_plan* plan, void* h_ptr);
 int32_t rsp_drain(rsp_plan* plan);
 int32_t rsp_results_count(const rsp_plan* plan, int32_t* n_frames, int64_t* n_targets);
 int32_t rsp_results_get(const rsp_plan* plan, int32_t i, int32_t* frame_idx, rsp_target* targets,
                         int32_t cap, int32_t* n_targets, int32_t* n_dets);
 int32_t rsp_results_clear(rsp_plan* plan);
+
+/* ---- multi-GPU frame batch in one process (BASELINE config #3 for a MEX / loadlibrary host) ----
+ * The reference's drivers loop over independent frames (main_simulate_echoes_with_array_v8.m:
+ * 164-190, fsf:13 per frame).  Frames j = 0 .. n_frames-1 (targets[j], n_targets[j] targets,
+ * frame_idx[j]) are split into contiguous shares over the plans -- plan i, typically one per
+ * device, takes [i n / n_plans, (i+1) n / n_plans) -- each driven by its own host thread: S4/S4.1
+ * synthesis into the plan's device ring, then the throughput queue.  The final targets of frame j
+ * are gathered into out[j * cap ...], n_out[j] entries (the detection-list gather, in process
+ * memory).  The plans must have no queued frames or uncleared results.  Synchronous. */
+int32_t rsp_process_targets_multi(rsp_plan* const* plans, int32_t n_plans, const rsp_target_in* const* targets,
+                                  const int32_t* n_targets, const int32_t* frame_idx, int32_t n_frames,
+                                  uint64_t seed, double p_noise, rsp_target* out, int32_t cap, int32_t* n_out);
 
 /* Stage-2 path (process_stage2_mtd.m:1): already-beamformed fast-time data
  * iq_data [P x N x B] (PNC layout with B beams) -> PC_results and MTD_results,

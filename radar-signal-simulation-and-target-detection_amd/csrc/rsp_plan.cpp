@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <deque>
 #include <string>
+#include <thread>
 #include <vector>
 
 // Error sink and host-only stages live in rsp_host.cpp (plain C++, built and sanitized
@@ -187,7 +188,17 @@ struct rsp_plan {
     // pending batch of the queue
     const void* pend_in[RSP_MAX_F];
     int pend_ids[RSP_MAX_F];
+    int pend_slot[RSP_MAX_F];   // producer-ring slot of each pending frame, -1 = caller's device cube
     int npend = 0;
+    // producer ring of the queue (rsp_enqueue_host, rsp_process_targets_multi): device cubes
+    // written on up_stream.  slot_ready[s] orders K1 after the write; slot_free[s], recorded after
+    // the K1 that read slot s, orders the next write after it.  (nlanes + 1) x F slots: a slot
+    // comes round again only after its frame's batch has been launched.
+    hipStream_t up_stream = nullptr;
+    std::vector<void*> ring;
+    std::vector<hipEvent_t> slot_ready, slot_free;
+    std::vector<char> slot_used;
+    int ring_next = 0;
     std::deque<FrameResult> results;
     bool overflow_seen = false;
 
@@ -255,6 +266,10 @@ rsp_plan::~rsp_plan() {
             if (e) (void)hipEventDestroy(e);
         if (L.stream) (void)hipStreamDestroy(L.stream);
     }
+    if (up_stream) (void)hipStreamSynchronize(up_stream);
+    for (auto e : slot_ready) if (e) (void)hipEventDestroy(e);
+    for (auto e : slot_free) if (e) (void)hipEventDestroy(e);
+    if (up_stream) (void)hipStreamDestroy(up_stream);
     if (h_stage) (void)hipHostFree(h_stage);
     for (void* p : dev_allocs) (void)hipFree(p);
 }
@@ -357,12 +372,19 @@ FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const void* const* in, int
 
 // Enqueue K1 -> K2 -> K3 for nf frames on lane L, plus the async detection read-back.
 // smap (optional, one frame): K3 also writes rdm_for_cfar_all there.
-int launch_batch(rsp_plan* p, Lane& L, const void* const* in, const int* ids, int nf, void* smap = nullptr) {
+int launch_batch(rsp_plan* p, Lane& L, const void* const* in, const int* ids, int nf, void* smap = nullptr,
+                 const int* slots = nullptr) {
     FramePtrs fp = lane_ptrs(p, L, in, nf);
     fp.smap[0] = smap;
+    if (slots)   // producer-ring frames: K1 after their upload / synthesis
+        for (int f = 0; f < nf; ++f)
+            if (slots[f] >= 0) HIPCHK(hipStreamWaitEvent(L.stream, p->slot_ready[slots[f]], 0));
     L.timed = p->time_stages;
     if (L.timed) HIPCHK(hipEventRecord(L.tev[0], L.stream));
     HIPCHK(launch_k1(p->g, p->k, fp, nf, 3, L.stream));
+    if (slots)   // K1 has read the cubes: their slots may be written again
+        for (int f = 0; f < nf; ++f)
+            if (slots[f] >= 0) HIPCHK(hipEventRecord(p->slot_free[slots[f]], L.stream));
     if (L.timed) HIPCHK(hipEventRecord(L.tev[1], L.stream));
     HIPCHK(launch_k2(p->g, p->k, fp, nf, p->g.B * p->g.P, L.stream));
     if (L.timed) HIPCHK(hipEventRecord(L.tev[2], L.stream));
@@ -422,7 +444,7 @@ int flush_pending(rsp_plan* p) {
     Lane& L = p->lanes[p->next_lane];
     int rc = harvest(p, L);
     if (rc) return rc;
-    rc = launch_batch(p, L, p->pend_in, p->pend_ids, p->npend);
+    rc = launch_batch(p, L, p->pend_in, p->pend_ids, p->npend, nullptr, p->pend_slot);
     p->npend = 0;
     p->next_lane = (p->next_lane + 1) % p->nlanes;
     return rc;
@@ -436,6 +458,42 @@ int drain_all(rsp_plan* p) {
         rc = harvest(p, p->lanes[(p->next_lane + q) % p->nlanes]);
         if (rc) return rc;
     }
+    return RSP_OK;
+}
+
+// Next slot of the producer ring (allocated on first use); up_stream waits until the K1 that
+// last read it has run.
+int ring_acquire(rsp_plan* p, int* slot) {
+    if (p->ring.empty()) {
+        const int n = (p->nlanes + 1) * p->F;
+        HIPCHK(hipStreamCreateWithFlags(&p->up_stream, hipStreamNonBlocking));
+        p->ring.assign(n, nullptr);
+        p->slot_ready.assign(n, nullptr);
+        p->slot_free.assign(n, nullptr);
+        p->slot_used.assign(n, 0);
+        for (int i = 0; i < n; ++i) {
+            int rc = p->dalloc_bytes(&p->ring[i], (size_t)p->g.C * p->g.cpitch * p->esz);
+            if (rc) return rc;
+            HIPCHK(hipEventCreateWithFlags(&p->slot_ready[i], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&p->slot_free[i], hipEventDisableTiming));
+        }
+    }
+    const int s = p->ring_next;
+    p->ring_next = (s + 1) % (int)p->ring.size();
+    if (p->slot_used[s]) HIPCHK(hipStreamWaitEvent(p->up_stream, p->slot_free[s], 0));
+    *slot = s;
+    return RSP_OK;
+}
+
+int enqueue_frame(rsp_plan* p, const void* d_cube, int slot, int frame_idx) {
+    if (slot >= 0) {
+        HIPCHK(hipEventRecord(p->slot_ready[slot], p->up_stream));
+        p->slot_used[slot] = 1;
+    }
+    p->pend_in[p->npend] = d_cube;
+    p->pend_ids[p->npend] = frame_idx;
+    p->pend_slot[p->npend] = slot;
+    if (++p->npend == p->F) return flush_pending(p);
     return RSP_OK;
 }
 
@@ -891,9 +949,96 @@ int32_t rsp_process_targets(rsp_plan* p, const rsp_target_in* t, int32_t nt, int
 int32_t rsp_enqueue_device(rsp_plan* p, const void* d_cube, int32_t frame_idx) {
     if (!p || !d_cube) return fail(RSP_ERR_INVALID, "null argument");
     HIPCHK(hipSetDevice(p->device));   // a host thread may drive plans on several devices
-    p->pend_in[p->npend] = d_cube;
-    p->pend_ids[p->npend] = frame_idx;
-    if (++p->npend == p->F) return flush_pending(p);
+    return enqueue_frame(p, d_cube, -1, frame_idx);
+}
+
+int32_t rsp_enqueue_host(rsp_plan* p, const void* h_cube, int32_t dtype, int32_t frame_idx) {
+    if (!p || !h_cube) return fail(RSP_ERR_INVALID, "null argument");
+    if (dtype != (p->g.prec == RSP_PREC_F64 ? RSP_C128 : RSP_C64))
+        return fail(RSP_ERR_INVALID, "rsp_enqueue_host: dtype %d differs from the plan precision (rsp_process_cube converts)",
+                    dtype);
+    HIPCHK(hipSetDevice(p->device));
+    int s, rc;
+    if ((rc = ring_acquire(p, &s))) return rc;
+    // only the fast-time samples the chain reads (Geometry::ivl_*): per interval, the channel
+    // slabs' [lo, lo + len) x P block, pitch N P
+    const Geometry& g = p->g;
+    const size_t row = (size_t)g.P * p->esz;
+    for (int q = 0; q < g.nivl; ++q) {
+        const int len = (q + 1 < g.nivl ? g.ivl_start[q + 1] : g.nU) - g.ivl_start[q];
+        const size_t off = (size_t)g.ivl_lo[q] * row;
+        HIPCHK(hipMemcpy2DAsync((char*)p->ring[s] + off, (size_t)g.cpitch * p->esz, (const char*)h_cube + off,
+                                (size_t)g.N * row, (size_t)len * row, g.C, hipMemcpyHostToDevice, p->up_stream));
+    }
+    return enqueue_frame(p, p->ring[s], s, frame_idx);
+}
+
+int32_t rsp_host_alloc(rsp_plan* p, int64_t bytes, void** h_ptr) {
+    if (!p || !h_ptr || bytes <= 0) return fail(RSP_ERR_INVALID, "bad argument");
+    HIPCHK(hipSetDevice(p->device));
+    *h_ptr = nullptr;
+    if (hipHostMalloc(h_ptr, (size_t)bytes, hipHostMallocDefault) != hipSuccess)
+        return fail(RSP_ERR_NOMEM, "hipHostMalloc(%lld bytes) failed", (long long)bytes);
+    return RSP_OK;
+}
+
+int32_t rsp_host_free(rsp_plan* p, void* h_ptr) {
+    if (!p) return fail(RSP_ERR_INVALID, "null argument");
+    if (h_ptr) HIPCHK(hipHostFree(h_ptr));
+    return RSP_OK;
+}
+
+int32_t rsp_process_targets_multi(rsp_plan* const* plans, int32_t n_plans, const rsp_target_in* const* targets,
+                                  const int32_t* n_targets, const int32_t* frame_idx, int32_t n_frames, uint64_t seed,
+                                  double p_noise, rsp_target* out, int32_t cap, int32_t* n_out) {
+    if (!plans || n_plans < 1 || !targets || !n_targets || !frame_idx || n_frames < 0 || !out || cap < 0 || !n_out)
+        return fail(RSP_ERR_INVALID, "bad argument");
+    for (int i = 0; i < n_plans; ++i) {
+        if (!plans[i]) return fail(RSP_ERR_INVALID, "plan %d is null", i);
+        for (int j = 0; j < i; ++j)
+            if (plans[j] == plans[i]) return fail(RSP_ERR_INVALID, "plan %d listed twice (one host thread per plan)", i);
+        if (!plans[i]->results.empty() || plans[i]->npend)
+            return fail(RSP_ERR_INVALID, "plan %d has queued frames or uncleared results", i);
+    }
+    struct Work { int rc = RSP_OK; std::string err; };
+    std::vector<Work> work(n_plans);
+    auto run = [&](int i) {
+        rsp_plan* p = plans[i];
+        const int f0 = (int)((int64_t)n_frames * i / n_plans), f1 = (int)((int64_t)n_frames * (i + 1) / n_plans);
+        auto body = [&]() -> int {
+            HIPCHK(hipSetDevice(p->device));
+            int rc;
+            for (int j = f0; j < f1; ++j) {
+                int s;
+                if ((rc = ring_acquire(p, &s))) return rc;
+                if ((rc = synth_into(p, targets[j], n_targets[j], frame_idx[j], seed, p_noise, p->ring[s], p->up_stream)))
+                    return rc;
+                if ((rc = enqueue_frame(p, p->ring[s], s, frame_idx[j]))) return rc;
+            }
+            if ((rc = drain_all(p))) return rc;
+            if (p->overflow_seen) {
+                p->overflow_seen = false;
+                return fail(RSP_ERR_OVERFLOW, "a frame exceeded the detection capacity %d", p->g.max_dets);
+            }
+            for (int j = f0; j < f1; ++j) {   // results come back in enqueue order
+                const FrameResult& r = p->results[j - f0];
+                n_out[j] = (int32_t)r.targets.size();
+                memcpy(out + (size_t)j * cap, r.targets.data(), sizeof(rsp_target) * std::min<size_t>(cap, r.targets.size()));
+                if ((int)r.targets.size() > cap) return fail(RSP_ERR_OVERFLOW, "frame %d: %d targets > cap %d", frame_idx[j],
+                                                             (int)r.targets.size(), cap);
+            }
+            p->results.clear();
+            return RSP_OK;
+        };
+        work[i].rc = body();
+        if (work[i].rc) work[i].err = rsp_last_error();
+    };
+    std::vector<std::thread> th;
+    for (int i = 1; i < n_plans; ++i) th.emplace_back(run, i);
+    run(0);
+    for (auto& t : th) t.join();
+    for (int i = 0; i < n_plans; ++i)
+        if (work[i].rc) return fail(work[i].rc, "plan %d (device %d): %s", i, plans[i]->device, work[i].err.c_str());
     return RSP_OK;
 }
 

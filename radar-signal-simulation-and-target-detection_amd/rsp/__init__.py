@@ -21,7 +21,7 @@ import numpy as np
 from .config import (named_config, make_config, default_cfar_params, default_cluster_params,
                      v8_2_targets, evolve_targets, V8_FIR)
 from .precompute import precompute
-from .plan import Plan
+from .plan import Plan, process_targets_multi
 from ._abi import RspError
 from .matio import load_frame, save_frame
 from .music import MusicPlan, MUSIC_1D

@@ -213,6 +213,34 @@ class Plan:
     def enqueue(self, ptr, frame_idx):
         check(lib().rsp_enqueue_device(self.h, ct.c_void_p(ptr), int(frame_idx)))
 
+    def host_alloc(self, nbytes):
+        """Pinned host memory (rsp_host_alloc); returns the address."""
+        p = ct.c_void_p()
+        check(lib().rsp_host_alloc(self.h, int(nbytes), ct.byref(p)))
+        return p.value
+
+    def host_free(self, ptr):
+        check(lib().rsp_host_free(self.h, ct.c_void_p(ptr)))
+
+    def host_cube(self, ptr):
+        """A numpy [P, N, C] view (column-major, plan precision) of host memory at ``ptr``."""
+        P, N, C = self.P, self.N, self.sizes.C
+        buf = (ct.c_char * (P * N * C * np.dtype(self.cdtype).itemsize)).from_address(ptr)
+        return np.ndarray((P, N, C), self.cdtype, buffer=buf, order='F')
+
+    def enqueue_host(self, ptr_or_cube, frame_idx):
+        """rsp_enqueue_host: a host cube (address, or a Fortran-ordered array in the plan's
+        precision) that must stay unchanged until drain()."""
+        if isinstance(ptr_or_cube, np.ndarray):
+            a = ptr_or_cube
+            if a.dtype != np.dtype(self.cdtype) or not a.flags.f_contiguous:
+                raise ValueError('enqueue_host needs a Fortran-ordered %s cube' % np.dtype(self.cdtype))
+            ptr = a.ctypes.data
+        else:
+            ptr = ptr_or_cube
+        dt = _abi.RSP_C128 if np.dtype(self.cdtype) == np.complex128 else _abi.RSP_C64
+        check(lib().rsp_enqueue_host(self.h, ct.c_void_p(ptr), dt, int(frame_idx)))
+
     def drain(self):
         check(lib().rsp_drain(self.h))
 
@@ -258,3 +286,19 @@ class Plan:
         check(lib().rsp_profile_stages(self.h, arr, len(d_cubes), int(iters), ms, by, n, ct.byref(nf)))
         return [{'stage': lib().rsp_stage_name(i).decode(), 'ms': ms[i], 'bytes': by[i], 'frames': nf.value}
                 for i in range(n)]
+
+
+def process_targets_multi(plans, frames, seed=20250101, p_noise=1.0, cap=1024):
+    """rsp_process_targets_multi: frames = [(targets, frame_idx), ...] split over ``plans`` (one
+    host thread each, typically one plan per device); returns the final targets of every frame,
+    in order."""
+    n = len(frames)
+    tins = [Plan._targets_in(t) for t, _ in frames]
+    tptr = (ct.POINTER(_abi.TargetIn) * max(n, 1))(*[ct.cast(t, ct.POINTER(_abi.TargetIn)) for t in tins])
+    nt = (ct.c_int32 * max(n, 1))(*[len(t) for t, _ in frames])
+    fi = (ct.c_int32 * max(n, 1))(*[int(f) for _, f in frames])
+    out = (_abi.Target * (max(n, 1) * cap))()
+    nout = (ct.c_int32 * max(n, 1))()
+    ph = (ct.c_void_p * len(plans))(*[p.h for p in plans])
+    check(lib().rsp_process_targets_multi(ph, len(plans), tptr, nt, fi, n, int(seed), float(p_noise), out, cap, nout))
+    return [[_tgt_dict(out[j * cap + i]) for i in range(nout[j])] for j in range(n)]
