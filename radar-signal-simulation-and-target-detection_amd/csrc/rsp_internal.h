@@ -21,6 +21,10 @@
 #ifndef RSP_K2_MIX
 #define RSP_K2_MIX 1
 #endif
+// pulse-compression workgroups dispatched with the jobs interleaved (1) or job after job (0)
+#ifndef RSP_K2_ORDER
+#define RSP_K2_ORDER 1
+#endif
 #ifndef RSP_K2_SH64
 #define RSP_K2_SH64 5
 #endif
@@ -90,6 +94,7 @@ struct Geometry {
     int pow2P, logP;
     int nseg, njobs, nwg_k2;
     int cfar_RT, cfar_hR, cfar_W;
+    int cfar_VB, cfar_nband, cfar_rows;   // K3 Doppler bands: cells under test per band, bands, tile rows
     int refR, guardR, refV, guardV;
     double T;        // T_CFAR
     int max_dets;
@@ -132,6 +137,7 @@ struct DevConsts {
     const void* taps;        // narrow FIR taps, real
     const void* H;           // overlap-save spectra, 1/M scaled, complex
     const void* twM;         // per-pass Stockham twiddles of each overlap-save block size, complex
+    const int* k2order;      // pulse-compression workgroup dispatch order (RSP_K2_ORDER): job kinds interleaved
     const double* range_axis;
     const double* velocity_axis;
     const double* beam_angles;

@@ -1092,7 +1092,7 @@ __global__ __launch_bounds__(K2_THREADS, 512 / K2_THREADS) void k2_pc(Geometry g
     typedef cx<T> V;
     V* L = reinterpret_cast<V*>(rsp_lds);   // overlap-save rows | narrow: staged rows + taps
     const int f = blockIdx.y;
-    const int wg = blockIdx.x;
+    const int wg = RSP_K2_ORDER ? k.k2order[blockIdx.x] : blockIdx.x;
     int ji = 0;
     while (ji + 1 < g.njobs && wg >= g.jobs[ji + 1].wg_begin) ++ji;
     const K2Job job = g.jobs[ji];
@@ -1334,15 +1334,22 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
         wg = (xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q) + (wg >> 3);
     }
     const int pair = wg % npair, col = wg / npair;
-    const int tile = col % ntile, f = col / ntile;
+    const int tile = col % ntile, col2 = col / ntile;
+    const int band = col2 % g.cfar_nband, f = col2 / g.cfar_nband;
     const int P = g.P, G = g.G, W = FAST ? WC : g.cfar_W, hR = FAST ? HRC : g.cfar_hR, RT = FAST ? RTC : g.cfar_RT;
     const int rR = RR ? RR : g.refR, gR = GR ? GR : g.guardR, rV = RV ? RV : g.refV, gV = GV ? GV : g.guardV;
     const int rc0 = rR + gR;                           // first cell under test (0-based)
     const int tstart = (rc0 & ~3) + tile * RT;         // multiple of 4
     const int c0 = tstart - hR;                        // tile column 0 (multiple of 4; may be < 0)
     const int cut_lo = max(tstart, rc0), cut_hi = min(tstart + RT, G - rc0);
-    int* queue = reinterpret_cast<int*>(S + P * W);
+    // Doppler band: cells under test in rows [v0, v1), the tile holds rows [vt0, vt1) (the
+    // band plus the rV + gV window rows on each side; bands of one tile column tile the map)
+    const int hV = rV + gV;
+    const int v0 = hV + band * g.cfar_VB, v1 = min(hV + (band + 1) * g.cfar_VB, P - hV);
+    const int vt0 = max(v0 - hV, 0), vt1 = min(v1 + hV, P), nv = vt1 - vt0;
+    int* queue = reinterpret_cast<int*>(S + g.cfar_rows * W);
     int* qn = queue + K3_QCAP;
+    const T* Sv = S - vt0 * W;                         // row v of the map at Sv + v W
     const int Gp = g.Gp;
     const T* __restrict__ MA = static_cast<const T*>(fp.mag[f]) + (size_t)pair * P * Gp;   // |RDM| of beams pair, pair+1
     const T* __restrict__ MB = MA + (size_t)P * Gp;
@@ -1355,16 +1362,16 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
         const int u = threadIdx.x % WU, rr = threadIdx.x / WU;
         const int r = c0 + EPU * u;
         const bool colok = rr < NTR && r >= 0 && r < G;   // rows are padded to Gp: r + EPU - 1 < Gp
-        const T* pa = MA + (size_t)rr * Gp + r;
-        const T* pb = MB + (size_t)rr * Gp + r;
+        const T* pa = MA + (size_t)(vt0 + rr) * Gp + r;
+        const T* pb = MB + (size_t)(vt0 + rr) * Gp + r;
         U* sd = reinterpret_cast<U*>(S + rr * WC) + u;
-        for (int vb = 0; vb < P; vb += K3_VEC * NTR) {
+        for (int vb = 0; vb < nv; vb += K3_VEC * NTR) {
             U xa[K3_VEC], xb[K3_VEC];
 #pragma unroll
             for (int q = 0; q < K3_VEC; ++q) {
                 xa[q] = U{};
                 xb[q] = xa[q];
-                if (colok && vb + rr + q * NTR < P) {
+                if (colok && vb + rr + q * NTR < nv) {
                     xa[q] = *reinterpret_cast<const U*>(pa + (size_t)(vb + q * NTR) * Gp);
                     xb[q] = *reinterpret_cast<const U*>(pb + (size_t)(vb + q * NTR) * Gp);
 #pragma unroll
@@ -1374,10 +1381,10 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
             }
 #pragma unroll
             for (int q = 0; q < K3_VEC; ++q)
-                if (rr < NTR && vb + rr + q * NTR < P) sd[(vb + q * NTR) * WU] = xa[q] + xb[q];
+                if (rr < NTR && vb + rr + q * NTR < nv) sd[(vb + q * NTR) * WU] = xa[q] + xb[q];
         }
     } else {
-        const int WU = W / EPU, nu = P * WU;
+        const int WU = W / EPU, nu = nv * WU;
         for (int e0 = 0; e0 < nu; e0 += K3_VEC * RSP_THREADS) {
             U xa[K3_VEC], xb[K3_VEC];
 #pragma unroll
@@ -1386,7 +1393,7 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
                 xa[u] = U{};
                 xb[u] = xa[u];
                 if (e < nu) {
-                    const int v = e / WU, r = c0 + EPU * (e - v * WU);
+                    const int vl = e / WU, r = c0 + EPU * (e - vl * WU), v = vt0 + vl;
                     if (r >= 0 && r < G) {   // rows are padded to Gp (multiple of 4): r + EPU - 1 < Gp
                         xa[u] = *reinterpret_cast<const U*>(MA + (size_t)v * Gp + r);
                         xb[u] = *reinterpret_cast<const U*>(MB + (size_t)v * Gp + r);
@@ -1407,13 +1414,13 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
     if (fp.smap[f]) {   // on request: rdm_for_cfar_all as thresholded here, [pair][v][r]
         T* sm = static_cast<T*>(fp.smap[f]) + (size_t)pair * P * G;
         const int wlo = tile == 0 ? 0 : tstart, whi = tile == ntile - 1 ? G : min(tstart + RT, G);
+        const int vlo = band == 0 ? 0 : v0, vhi = band == g.cfar_nband - 1 ? P : v1;   // inside [vt0, vt1)
         const int nwc = whi - wlo;
-        for (int e = threadIdx.x; e < P * nwc; e += RSP_THREADS) {
-            const int v = e / nwc, r = wlo + (e - v * nwc);
-            sm[(size_t)v * G + r] = S[v * W + (r - c0)];
+        for (int e = threadIdx.x; e < (vhi - vlo) * nwc; e += RSP_THREADS) {
+            const int v = vlo + e / nwc, r = wlo + (e - (v - vlo) * nwc);
+            sm[(size_t)v * G + r] = Sv[v * W + (r - c0)];
         }
     }
-    const int v0 = rV + gV, v1 = P - rV - gV;
     if (v1 <= v0 || cut_hi <= cut_lo) return;
     const double Tc = g.T;
     // mean() = sum / n over the slices of fsf:197-203 (max(a/n, b/n) = max(a, b)/n).  double: the
@@ -1465,7 +1472,7 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
         const int rgp = lgT == 4 ? (rg & ~3) | ((rg & 1) << 1) | ((rg >> 1) & 1) : rg;
 #pragma unroll 1
         for (int v = v0 + rgp; v < v1; v += RSP_THREADS >> lgT) {
-            const T* row = S + v * WC + c;
+            const T* row = Sv + v * WC + c;
             T xl[4 * NL], xr[4 * NR], cv[4];
             T lv[4] = {0, 0, 0, 0}, tv[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -1513,12 +1520,12 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
             if (r >= cut_hi) continue;
             const int c = r - c0;
             for (int v = v0 + wv; v < v1; v += 4) {
-                const T* rowp = S + v * W;
+                const T* rowp = Sv + v * W;
                 T lr = 0, tr = 0, lv = 0, tv = 0;
                 const T* lrp = rowp + c - gR - rR;
                 const T* trp = rowp + c + gR + 1;
-                const T* lvp = S + (v - gV - rV) * W + c;
-                const T* tvp = S + (v + gV + 1) * W + c;
+                const T* lvp = Sv + (v - gV - rV) * W + c;
+                const T* tvp = Sv + (v + gV + 1) * W + c;
                 for (int qq = 0; qq < rR; ++qq) {
                     lr += lrp[qq];
                     tr += trp[qq];
@@ -1546,7 +1553,7 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
         if (idx >= g.max_dets) break;
         const int e = queue[i];
         const int v = e >> 16, c = e & 0xFFFF;
-        s9_estimate<T>(k, S, W, c0, P, G, Gp, v, c0 + c, pair, MA, MB, &fp.dets[f][idx]);
+        s9_estimate<T>(k, Sv, W, c0, P, G, Gp, v, c0 + c, pair, MA, MB, &fp.dets[f][idx]);
     }
 }
 
@@ -1741,8 +1748,8 @@ hipError_t launch_k2(const Geometry& g, const DevConsts& k, const FramePtrs& fp,
 
 template <class T>
 static hipError_t launch_k3_p(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, hipStream_t s) {
-    const size_t lds = (size_t)g.P * g.cfar_W * sizeof(T) + (K3_QCAP + 4) * sizeof(int);
-    const dim3 grid(k3_ntiles(g) * (g.B - 1) * nf);   // 1-D; k3_cfar remaps it XCD-aware
+    const size_t lds = (size_t)g.cfar_rows * g.cfar_W * sizeof(T) + (K3_QCAP + 4) * sizeof(int);
+    const dim3 grid(k3_ntiles(g) * g.cfar_nband * (g.B - 1) * nf);   // 1-D; k3_cfar remaps it XCD-aware
     hipError_t e;
     const bool ref = g.refR == 5 && g.refV == 5 && g.guardR == 10 && g.guardV == 10;   // the reference's cfar_params (v8:45-46)
     if (ref && g.cfar_RT == 64) {

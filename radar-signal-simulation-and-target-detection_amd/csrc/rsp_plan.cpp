@@ -799,10 +799,19 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
     g.nwg_k2 = wg;
     // K3 tile: <= 64 KB of S per tile (>= 2 workgroups per CU); the fast path covers RT 32/64
     g.cfar_hR = (std::max(g.refR + g.guardR, 2) + 3) & ~3;   // halo, multiple of 4 (16-B tile loads)
-    g.cfar_RT = 64;
-    while (g.cfar_RT > 8 && (size_t)P * (g.cfar_RT + 2 * g.cfar_hR) * p->rsz > 64 * 1024) g.cfar_RT >>= 1;
+    // tiles of RT range cells (64 complex single / 32 complex double: the fast path) x a band of
+    // Doppler rows, <= 64 KB of S per tile: at P = 128 one band holds every row; longer P (x4's 256)
+    // splits the rows into bands, each with the rV + gV window rows on either side
+    g.cfar_RT = p->rsz == 4 ? 64 : 32;
     g.cfar_W = (g.cfar_RT + 2 * g.cfar_hR + 3) & ~3;   // LDS row stride, 16-B aligned
-    if ((size_t)P * g.cfar_W * p->rsz > 150 * 1024) return bail(fail(RSP_ERR_UNSUPPORTED, "CFAR tile exceeds LDS"));
+    {
+        const int hV = g.refV + g.guardV, ncut = std::max(P - 2 * hV, 1);
+        const int rows_max = (int)((64 * 1024) / ((size_t)g.cfar_W * p->rsz));
+        if (rows_max - 2 * hV < 1) return bail(fail(RSP_ERR_UNSUPPORTED, "CFAR window %d x %d exceeds the LDS tile", hV, g.cfar_hR));
+        g.cfar_nband = (ncut + rows_max - 2 * hV - 1) / (rows_max - 2 * hV);
+        g.cfar_VB = (ncut + g.cfar_nband - 1) / g.cfar_nband;
+        g.cfar_rows = std::min(P, g.cfar_VB + 2 * hV);
+    }
 
     // ---- constants to the device, in the plan's precision
     int rc;
@@ -847,6 +856,20 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
         (rc = p->upload(&dang, ang)) || (rc = p->upload(&dkl, kl)))
         return bail(rc);
     k.range_axis = dra; k.velocity_axis = dva; k.beam_angles = dang; k.klut = dkl;
+    {   // K2 dispatch order: workgroup i of job j at key (i + 1/2) / nwg_j, so that the narrow FIR,
+        // medium and long jobs are interleaved in proportion through the launch
+        std::vector<std::pair<double, int>> key;
+        for (const K2Job& jb : p->jobs)
+            for (int i = 0; i < jb.wg_count; ++i) key.push_back({(i + 0.5) / jb.wg_count, jb.wg_begin + i});
+        std::stable_sort(key.begin(), key.end(), [](const std::pair<double, int>& a, const std::pair<double, int>& b) {
+            return a.first < b.first;
+        });
+        std::vector<int> order(key.size());
+        for (size_t i = 0; i < key.size(); ++i) order[i] = key[i].second;
+        int* dord;
+        if ((rc = p->upload(&dord, order))) return bail(rc);
+        k.k2order = dord;
+    }
     k.deltaR = pre->deltaR; k.deltaV = pre->deltaV;
     if (pre->tx_pulse) {
         std::vector<double> tx(pre->tx_pulse, pre->tx_pulse + 2 * (size_t)N);
