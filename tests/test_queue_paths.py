@@ -23,7 +23,7 @@ def _same(a, b):
 
 @pytest.mark.parametrize('prec', ['c128', 'c64'])
 def test_enqueue_host_equals_device_queue(prec):
-    """x2 frames (two used-sample intervals) uploaded from pinned host cubes through the plan's
+    """x2 frames (several used-sample intervals) uploaded from pinned host cubes through the plan's
     ring, which wraps (F = 2: 8 slots for 20 frames), give the device queue's results."""
     s = scenario('x2')
     tg = targets_for('x2')
