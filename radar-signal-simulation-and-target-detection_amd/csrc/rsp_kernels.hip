@@ -106,6 +106,16 @@ __device__ __forceinline__ void buf_st1(__amdgpu_buffer_rsrc_t r, unsigned off, 
 }
 
 // ---- radix-R DFT kernels in registers -------------------------------------------------
+// Radix-2 butterfly with a twiddle, (a, b) <- (a + w b, a - w b): four FMAs for a + w b and one
+// per component for a - w b = 2a - (a + w b) -- 6 operations instead of a complex multiply (4)
+// plus an add and a subtract (4).
+template <class V>
+__device__ __forceinline__ void bfly_tw(V& a, V& b, V w) {
+    typedef scal<V> S;
+    const V t = a + w.xx * b + w.yy * V{-b.y, b.x};
+    b = a * (S)2 - t;
+    a = t;
+}
 template <int R, bool INV, class V> struct Dft;
 template <bool INV, class V> struct Dft<2, INV, V> {
     static __device__ __forceinline__ void run(V* a) {
@@ -131,14 +141,17 @@ template <bool INV, class V> struct Dft<8, INV, V> {
         Dft<4, INV, V>::run(e);
         Dft<4, INV, V>::run(o);
         constexpr double r = 0.70710678118654752440;
-        o[1] = vmul(o[1], vtw<INV, V>(r, r));
         o[2] = vrot<INV>(o[2]);
-        o[3] = vmul(o[3], vtw<INV, V>(-r, r));
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            a[k] = e[k] + o[k];
-            a[k + 4] = e[k] - o[k];
-        }
+        bfly_tw(e[1], o[1], vtw<INV, V>(r, r));
+        bfly_tw(e[3], o[3], vtw<INV, V>(-r, r));
+        a[0] = e[0] + o[0];
+        a[4] = e[0] - o[0];
+        a[2] = e[2] + o[2];
+        a[6] = e[2] - o[2];
+        a[1] = e[1];
+        a[5] = o[1];
+        a[3] = e[3];
+        a[7] = o[3];
     }
 };
 template <bool INV, class V> struct Dft<16, INV, V> {
@@ -152,17 +165,22 @@ template <bool INV, class V> struct Dft<16, INV, V> {
         Dft<8, INV, V>::run(e);
         Dft<8, INV, V>::run(o);
         constexpr double c1 = 0.92387953251128675613, s1 = 0.38268343236508977173, r = 0.70710678118654752440;
-        o[1] = vmul(o[1], vtw<INV, V>(c1, s1));
-        o[2] = vmul(o[2], vtw<INV, V>(r, r));
-        o[3] = vmul(o[3], vtw<INV, V>(s1, c1));
         o[4] = vrot<INV>(o[4]);
-        o[5] = vmul(o[5], vtw<INV, V>(-s1, c1));
-        o[6] = vmul(o[6], vtw<INV, V>(-r, r));
-        o[7] = vmul(o[7], vtw<INV, V>(-c1, s1));
+        bfly_tw(e[1], o[1], vtw<INV, V>(c1, s1));
+        bfly_tw(e[2], o[2], vtw<INV, V>(r, r));
+        bfly_tw(e[3], o[3], vtw<INV, V>(s1, c1));
+        bfly_tw(e[5], o[5], vtw<INV, V>(-s1, c1));
+        bfly_tw(e[6], o[6], vtw<INV, V>(-r, r));
+        bfly_tw(e[7], o[7], vtw<INV, V>(-c1, s1));
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            a[k] = e[k] + o[k];
-            a[k + 8] = e[k] - o[k];
+            if (k == 0 || k == 4) {
+                a[k] = e[k] + o[k];
+                a[k + 8] = e[k] - o[k];
+            } else {
+                a[k] = e[k];
+                a[k + 8] = o[k];
+            }
         }
     }
 };
