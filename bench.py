@@ -191,12 +191,18 @@ def main_music(a):
         flops = 8.0 * N * (N + 1) / 2 * K * I   # Hermitian X X^H: N(N+1)/2 entries x K complex MACs
         cov_tf = flops / (pr['cov_ms'] * 1e-3) / 1e12
         bytes_ = 8.0 * N * K * I
+        eig_flops = (16.0 / 3.0 * N ** 3 + 8.0 * M * N * N + 8.0 * len(scan) * M * N) * I
         stages = [{'stage': 'k_music_cov', 'ms_per_launch': pr['cov_ms'], 'instances_per_launch': I,
                    'alg_flops_per_launch': flops, 'achieved_TFLOPs': cov_tf,
                    'achieved_GBps': bytes_ / (pr['cov_ms'] * 1e-3) / 1e9},
                   {'stage': 'k_music_eig', 'ms_per_launch': pr['eig_ms'], 'instances_per_launch': I,
-                   'note': 'Householder + bisection + inverse iteration + spectrum per workgroup: '
-                           'latency-bound (neither HBM nor MFMA), see DESIGN.md'}]
+                   # algorithmic model: complex Householder tridiagonalisation 16/3 N^3, back-transform
+                   # of the M signal vectors 8 M N^2, pseudo-spectrum 8 n_scan M N real flop
+                   'alg_flops_per_launch': eig_flops,
+                   'achieved_TFLOPs': eig_flops / (pr['eig_ms'] * 1e-3) / 1e12,
+                   'frac_of_f32_vector_peak': eig_flops / (pr['eig_ms'] * 1e-3) / 1e12 / MFMA_F32_PEAK_TFLOPS,
+                   'note': 'the dominant kernel: one wave per instance, Householder + bisection + inverse '
+                           'iteration + spectrum, latency-bound (neither HBM nor MFMA), see DESIGN.md'}]
         out = {'metric': 'MUSIC_1D DOA instances/sec, 64ch x 1024 snapshots (BASELINE config #5)',
                'value': I * a.steps * world / el, 'unit': 'instances/s', 'n_gpus': world, 'steps': a.steps,
                'warmup': a.warmup, 'ms_per_step': el / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
@@ -208,6 +214,8 @@ def main_music(a):
                             'peak': MFMA_F32_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': cov_tf / MFMA_F32_PEAK_TFLOPS,
                             'traffic': music_traffic(), 'kernel_ms': pr['cov_ms'],
                             'timing': 'HIP events on the plan stream, %d launches' % a.profile_iters,
+                            'note': 'roofline of the MFMA kernel (k_music_cov); the dominant kernel is k_music_eig, '
+                                    'latency-bound: its algorithmic fraction of the f32 vector peak is in stages',
                             'stages': stages},
                'cpu_baseline': music_cpu_baseline(scene, scan, dl, N, K, M) if (world == 1 and not a.no_cpu_baseline)
                else None}

@@ -1311,6 +1311,9 @@ __device__ __forceinline__ void s9_estimate(const DevConsts& k, const T* S, int 
 }
 
 #define K3_QCAP 1024
+#ifndef RSP_K3_ABLATE
+#define RSP_K3_ABLATE 0   // timing ablations (A/B builds only): 1 = no CFAR, 2 = no map loads
+#endif
 #define K3_VEC 12   // 16-B loads per beam per thread in flight
 
 constexpr int floor4(int x) { return x >= 0 ? (x & ~3) : -((-x + 3) & ~3); }
@@ -1389,7 +1392,7 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
             for (int q = 0; q < K3_VEC; ++q) {
                 xa[q] = U{};
                 xb[q] = xa[q];
-                if (colok && vb + rr + q * NTR < nv) {
+                if (colok && vb + rr + q * NTR < nv && !(RSP_K3_ABLATE & 2)) {
                     xa[q] = *reinterpret_cast<const U*>(pa + (size_t)(vb + q * NTR) * Gp);
                     xb[q] = *reinterpret_cast<const U*>(pb + (size_t)(vb + q * NTR) * Gp);
 #pragma unroll
@@ -1439,7 +1442,7 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
             sm[(size_t)v * G + r] = Sv[v * W + (r - c0)];
         }
     }
-    if (v1 <= v0 || cut_hi <= cut_lo) return;
+    if (v1 <= v0 || cut_hi <= cut_lo || (RSP_K3_ABLATE & 1)) return;
     const double Tc = g.T;
     // mean() = sum / n over the slices of fsf:197-203 (max(a/n, b/n) = max(a, b)/n).  double: the
     // correctly rounded quotient, as MATLAB, without a division: q0 = x * RN(1/n), r = x - q0 n
