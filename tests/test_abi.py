@@ -79,6 +79,11 @@ def test_null_arguments_are_rejected():
     assert lib.rsp_process_cube(None, None, 1, 0, 0, None) == _abi.RSP_ERR_INVALID
     assert lib.rsp_stage_name(99) == b'?'
     assert lib.rsp_plan_create_ex(None, None, None, None, None, None) == _abi.RSP_ERR_INVALID
+    assert lib.rsp_enqueue_host(None, None, _abi.RSP_C128, 1) == _abi.RSP_ERR_INVALID
+    assert lib.rsp_host_alloc(None, 16, None) == _abi.RSP_ERR_INVALID
+    assert lib.rsp_host_free(None, None) == _abi.RSP_ERR_INVALID
+    assert lib.rsp_process_targets_multi(None, 0, None, None, None, 0, 0, 0.0, None, 0, None) == _abi.RSP_ERR_INVALID
+    assert b'bad argument' in lib.rsp_last_error()
 
 
 def test_plan_options_defaults_and_validation():
