@@ -1344,7 +1344,9 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
     constexpr int EPU = U16<T>::E;
     constexpr bool FAST = RR > 0 && RV > 0 && GR > 0 && GV > 0 && (RTC == 32 || RTC == 64);
     constexpr int HRC = ((RR + GR > 2 ? RR + GR : 2) + 3) & ~3;   // = g.cfar_hR (rsp_plan.cpp)
-    constexpr int WC = (RTC + 2 * HRC + 3) & ~3;                 // = g.cfar_W
+    // = g.cfar_W; complex double rows get 2 extra cells (stride 132 dwords = 4 mod 64 banks), see
+    // the row-group order of the CFAR loop
+    constexpr int WC = ((RTC + 2 * HRC + 3) & ~3) + (sizeof(T) == 8 ? 2 : 0);
     // XCD-aware order (bijective swizzle, cdna_hip_programming.md T1): the workgroups that
     // share an XCD take consecutive (tile, pair) ids with pairs fastest, so beam b's tile --
     // read by pairs b-1 and b -- and the range halos of neighbouring tiles are L2 hits
@@ -1490,7 +1492,12 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
         // ({0-3,12-15,20-27}, ... MI355X_MICROARCH.md §LDS) then pair rows 2 apart, 2W = 192
         // floats = 0 mod 64 banks, conflict-free (adjacent rows, W = 96 = 32 mod 64, were 2-way)
         const int rg = threadIdx.x >> lgT;
-        const int rgp = lgT == 4 ? (rg & ~3) | ((rg & 1) << 1) | ((rg >> 1) & 1) : rg;
+        // complex double (8 threads per row, 32 B per thread, two ds_read_b128 of 16 lanes from 4
+        // row groups): with the 132-dword row stride, row groups 4a + {0, 1, 2, 3} take rows
+        // 2a + {0, 16, 1, 17}, whose bank offsets {0, 0, 4, 4} (mod 64) put the four lane sets of
+        // every ds_read_b128 on disjoint banks (2-way conflicted with 64-cell rows)
+        const int rgp = lgT == 4 ? (rg & ~3) | ((rg & 1) << 1) | ((rg >> 1) & 1)
+                                 : 2 * (rg >> 2) + ((rg & 1) << 4) + ((rg >> 1) & 1);
 #pragma unroll 1
         for (int v = v0 + rgp; v < v1; v += RSP_THREADS >> lgT) {
             const T* row = Sv + v * WC + c;

@@ -800,13 +800,14 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
     // K3 tile: <= 64 KB of S per tile (>= 2 workgroups per CU); the fast path covers RT 32/64
     g.cfar_hR = (std::max(g.refR + g.guardR, 2) + 3) & ~3;   // halo, multiple of 4 (16-B tile loads)
     // tiles of RT range cells (64 complex single / 32 complex double: the fast path) x a band of
-    // Doppler rows, <= 64 KB of S per tile: at P = 128 one band holds every row; longer P (x4's 256)
+    // Doppler rows, <= 68 KB of S per tile (2 workgroups per CU): at P = 128 one band holds every row; longer P (x4's 256)
     // splits the rows into bands, each with the rV + gV window rows on either side
     g.cfar_RT = p->rsz == 4 ? 64 : 32;
-    g.cfar_W = (g.cfar_RT + 2 * g.cfar_hR + 3) & ~3;   // LDS row stride, 16-B aligned
+    // LDS row stride, 16-B aligned; complex double + 2 cells (bank spread, k3_cfar)
+    g.cfar_W = ((g.cfar_RT + 2 * g.cfar_hR + 3) & ~3) + (p->rsz == 8 ? 2 : 0);
     {
         const int hV = g.refV + g.guardV, ncut = std::max(P - 2 * hV, 1);
-        const int rows_max = (int)((64 * 1024) / ((size_t)g.cfar_W * p->rsz));
+        const int rows_max = (int)((68 * 1024) / ((size_t)g.cfar_W * p->rsz));
         if (rows_max - 2 * hV < 1) return bail(fail(RSP_ERR_UNSUPPORTED, "CFAR window %d x %d exceeds the LDS tile", hV, g.cfar_hR));
         g.cfar_nband = (ncut + rows_max - 2 * hV - 1) / (rows_max - 2 * hV);
         g.cfar_VB = (ncut + g.cfar_nband - 1) / g.cfar_nband;
