@@ -512,6 +512,9 @@ __device__ __forceinline__ size_t zaddr(const Geometry& g, int b, int v, int np)
 // K1: DBF + MTD window + slow-time FFT + fftshift -> compacted rows
 // ======================================================================================
 #define K1_THREADS 512
+#ifndef RSP_K1_ABLATE
+#define RSP_K1_ABLATE 0   // timing ablations (A/B builds only): 1 = no FFT, 2 = no DBF MFMA, 4 = no z stores
+#endif
 #define K1_SH 4   // LDS pad shift of the slow-time FFT rows (row stride P + P/16)
 
 // DBF (fsf:93-97) on the matrix cores as a real GEMM: D[16 rows x 16 pulses] += A[16 x 4
@@ -577,6 +580,9 @@ struct StoreZ {
     __device__ __forceinline__ void put(int, int row, int o, int, V x) const {
         const int b = row >> lgNT, nl = row & ((1 << lgNT) - 1);
         const int v = (o + half) & (P - 1);
+#if RSP_K1_ABLATE & 4   // timing ablation only: no z stores
+        if (x.x == (scal<V>)1234.5678)
+#endif
         buf_st(z, (unsigned)(((((b * ntiles + tile) * P + v) << lgNT) + nl)) * (unsigned)sizeof(V), x);
     }
 };
@@ -837,10 +843,17 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
 #pragma unroll
                 for (int a = 0; a < D::NACC; ++a) acc[mb][a] = typename D::Acc{};
             if (vld[u]) {   // samples past the used ones: zero columns, like k1_dbf_mtd's n = -1
+#if RSP_K1_ABLATE & 2   // timing ablation only: no DBF arithmetic (the loads still feed the store)
+#pragma unroll
+                for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) acc[mb][0][j & 3] += xv[u][j][0];
+#else
 #pragma unroll
                 for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
                     for (int j = 0; j < NJ; ++j) D::mma(acc[mb], are[mb][j], aim[mb][j], xv[u][j]);
+#endif
             }
             dbf_store<T, MB>(Yf, acc, grp, B, NT, Ppad, nlv[u], pv[u], wv_[u], K1_SH);
         }
@@ -857,8 +870,16 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
         if (tile == 0 && threadIdx.x == 0 && fp.count[f]) *fp.count[f] = 0;   // K3's detection counter
         V* __restrict__ z = static_cast<V*>(fp.z[f]);
         const StoreZ<V> sz{buf_rsrc(z, (unsigned)(B * g.ntiles * zslab * sizeof(V))), lgNT, g.ntiles, tile, P, half};
+#if RSP_K1_ABLATE & 1   // timing ablation only: no FFT, the tile goes to z as is
+        for (int e = threadIdx.x; e < B * NT * P; e += K1_THREADS) {
+            const int row = e >> LGP, o = e & (P - 1);
+            sz.put(0, row, o, 0, (Y + cur * bufsz)[row * Ppad + o + (o >> K1_SH)]);
+        }
+        __syncthreads();
+#else
         fft_passes<LGP, k1p_pts<T>(), K1_SH, K1_THREADS>(Y + cur * bufsz, Ppad, B * NT, twl,
                                                           StoreLds<V>{Y + cur * bufsz}, sz);   // ends with a barrier
+#endif
         if (Tn < total) dbf(Y + (cur ^ 1) * bufsz);
         __syncthreads();
         cur ^= 1;
