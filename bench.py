@@ -289,7 +289,7 @@ def main():
         plan.drain()
 
     run(max(a.warmup, 2 * NLANES), 0)   # every lane (stream) warmed with full batches
-    plan.results(clear=True)
+    plan.results_rows(clear=True)
 
     if dist is not None:
         dist.barrier()
@@ -300,15 +300,16 @@ def main():
         run_all()
     else:
         run(a.steps, 1)
-    res = plan.results(clear=True)
-    n_targets_local = sum(len(r['final_targets']) for r in res)
+    # every frame's final targets as packed rows (frame_idx, Range, Velocity, Angle, Power), one
+    # C call; the same payload the multi-GPU gather moves
+    rows = plan.results_rows(clear=True)
     if dist is not None:
         # the one collective: gather every rank's detection list (RCCL over xGMI)
-        from rsp.dist import gather_targets
-        gathered = gather_targets(res, rank, world, device=local)
-        n_targets_all = sum(len(r['final_targets']) for r in gathered)
+        from rsp.dist import gather_rows
+        counts, bufs = gather_rows(rows, rank, world, device=local)
+        n_targets_all = int(sum(np.count_nonzero(~np.isnan(b[:c, 1])) for c, b in zip(counts, bufs)))
     else:
-        n_targets_all = n_targets_local
+        n_targets_all = int(np.count_nonzero(~np.isnan(rows[:, 1])))
     plan.sync()
     if dist is not None:
         dist.barrier()

@@ -216,6 +216,10 @@ int32_t rsp_results_count(const rsp_plan* plan, int32_t* n_frames, int64_t* n_ta
 int32_t rsp_results_get(const rsp_plan* plan, int32_t i, int32_t* frame_idx, rsp_target* targets,
                         int32_t cap, int32_t* n_targets, int32_t* n_dets);
 int32_t rsp_results_clear(rsp_plan* plan);
+/* Every queued result as rows of 5 doubles (frame_idx, Range, Velocity, Angle, Power), frames in
+ * enqueue order, one NaN row for a frame without targets -- the detection-list payload of the
+ * multi-GPU gather, in one call.  *n_rows = rows needed; RSP_ERR_OVERFLOW if more than cap. */
+int32_t rsp_results_rows(const rsp_plan* plan, double* rows, int64_t cap, int64_t* n_rows);
 
 /* ---- multi-GPU frame batch in one process (BASELINE config #3 for a MEX / loadlibrary host) ----
  * The reference's drivers loop over independent frames (main_simulate_echoes_with_array_v8.m:

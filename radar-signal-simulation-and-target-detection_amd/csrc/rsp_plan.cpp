@@ -1099,6 +1099,27 @@ int32_t rsp_results_get(const rsp_plan* p, int32_t i, int32_t* frame_idx, rsp_ta
     return RSP_OK;
 }
 
+int32_t rsp_results_rows(const rsp_plan* p, double* rows, int64_t cap, int64_t* n_rows) {
+    if (!p || !n_rows || (cap > 0 && !rows)) return fail(RSP_ERR_INVALID, "bad argument");
+    int64_t n = 0;
+    for (const FrameResult& r : p->results) {
+        const size_t nt = r.targets.size();
+        for (size_t i = 0; i < std::max<size_t>(nt, 1); ++i, ++n) {
+            if (n >= cap) continue;
+            double* o = rows + 5 * n;
+            o[0] = r.frame_idx;
+            if (nt) {
+                o[1] = r.targets[i].Range; o[2] = r.targets[i].Velocity; o[3] = r.targets[i].Angle; o[4] = r.targets[i].Power;
+            } else {   // an empty frame stays visible as one NaN row
+                o[1] = o[2] = o[3] = o[4] = std::nan("");
+            }
+        }
+    }
+    *n_rows = n;
+    if (n > cap) return fail(RSP_ERR_OVERFLOW, "%lld rows > cap %lld", (long long)n, (long long)cap);
+    return RSP_OK;
+}
+
 int32_t rsp_results_clear(rsp_plan* p) {
     if (!p) return fail(RSP_ERR_INVALID, "null argument");
     p->results.clear();

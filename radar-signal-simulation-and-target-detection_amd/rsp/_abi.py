@@ -153,6 +153,7 @@ PROTOTYPES = {
     'rsp_results_get': (ct.c_int32, [_P, ct.c_int32, ct.POINTER(ct.c_int32), ct.POINTER(Target), ct.c_int32,
                                      ct.POINTER(ct.c_int32), ct.POINTER(ct.c_int32)]),
     'rsp_results_clear': (ct.c_int32, [_P]),
+    'rsp_results_rows': (ct.c_int32, [_P, _dp, ct.c_int64, ct.POINTER(ct.c_int64)]),
     'rsp_process_stage2': (ct.c_int32, [_P, _P, ct.c_int32, _dp, _dp]),
     'rsp_process_stage2_gated': (ct.c_int32, [_P, _P, ct.c_int32, ct.c_int32, ct.POINTER(ct.c_int32), _dp, _dp]),
     'rsp_profile_stages': (ct.c_int32, [_P, ct.POINTER(_P), ct.c_int32, ct.c_int32, ct.POINTER(ct.c_float),

@@ -33,11 +33,28 @@ def gather_targets(results, rank, world, device=None):
 
     Returns a list of {'frame_idx', 'final_targets'} in (rank, frame) order, identical
     on every rank."""
+    counts, bufs = gather_rows(_pack(results), rank, world, device)
+    out = []
+    for r, (c, b) in enumerate(zip(counts, bufs)):
+        frames = {}
+        for f, R, V, A, P in b[:c]:
+            lst = frames.setdefault(int(f), [])
+            if not np.isnan(R):
+                lst.append({'Range': R, 'Velocity': V, 'Angle': A, 'Power': P})
+        for f in frames:                 # insertion order = the rank's processing order
+            out.append({'rank': r, 'frame_idx': f, 'final_targets': frames[f]})
+    return out
+
+
+def gather_rows(rows, rank, world, device=None):
+    """The collective itself on packed [n, 5] rows (Plan.results_rows / _pack): all-gather of
+    the counts, then a padded all-gather of the rows.  Returns (counts, [per-rank numpy
+    arrays of padded rows]), identical on every rank."""
     import torch
     import torch.distributed as dist
     backend = dist.get_backend()
     dev = torch.device('cuda', device) if (backend == 'nccl') else torch.device('cpu')
-    local = torch.from_numpy(_pack(results)).to(dev)
+    local = torch.from_numpy(np.ascontiguousarray(rows, np.float64).reshape(-1, 5)).to(dev)
     n = torch.tensor([local.shape[0]], dtype=torch.int64, device=dev)
     counts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
     dist.all_gather(counts, n)
@@ -47,14 +64,4 @@ def gather_targets(results, rank, world, device=None):
     pad[:local.shape[0]] = local
     bufs = [torch.zeros((m, 5), dtype=torch.float64, device=dev) for _ in range(world)]
     dist.all_gather(bufs, pad)
-    out = []
-    for r, (c, b) in enumerate(zip(counts, bufs)):
-        rows = b[:c].cpu().numpy()
-        frames = {}
-        for f, R, V, A, P in rows:
-            lst = frames.setdefault(int(f), [])
-            if not np.isnan(R):
-                lst.append({'Range': R, 'Velocity': V, 'Angle': A, 'Power': P})
-        for f in frames:                 # insertion order = the rank's processing order
-            out.append({'rank': r, 'frame_idx': f, 'final_targets': frames[f]})
-    return out
+    return counts, [b.cpu().numpy() for b in bufs]

@@ -261,6 +261,17 @@ class Plan:
             check(lib().rsp_results_clear(self.h))
         return out
 
+    def results_rows(self, clear=True):
+        """The queued results as an [n, 5] float64 array (frame_idx, Range, Velocity, Angle,
+        Power; one NaN row per frame without targets) in one C call (rsp_results_rows)."""
+        n = ct.c_int64()
+        check(lib().rsp_results_rows(self.h, None, 0, ct.byref(n)))
+        rows = np.empty((max(n.value, 1), 5), np.float64)
+        check(lib().rsp_results_rows(self.h, rows.ctypes.data_as(ct.POINTER(ct.c_double)), n.value, ct.byref(n)))
+        if clear:
+            check(lib().rsp_results_clear(self.h))
+        return rows[:n.value]
+
     def set_stage_timing(self, on=True):
         """Live HIP-event timing of K1/K2/K3 of every queued batch (resets the sums)."""
         check(lib().rsp_set_stage_timing(self.h, 1 if on else 0))

@@ -82,3 +82,33 @@ def test_process_targets_multi_equals_per_frame_calls():
     finally:
         for p in plans:
             p.close()
+
+
+def test_results_rows_equal_results():
+    """rsp_results_rows packs what rsp_results_get returns: frame by frame, one NaN row for a
+    frame without targets (the payload rsp.dist.gather_rows moves)."""
+    s = scenario('small')
+    t = targets_for('small')
+    plan = Plan(s['cfg'], s['cfar'], s['clus'], s['pre_p'], frames_per_launch=2)
+    d = plan.device_alloc(plan.cube_bytes)
+    e = plan.device_alloc(plan.cube_bytes)
+    try:
+        plan.synthesize_device(d, t, frame_idx=1)
+        plan.synthesize_device(e, [], frame_idx=2)   # noise only: no targets
+        for k in range(5):
+            plan.enqueue(d if k % 2 == 0 else e, 10 + k)
+        plan.drain()
+        rows = plan.results_rows(clear=False)
+        res = plan.results(clear=True)
+        want = []
+        for r in res:
+            for x in r['final_targets']:
+                want.append((r['frame_idx'], x['Range'], x['Velocity'], x['Angle'], x['Power']))
+            if not r['final_targets']:
+                want.append((r['frame_idx'],) + (np.nan,) * 4)
+        np.testing.assert_array_equal(rows, np.asarray(want, np.float64).reshape(-1, 5))
+        assert len(plan.results_rows()) == 0
+    finally:
+        plan.device_free(d)
+        plan.device_free(e)
+        plan.close()
