@@ -203,6 +203,8 @@ int32_t rsp_synthesize_device(rsp_plan* plan, const rsp_target_in* targets, int3
  * on the host.  rsp_drain waits for everything queued.  Results are kept in
  * enqueue order until rsp_results_clear. */
 int32_t rsp_enqueue_device(rsp_plan* plan, const void* d_cube, int32_t frame_idx);
+/* rsp_enqueue_device for n frames in one call (d_cubes[i], frame_idx[i]). */
+int32_t rsp_enqueue_device_n(rsp_plan* plan, const void* const* d_cubes, const int32_t* frame_idx, int32_t n);
 /* End-to-end form of rsp_enqueue_device: a host PNC cube in the plan's precision (no conversion;
  * rsp_process_cube converts).  Only the fast-time samples the chain reads (rsp_sizes.used_samples)
  * are copied, asynchronously on the plan's upload stream into a plan-owned device ring, so
@@ -218,7 +220,8 @@ int32_t rsp_results_get(const rsp_plan* plan, int32_t i, int32_t* frame_idx, rsp
 int32_t rsp_results_clear(rsp_plan* plan);
 /* Every queued result as rows of 5 doubles (frame_idx, Range, Velocity, Angle, Power), frames in
  * enqueue order, one NaN row for a frame without targets -- the detection-list payload of the
- * multi-GPU gather, in one call.  *n_rows = rows needed; RSP_ERR_OVERFLOW if more than cap. */
+ * multi-GPU gather, in one call.  *n_rows = rows needed (rows == NULL: a size query);
+ * RSP_ERR_OVERFLOW if more than cap. */
 int32_t rsp_results_rows(const rsp_plan* plan, double* rows, int64_t cap, int64_t* n_rows);
 
 /* ---- multi-GPU frame batch in one process (BASELINE config #3 for a MEX / loadlibrary host) ----

@@ -976,6 +976,17 @@ int32_t rsp_enqueue_device(rsp_plan* p, const void* d_cube, int32_t frame_idx) {
     return enqueue_frame(p, d_cube, -1, frame_idx);
 }
 
+int32_t rsp_enqueue_device_n(rsp_plan* p, const void* const* d_cubes, const int32_t* frame_idx, int32_t n) {
+    if (!p || (n > 0 && (!d_cubes || !frame_idx)) || n < 0) return fail(RSP_ERR_INVALID, "bad argument");
+    HIPCHK(hipSetDevice(p->device));
+    for (int i = 0; i < n; ++i) {
+        if (!d_cubes[i]) return fail(RSP_ERR_INVALID, "cube %d is null", i);
+        int rc = enqueue_frame(p, d_cubes[i], -1, frame_idx[i]);
+        if (rc) return rc;
+    }
+    return RSP_OK;
+}
+
 int32_t rsp_enqueue_host(rsp_plan* p, const void* h_cube, int32_t dtype, int32_t frame_idx) {
     if (!p || !h_cube) return fail(RSP_ERR_INVALID, "null argument");
     if (dtype != (p->g.prec == RSP_PREC_F64 ? RSP_C128 : RSP_C64))
@@ -1100,12 +1111,12 @@ int32_t rsp_results_get(const rsp_plan* p, int32_t i, int32_t* frame_idx, rsp_ta
 }
 
 int32_t rsp_results_rows(const rsp_plan* p, double* rows, int64_t cap, int64_t* n_rows) {
-    if (!p || !n_rows || (cap > 0 && !rows)) return fail(RSP_ERR_INVALID, "bad argument");
+    if (!p || !n_rows) return fail(RSP_ERR_INVALID, "bad argument");
     int64_t n = 0;
     for (const FrameResult& r : p->results) {
         const size_t nt = r.targets.size();
         for (size_t i = 0; i < std::max<size_t>(nt, 1); ++i, ++n) {
-            if (n >= cap) continue;
+            if (!rows || n >= cap) continue;
             double* o = rows + 5 * n;
             o[0] = r.frame_idx;
             if (nt) {
@@ -1116,8 +1127,8 @@ int32_t rsp_results_rows(const rsp_plan* p, double* rows, int64_t cap, int64_t* 
         }
     }
     *n_rows = n;
-    if (n > cap) return fail(RSP_ERR_OVERFLOW, "%lld rows > cap %lld", (long long)n, (long long)cap);
-    return RSP_OK;
+    if (rows && n > cap) return fail(RSP_ERR_OVERFLOW, "%lld rows > cap %lld", (long long)n, (long long)cap);
+    return RSP_OK;   // rows == NULL: a size query
 }
 
 int32_t rsp_results_clear(rsp_plan* p) {

@@ -142,6 +142,7 @@ PROTOTYPES = {
     'rsp_synthesize_device': (ct.c_int32, [_P, ct.POINTER(TargetIn), ct.c_int32, ct.c_int32, ct.c_uint64,
                                            ct.c_double, _P]),
     'rsp_enqueue_device': (ct.c_int32, [_P, _P, ct.c_int32]),
+    'rsp_enqueue_device_n': (ct.c_int32, [_P, ct.POINTER(_P), ct.POINTER(ct.c_int32), ct.c_int32]),
     'rsp_enqueue_host': (ct.c_int32, [_P, _P, ct.c_int32, ct.c_int32]),
     'rsp_host_alloc': (ct.c_int32, [_P, ct.c_int64, ct.POINTER(_P)]),
     'rsp_host_free': (ct.c_int32, [_P, _P]),

@@ -213,6 +213,13 @@ class Plan:
     def enqueue(self, ptr, frame_idx):
         check(lib().rsp_enqueue_device(self.h, ct.c_void_p(ptr), int(frame_idx)))
 
+    def enqueue_many(self, ptrs, frame_ids):
+        """rsp_enqueue_device_n: device cubes ptrs[i] as frames frame_ids[i], one C call."""
+        n = len(ptrs)
+        arr = (ct.c_void_p * max(n, 1))(*ptrs)
+        ids = (ct.c_int32 * max(n, 1))(*[int(f) for f in frame_ids])
+        check(lib().rsp_enqueue_device_n(self.h, arr, ids, n))
+
     def host_alloc(self, nbytes):
         """Pinned host memory (rsp_host_alloc); returns the address."""
         p = ct.c_void_p()

@@ -95,8 +95,7 @@ def test_results_rows_equal_results():
     try:
         plan.synthesize_device(d, t, frame_idx=1)
         plan.synthesize_device(e, [], frame_idx=2)   # noise only: no targets
-        for k in range(5):
-            plan.enqueue(d if k % 2 == 0 else e, 10 + k)
+        plan.enqueue_many([d if k % 2 == 0 else e for k in range(5)], range(10, 15))   # rsp_enqueue_device_n
         plan.drain()
         rows = plan.results_rows(clear=False)
         res = plan.results(clear=True)
