@@ -8,8 +8,9 @@ frame cubes (ring > 256 MiB Infinity Cache, so every step reads its cube from HB
 One step = one batch of ``--fpl`` distinct frames (one launch of each kernel) through
 DBF -> MTD -> pulse compression -> GOCA-CFAR -> S9 estimation (device) -> S10/S11
 clustering (host); batches rotate over the plan's lanes (3 HIP streams).  Warm-up
-always runs at least two batches per lane, so every stream is warm before the timed
-region whatever ``--warmup`` says.  ``value`` is frames/s = steps x fpl / time.
+always runs at least 20 batches (every lane, settled clocks) whatever ``--warmup`` says.
+``value`` is frames/s = steps x fpl / time; inside the timed region the frames are
+queued with one C call and every frame's final targets come back as packed rows.
 
 Multi-GPU: one process per GPU (torchrun); frames are sharded (each rank processes its
 own K frames, weak scaling); the only collective is an RCCL all-gather of the
