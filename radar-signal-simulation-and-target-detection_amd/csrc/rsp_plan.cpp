@@ -881,16 +881,29 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
         (rc = p->upload(&dang, ang)) || (rc = p->upload(&dkl, kl)))
         return bail(rc);
     k.range_axis = dra; k.velocity_axis = dva; k.beam_angles = dang; k.klut = dkl;
-    {   // K2 dispatch order: workgroup i of job j at key (i + 1/2) / nwg_j, so that the narrow FIR,
-        // medium and long jobs are interleaved in proportion through the launch
-        std::vector<std::pair<double, int>> key;
-        for (const K2Job& jb : p->jobs)
-            for (int i = 0; i < jb.wg_count; ++i) key.push_back({(i + 0.5) / jb.wg_count, jb.wg_begin + i});
-        std::stable_sort(key.begin(), key.end(), [](const std::pair<double, int>& a, const std::pair<double, int>& b) {
-            return a.first < b.first;
-        });
-        std::vector<int> order(key.size());
-        for (size_t i = 0; i < key.size(); ++i) order[i] = key[i].second;
+    {   // K2 dispatch order.  (1) Workgroups 2i and 2i+1 of a job (adjacent rows) form pair i, at
+        // key (i + 1/2) / npairs_j, so that the narrow FIR, medium and long jobs are interleaved in
+        // proportion through the launch.  (2) Workgroups go to the 8 XCDs round-robin by
+        // dispatch position, so the pairs are laid out 8 at a time: positions 16c + x and
+        // 16c + 8 + x hold pair 8c + x -- both rows of a pair on one XCD, whose L2 then serves
+        // the second half of every 128-B z line the first one fetched (a one-row overlap-save
+        // workgroup reads 64 B per line).  Unpaired workgroups go last.
+        struct Pr { double key; int a, b; };
+        std::vector<Pr> pr;
+        std::vector<int> single;
+        for (const K2Job& jb : p->jobs) {
+            const int np = jb.wg_count / 2;
+            for (int i = 0; i < np; ++i) pr.push_back({(i + 0.5) / np, jb.wg_begin + 2 * i, jb.wg_begin + 2 * i + 1});
+            if (jb.wg_count & 1) single.push_back(jb.wg_begin + jb.wg_count - 1);
+        }
+        std::stable_sort(pr.begin(), pr.end(), [](const Pr& x, const Pr& y) { return x.key < y.key; });
+        std::vector<int> order;
+        for (size_t c = 0; c < pr.size(); c += 8) {
+            const size_t e = std::min(pr.size(), c + 8);
+            for (size_t i = c; i < e; ++i) order.push_back(pr[i].a);
+            for (size_t i = c; i < e; ++i) order.push_back(pr[i].b);
+        }
+        for (int w : single) order.push_back(w);
         int* dord;
         if ((rc = p->upload(&dord, order))) return bail(rc);
         k.k2order = dord;
