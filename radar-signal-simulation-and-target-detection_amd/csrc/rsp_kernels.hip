@@ -1335,7 +1335,9 @@ __device__ __forceinline__ void s9_estimate(const DevConsts& k, const T* S, int 
 #ifndef RSP_K3_ABLATE
 #define RSP_K3_ABLATE 0   // timing ablations (A/B builds only): 1 = no CFAR, 2 = no map loads
 #endif
+#ifndef K3_VEC
 #define K3_VEC 12   // 16-B loads per beam per thread in flight
+#endif
 
 constexpr int floor4(int x) { return x >= 0 ? (x & ~3) : -((-x + 3) & ~3); }
 
