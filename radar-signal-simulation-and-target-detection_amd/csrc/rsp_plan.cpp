@@ -372,6 +372,9 @@ FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const void* const* in, int
 
 // Enqueue K1 -> K2 -> K3 for nf frames on lane L, plus the async detection read-back.
 // smap (optional, one frame): K3 also writes rdm_for_cfar_all there.
+#ifndef RSP_K3_TILE_KB
+#define RSP_K3_TILE_KB 48   // KB of S per K3 tile (48: 2 Doppler bands at P = 128, 3 workgroups per CU)
+#endif
 #ifndef RSP_K12_SUB
 #define RSP_K12_SUB 0
 #endif
@@ -824,14 +827,15 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
     // K3 tile: <= 64 KB of S per tile (>= 2 workgroups per CU); the fast path covers RT 32/64
     g.cfar_hR = (std::max(g.refR + g.guardR, 2) + 3) & ~3;   // halo, multiple of 4 (16-B tile loads)
     // tiles of RT range cells (64 complex single / 32 complex double: the fast path) x a band of
-    // Doppler rows, <= 68 KB of S per tile (2 workgroups per CU): at P = 128 one band holds every row; longer P (x4's 256)
+    // Doppler rows, <= RSP_K3_TILE_KB of S per tile (48 KB: 3 workgroups per CU; at P = 128 two
+    // bands measured 78 vs 85 us per 8 x2 frames for one band at 2 workgroups per CU): at P = 128 one band holds every row; longer P (x4's 256)
     // splits the rows into bands, each with the rV + gV window rows on either side
     g.cfar_RT = p->rsz == 4 ? 64 : 32;
     // LDS row stride, 16-B aligned; complex double + 2 cells (bank spread, k3_cfar)
     g.cfar_W = ((g.cfar_RT + 2 * g.cfar_hR + 3) & ~3) + (p->rsz == 8 ? 2 : 0);
     {
         const int hV = g.refV + g.guardV, ncut = std::max(P - 2 * hV, 1);
-        const int rows_max = (int)((68 * 1024) / ((size_t)g.cfar_W * p->rsz));
+        const int rows_max = (int)((RSP_K3_TILE_KB * 1024) / ((size_t)g.cfar_W * p->rsz));
         if (rows_max - 2 * hV < 1) return bail(fail(RSP_ERR_UNSUPPORTED, "CFAR window %d x %d exceeds the LDS tile", hV, g.cfar_hR));
         g.cfar_nband = (ncut + rows_max - 2 * hV - 1) / (rows_max - 2 * hV);
         g.cfar_VB = (ncut + g.cfar_nband - 1) / g.cfar_nband;
