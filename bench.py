@@ -81,6 +81,10 @@ def parse():
     ap.add_argument('--e2e', action='store_true',
                     help='end-to-end mode: frames enter as host cubes in pinned memory (rsp_enqueue_host: '
                          'async H2D of the used samples overlapping the kernels), not the headline')
+    ap.add_argument('--dist-backend', default='nccl', choices=['nccl', 'gloo'],
+                    help='collective backend for N > 1 (nccl = RCCL over xGMI; gloo: CPU tensors, for rehearsing '
+                         'several ranks on one GPU together with --same-device)')
+    ap.add_argument('--same-device', action='store_true', help='every rank uses GPU 0 (rehearsal only)')
     ap.add_argument('--stage-timing', action='store_true',
                     help='HIP events around every kernel in the timed region (diagnostic: overlapped durations)')
     return ap.parse_args()
@@ -237,11 +241,15 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', 0))
     dist = None
+    dev = 0 if (world == 1 or a.same_device) else local
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if a.dist_backend == 'nccl':
+            torch.cuda.set_device(dev)
+            dist.init_process_group('nccl', device_id=torch.device('cuda', dev))
+        else:
+            dist.init_process_group('gloo')
 
     from rsp import config as C
     from rsp.precompute import precompute
@@ -249,8 +257,7 @@ def main():
 
     cfg, cfar, clus, W, ang, k = C.named_config(a.config)
     pre = precompute(cfg, W, ang, k, C.V8_FIR)
-    plan = Plan(cfg, cfar, clus, pre, device=local if world > 1 else 0, frames_per_launch=a.fpl,
-                precision=a.precision)
+    plan = Plan(cfg, cfar, clus, pre, device=dev, frames_per_launch=a.fpl, precision=a.precision)
     sz = plan.sizes
     targets = scene(cfg)
     cube_bytes = plan.cube_bytes
@@ -312,7 +319,7 @@ def main():
     if dist is not None:
         # the one collective: gather every rank's detection list (RCCL over xGMI)
         from rsp.dist import gather_rows
-        counts, bufs = gather_rows(rows, rank, world, device=local)
+        counts, bufs = gather_rows(rows, rank, world, device=dev)
         n_targets_all = int(sum(np.count_nonzero(~np.isnan(b[:c, 1])) for c, b in zip(counts, bufs)))
     else:
         n_targets_all = int(np.count_nonzero(~np.isnan(rows[:, 1])))
@@ -325,7 +332,7 @@ def main():
     el = t1 - t0
     if dist is not None:
         import torch
-        t = torch.tensor([el], dtype=torch.float64, device='cuda')
+        t = torch.tensor([el], dtype=torch.float64, device='cuda' if a.dist_backend == 'nccl' else 'cpu')
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
