@@ -3,7 +3,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifndef RSP_MAX_F
 #define RSP_MAX_F 8          // frames batched per launch
+#endif
 #define RSP_LANES 4          // max streams of the throughput queue (batches in flight)
 #define RSP_K2_POINTS 4096   // complex points per pulse-compression workgroup
 #define K2_THREADS 256       // threads per pulse-compression workgroup (16 points each)

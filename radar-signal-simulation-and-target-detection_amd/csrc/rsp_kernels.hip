@@ -265,10 +265,12 @@ struct StoreLds {
 };
 
 // Twiddles w[r] = W_{Ns R}^{k r}, r = 1..R-1, of one butterfly (conjugated for the inverse)
-// from this pass's table row k: CMP = false: full rows [k][r-1] (R-1 loads); CMP = true:
-// compact rows [k][i] = W^(k 2^i) (lgR loads), the other powers formed as products of at
-// most lgR - 1 of them.
-template <int R, bool INV, bool CMP, class V>
+// from this pass's table: CMP = false: full rows [k][r-1] (R-1 loads, twk = row k); CMP = true:
+// compact columns [i][k] = W^(k 2^i) (lgR loads, twk = table + k, column stride NS), the other
+// powers formed as products of at most lgR - 1 of them.  Column-major so that the lanes of a
+// pass (consecutive k) read consecutive 16-B entries: conflict-free, where [k][i] rows of 4
+// entries put every 4th lane on the same banks (tools/lds_conflicts_k2v2.py).
+template <int R, bool INV, bool CMP, int NS, class V>
 __device__ __forceinline__ void load_tw(const V* twk, V (&w)[R]) {
     if constexpr (!CMP) {
 #pragma unroll
@@ -281,7 +283,7 @@ __device__ __forceinline__ void load_tw(const V* twk, V (&w)[R]) {
         V b[lgR];
 #pragma unroll
         for (int i = 0; i < lgR; ++i) {
-            const V t = twk[i];
+            const V t = twk[i * NS];
             b[i] = V{t.x, INV ? -t.y : t.y};
         }
 #pragma unroll
@@ -362,7 +364,7 @@ __device__ __forceinline__ void sh_load(const V* buf, int rs, int nrows, const V
             const int k = j & (Ns - 1);
             const V* src = buf + row * rs + lidx<SH>(j);
             V w[R];
-            if (LGNS > 0) load_tw<R, INV, CMP>(tw + k * tw_row(R, CMP), w);
+            if (LGNS > 0) load_tw<R, INV, CMP, Ns>(tw + (CMP ? k : k * tw_row(R, CMP)), w);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 V x = src[r * nb + (SH ? (r * nb) >> SH : 0)];
@@ -448,7 +450,7 @@ __device__ __forceinline__ void shg_load(const V* buf, int rs, int nrows, const 
             const int row = beta / nb, j = beta - row * nb;
             const V* src = buf + row * rs;
             V w[R];
-            if (NS > 1) load_tw<R, INV, CMP>(tw + (j % NS) * tw_row(R, CMP), w);
+            if (NS > 1) load_tw<R, INV, CMP, NS>(tw + (CMP ? j % NS : (j % NS) * tw_row(R, CMP)), w);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 V x = src[lidx<SH>(j + r * nb)];

@@ -96,9 +96,20 @@ void radix_plan(int m, int* nrad, int* rad, bool pal = false) {
     if (pal && *nrad == 3) std::swap(rad[1], rad[2]);
 }
 
+void push_pass_twiddles(std::vector<cd>& out, int Ns, int R, bool cmp) {
+    if (cmp) {
+        for (int r = 1; r < R; r *= 2)
+            for (int k = 0; k < Ns; ++k) out.push_back(root_of_unity((long long)k * r, (long long)Ns * R));
+    } else {
+        for (int k = 0; k < Ns; ++k)
+            for (int r = 1; r < R; ++r) out.push_back(root_of_unity((long long)k * r, (long long)Ns * R));
+    }
+}
+
 // Per-pass Stockham twiddle tables of a 2^m-point FFT (radix order reversed if rev),
 // concatenated: pass q >= 1 owns Ns_q x (R_q - 1) entries T[k][r-1] = exp(-2 pi i k r / (Ns_q R_q))
-// (must match tw_pass_off() in rsp_kernels.hip).  Compact rows (cmp): r = 1, 2, 4, 8 only.
+// (must match tw_pass_off() in rsp_kernels.hip).  Compact tables (cmp): r = 1, 2, 4, 8 only,
+// stored column-major, [i][k] = T[k][2^i] (load_tw in rsp_kernels.hip).
 // The angle's numerator is reduced modulo the period first, so every entry is the correctly
 // rounded double of the exact root of unity's angle.
 void build_pass_twiddles(int m, std::vector<cd>& out, bool rev = false, bool cmp = false, bool pal = false) {
@@ -108,9 +119,7 @@ void build_pass_twiddles(int m, std::vector<cd>& out, bool rev = false, bool cmp
     int Ns = 1;
     for (int q = 0; q < nrad; ++q) {
         const int R = rad[q];
-        if (q > 0)
-            for (int k = 0; k < Ns; ++k)
-                for (int r = 1; r < R; r = cmp ? 2 * r : r + 1) out.push_back(root_of_unity((long long)k * r, (long long)Ns * R));
+        if (q > 0) push_pass_twiddles(out, Ns, R, cmp);
         Ns *= R;
     }
 }
@@ -122,9 +131,7 @@ void build_mix_twiddles(int R1, std::vector<cd>& out, bool cmp) {
     int Ns = 1;
     for (int q = 0; q < 3; ++q) {
         const int R = rad[q];
-        if (q > 0)
-            for (int k = 0; k < Ns; ++k)
-                for (int r = 1; r < R; r = cmp ? 2 * r : r + 1) out.push_back(root_of_unity((long long)k * r, (long long)Ns * R));
+        if (q > 0) push_pass_twiddles(out, Ns, R, cmp);
         Ns *= R;
     }
 }

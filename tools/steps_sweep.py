@@ -1,0 +1,59 @@
+"""Fixed-overhead probe of the bench's timed region: one plan, the same ring as bench.py, then
+timed runs of k batches (sync on both sides, like bench.py) for several k, back to back and after
+an idle gap.  T(k) = a + b k separates the per-batch rate b from the fixed cost a.
+usage: steps_sweep.py [config] [precision] [frames per launch]   (AB_LIB=path: a variant library)"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, 'radar-signal-simulation-and-target-detection_amd'))
+import numpy as np  # noqa: E402
+import bench  # noqa: E402
+from rsp import _abi  # noqa: E402
+if os.environ.get('AB_LIB'):   # timing experiments only: an A/B variant of librsp.so
+    _abi.LIB_PATH = os.environ['AB_LIB']
+from rsp import config as C  # noqa: E402
+from rsp.precompute import precompute  # noqa: E402
+from rsp.plan import Plan  # noqa: E402
+
+name = sys.argv[1] if len(sys.argv) > 1 else 'x2'
+prec = sys.argv[2] if len(sys.argv) > 2 else 'c128'
+F = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+cfg, cfar, clus, W, ang, k = C.named_config(name)
+pre = precompute(cfg, W, ang, k, C.V8_FIR)
+plan = Plan(cfg, cfar, clus, pre, device=0, frames_per_launch=F, precision=prec)
+tg = bench.scene(cfg)
+ring = [plan.device_alloc(plan.cube_bytes) for _ in range(8)]
+for i, p in enumerate(ring):
+    plan.synthesize_device(p, tg, frame_idx=1 + i, seed=20250101)
+    tg = C.evolve_targets(tg, cfg)
+plan.sync()
+seq = [ring[i % 8] for i in range(400 * 8)]
+
+
+def run(nb):
+    plan.sync()
+    t0 = time.perf_counter()
+    plan.enqueue_many(seq[:nb * F], range(1, 1 + nb * F))
+    plan.drain()
+    plan.results_rows(clear=True)
+    plan.sync()
+    return time.perf_counter() - t0
+
+
+run(20 * 8 // F)
+run(20 * 8 // F)
+res = []
+for nb in [x * 8 // F for x in [20, 20, 40, 80, 160, 320, 20, 20]]:
+    res.append((nb, run(nb)))
+    print('back-to-back k=%3d  %.3f ms  %.4f ms/batch' % (nb, res[-1][1] * 1e3, res[-1][1] * 1e3 / nb), flush=True)
+ks = np.array([r[0] for r in res], float)
+ts = np.array([r[1] for r in res]) * 1e3
+b, a = np.polyfit(ks, ts, 1)
+print('F=%d fit: T(k) = %.3f ms + %.4f ms x k   (160 frames -> %.0f frames/s, k=inf -> %.0f)' %
+      (F, a, b, 160 / (a + 160 / F * b) * 1e3, F / b * 1e3))
+for gap in [0.002, 0.02, 0.2]:
+    time.sleep(gap)
+    print('after %.0f ms idle k=%d  %.3f ms' % (gap * 1e3, 20 * 8 // F, run(20 * 8 // F) * 1e3), flush=True)
