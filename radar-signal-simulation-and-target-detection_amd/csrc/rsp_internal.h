@@ -7,6 +7,9 @@
 #define RSP_MAX_F 8          // frames batched per launch
 #endif
 #define RSP_LANES 4          // max streams of the throughput queue (batches in flight)
+#ifndef RSP_NLANES
+#define RSP_NLANES 3         // streams the throughput queue uses (<= RSP_LANES)
+#endif
 #define RSP_K2_POINTS 4096   // complex points per pulse-compression workgroup
 #define K2_THREADS 256       // threads per pulse-compression workgroup (16 points each)
 #define RSP_THREADS 256

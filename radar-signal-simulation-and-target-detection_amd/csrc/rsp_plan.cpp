@@ -11,7 +11,11 @@
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
+#include <condition_variable>
 #include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -153,6 +157,60 @@ struct Lane {
     bool busy = false;
 };
 
+// Host worker threads for S10/S11 (fsf:302-407) of the queue's frames: a harvested batch's
+// frames are clustered in parallel while the host thread goes on launching batches, so the
+// clustering neither delays the next launch nor serialises the end of a run (one x2 frame with
+// ~250 detections takes ~60 us; eight in a row were ~0.5 ms of host time per batch).
+class ClusterPool {
+public:
+    explicit ClusterPool(int n) {
+        for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+    }
+    ~ClusterPool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    void submit(std::function<void()> f) {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            q_.push_back(std::move(f));
+            ++pending_;
+        }
+        cv_.notify_one();
+    }
+    void wait() {   // every submitted task has finished
+        std::unique_lock<std::mutex> g(m_);
+        done_.wait(g, [this] { return pending_ == 0; });
+    }
+
+private:
+    void loop() {
+        for (;;) {
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [this] { return stop_ || !q_.empty(); });
+                if (q_.empty()) return;
+                f = std::move(q_.front());
+                q_.pop_front();
+            }
+            f();
+            std::lock_guard<std::mutex> g(m_);
+            if (--pending_ == 0) done_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    std::deque<std::function<void()>> q_;
+    int pending_ = 0;
+    bool stop_ = false;
+};
+
 struct FrameResult {
     int frame_idx;
     int n_dets;
@@ -185,7 +243,7 @@ struct rsp_plan {
     unsigned char* h_stage = nullptr;   // pinned staging for uploads
     size_t h_stage_bytes = 0;
     Lane lanes[RSP_LANES];
-    int nlanes = 3;   // lanes (streams) of the throughput queue
+    int nlanes = RSP_NLANES;   // lanes (streams) of the throughput queue
     int next_lane = 0;
     // live stage timing of the queue (rsp_set_stage_timing): HIP events around K1/K2/K3 of
     // every batch, summed at harvest
@@ -206,8 +264,14 @@ struct rsp_plan {
     std::vector<hipEvent_t> slot_ready, slot_free;
     std::vector<char> slot_used;
     int ring_next = 0;
-    std::deque<FrameResult> results;
+    std::deque<FrameResult> results;   // deque: push_back keeps the elements the pool writes in place
     bool overflow_seen = false;
+    // clustering workers of the queue (created with the first batch of F > 1 frames); every
+    // reader of `results` calls results_ready() first.  Declared after `results`: destroyed first.
+    std::unique_ptr<ClusterPool> pool;
+    void results_ready() const {
+        if (pool) pool->wait();
+    }
 
     ~rsp_plan();
     int dalloc_bytes(void** p, size_t bytes) {
@@ -264,6 +328,7 @@ struct rsp_plan {
 };
 
 rsp_plan::~rsp_plan() {
+    results_ready();
     (void)hipSetDevice(device);
     for (auto& L : lanes) {
         if (L.stream) (void)hipStreamSynchronize(L.stream);
@@ -465,10 +530,18 @@ int harvest(rsp_plan* p, Lane& L, std::vector<std::vector<rsp_detection>>* keep_
         if (n > na)
             HIPCHK(hipMemcpy(dets.data() + na, L.dets + (size_t)(p->g.max_dets + 1) * f + 1 + na,
                              sizeof(DevDet) * (n - na), hipMemcpyDeviceToHost));
-        rsp_cluster_frame(p->cl, dets, fr.targets);
         if (fr.overflow) p->overflow_seen = true;
-        if (keep_dets) (*keep_dets)[f] = dets;
-        p->results.push_back(std::move(fr));
+        if (keep_dets || L.nf == 1) {   // synchronous frame paths: cluster here
+            rsp_cluster_frame(p->cl, dets, fr.targets);
+            if (keep_dets) (*keep_dets)[f] = dets;
+            p->results.push_back(std::move(fr));
+        } else {
+            if (!p->pool) p->pool.reset(new ClusterPool(std::max(1, std::min<int>(p->F, 8))));
+            p->results.push_back(std::move(fr));
+            FrameResult* slot = &p->results.back();
+            const rsp_cluster_params cl = p->cl;
+            p->pool->submit([cl, slot, d = std::move(dets)]() mutable { rsp_cluster_frame(cl, d, slot->targets); });
+        }
     }
     return RSP_OK;
 }
@@ -492,6 +565,7 @@ int drain_all(rsp_plan* p) {
         rc = harvest(p, p->lanes[(p->next_lane + q) % p->nlanes]);
         if (rc) return rc;
     }
+    p->results_ready();
     return RSP_OK;
 }
 
@@ -1080,6 +1154,7 @@ int32_t rsp_process_targets_multi(rsp_plan* const* plans, int32_t n_plans, const
         if (!plans[i]) return fail(RSP_ERR_INVALID, "plan %d is null", i);
         for (int j = 0; j < i; ++j)
             if (plans[j] == plans[i]) return fail(RSP_ERR_INVALID, "plan %d listed twice (one host thread per plan)", i);
+        plans[i]->results_ready();
         if (!plans[i]->results.empty() || plans[i]->npend)
             return fail(RSP_ERR_INVALID, "plan %d has queued frames or uncleared results", i);
     }
@@ -1139,6 +1214,7 @@ int32_t rsp_drain(rsp_plan* p) {
 
 int32_t rsp_results_count(const rsp_plan* p, int32_t* n_frames, int64_t* n_targets) {
     if (!p) return fail(RSP_ERR_INVALID, "null argument");
+    p->results_ready();
     int64_t nt = 0;
     for (auto& r : p->results) nt += (int64_t)r.targets.size();
     if (n_frames) *n_frames = (int32_t)p->results.size();
@@ -1148,7 +1224,9 @@ int32_t rsp_results_count(const rsp_plan* p, int32_t* n_frames, int64_t* n_targe
 
 int32_t rsp_results_get(const rsp_plan* p, int32_t i, int32_t* frame_idx, rsp_target* targets, int32_t cap,
                         int32_t* n_targets, int32_t* n_dets) {
-    if (!p || i < 0 || i >= (int)p->results.size()) return fail(RSP_ERR_INVALID, "result index out of range");
+    if (!p) return fail(RSP_ERR_INVALID, "null argument");
+    p->results_ready();
+    if (i < 0 || i >= (int)p->results.size()) return fail(RSP_ERR_INVALID, "result index out of range");
     const FrameResult& r = p->results[i];
     if (frame_idx) *frame_idx = r.frame_idx;
     if (n_targets) *n_targets = (int32_t)r.targets.size();
@@ -1160,6 +1238,7 @@ int32_t rsp_results_get(const rsp_plan* p, int32_t i, int32_t* frame_idx, rsp_ta
 
 int32_t rsp_results_rows(const rsp_plan* p, double* rows, int64_t cap, int64_t* n_rows) {
     if (!p || !n_rows) return fail(RSP_ERR_INVALID, "bad argument");
+    p->results_ready();
     int64_t n = 0;
     for (const FrameResult& r : p->results) {
         const size_t nt = r.targets.size();
@@ -1181,6 +1260,7 @@ int32_t rsp_results_rows(const rsp_plan* p, double* rows, int64_t cap, int64_t* 
 
 int32_t rsp_results_clear(rsp_plan* p) {
     if (!p) return fail(RSP_ERR_INVALID, "null argument");
+    p->results_ready();
     p->results.clear();
     return RSP_OK;
 }
