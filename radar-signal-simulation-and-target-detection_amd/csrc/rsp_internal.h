@@ -30,6 +30,10 @@
 #ifndef RSP_K2_ORDER
 #define RSP_K2_ORDER 1
 #endif
+// Ns = 1 pass outputs of the overlap-save blocks XOR-swizzled (1) or padded like the others (0)
+#ifndef RSP_K2_XOR
+#define RSP_K2_XOR 1
+#endif
 #ifndef RSP_K2_SH64
 #define RSP_K2_SH64 5
 #endif

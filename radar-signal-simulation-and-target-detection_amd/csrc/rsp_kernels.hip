@@ -349,12 +349,13 @@ constexpr int tw_total(int LG, bool rev = false, bool cmp = false, bool pal = fa
 // With power-of-two nb, Ns and pads every 2^SH, lidx(j + r nb) = lidx(j) + r nb + ((r nb) >> SH)
 // and lidx(idxD + r Ns) = lidx(idxD) + r Ns + ((r Ns) >> SH): every LDS address of a butterfly
 // is a per-thread base plus a compile-time offset (ds_read/ds_write immediate offsets).
-template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP = false, class V>
+template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP = false, int XL = 0, class V>
 __device__ __forceinline__ void sh_load(const V* buf, int rs, int nrows, const V* tw, V (&v)[NB][R]) {
     constexpr int lgR = clog2(R);
     constexpr int lgnb = LGL - lgR;
     constexpr int nb = 1 << lgnb;
     constexpr int Ns = 1 << LGNS;
+    static_assert(!XL || nb % 128 == 0, "XOR-swizzled input needs r nb to keep the swizzle bits");
     const int total = nb * nrows;
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
@@ -362,12 +363,12 @@ __device__ __forceinline__ void sh_load(const V* buf, int rs, int nrows, const V
         if (beta < total) {
             const int row = beta >> lgnb, j = beta & (nb - 1);
             const int k = j & (Ns - 1);
-            const V* src = buf + row * rs + lidx<SH>(j);
+            const V* src = XL ? buf + (row << LGL) + (j ^ ((j >> 4) & 7)) : buf + row * rs + lidx<SH>(j);
             V w[R];
             if (LGNS > 0) load_tw<R, INV, CMP, Ns>(tw + (CMP ? k : k * tw_row(R, CMP)), w);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                V x = src[r * nb + (SH ? (r * nb) >> SH : 0)];
+                V x = src[r * nb + (SH && !XL ? (r * nb) >> SH : 0)];
                 if (r > 0 && LGNS > 0) x = vmul(x, w[r]);
                 v[t][r] = x;
             }
@@ -376,12 +377,17 @@ __device__ __forceinline__ void sh_load(const V* buf, int rs, int nrows, const V
 }
 
 // Radix-R DFT of the loaded butterflies and the Stockham store (through policy st).
-template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, class V, class St>
+// XL = 1: the output is stored XOR-swizzled, element i at (i ^ ((i >> 4) & 7)) of a row of 2^LGL
+// (Ns = 1 radix-16 passes only).  Their stores write 16 j + r for lane j, which the pad layout
+// puts 2-way on the banks of every group of 8 lanes; swizzled, the 8 lanes hit 8 distinct
+// 16-B banks, and the next pass's reads (j + r nb, nb a multiple of 128) stay conflict-free.
+template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, int XL = 0, class V, class St>
 __device__ __forceinline__ void sh_store(V (&v)[NB][R], int rs, int nrows, const St& st) {
     constexpr int lgR = clog2(R);
     constexpr int lgnb = LGL - lgR;
     constexpr int nb = 1 << lgnb;
     constexpr int Ns = 1 << LGNS;
+    static_assert(!XL || (LGNS == 0 && R == 16), "XOR-swizzled output: Ns = 1 radix-16 passes");
     const int total = nb * nrows;
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
@@ -391,18 +397,24 @@ __device__ __forceinline__ void sh_store(V (&v)[NB][R], int rs, int nrows, const
             const int k = j & (Ns - 1);
             Dft<R, INV, V>::run(v[t]);
             const int idxD = ((j >> LGNS) << (LGNS + lgR)) + k;
-            const int wbase = row * rs + lidx<SH>(idxD);
+            if constexpr (XL) {
+                const int wbase = (row << LGL) + idxD, c = j & 7;
 #pragma unroll
-            for (int r = 0; r < R; ++r)
-                st.put(t * R + r, row, idxD + r * Ns, wbase + r * Ns + (SH ? (r * Ns) >> SH : 0), v[t][r]);
+                for (int r = 0; r < R; ++r) st.put(t * R + r, row, idxD + r, wbase + (r & 8) + ((r & 7) ^ c), v[t][r]);
+            } else {
+                const int wbase = row * rs + lidx<SH>(idxD);
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    st.put(t * R + r, row, idxD + r * Ns, wbase + r * Ns + (SH ? (r * Ns) >> SH : 0), v[t][r]);
+            }
         }
     }
 }
 
-template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP, class V, class St>
+template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP, int XL = 0, class V, class St>
 __device__ __forceinline__ void sh_pass(V* buf, int rs, int nrows, const V* tw, const St& st) {
     V v[NB][R];
-    sh_load<R, INV, NB, SH, NTHR, LGL, LGNS, CMP>(buf, rs, nrows, tw, v);
+    sh_load<R, INV, NB, SH, NTHR, LGL, LGNS, CMP, XL>(buf, rs, nrows, tw, v);
     __syncthreads();
     sh_store<R, INV, NB, SH, NTHR, LGL, LGNS>(v, rs, nrows, st);
     __syncthreads();
@@ -412,7 +424,7 @@ __device__ __forceinline__ void sh_pass(V* buf, int rs, int nrows, const V* tw, 
 // pass n_passes - 1 stores through `last`, the others through `mid`.  tw = this plan's
 // concatenated tables.  PTS = complex points per thread (nrows * L / NTHR).
 template <int LG, int Q, int QEND, int LGNS, int PTS, bool INV, bool REV, int SH, int NTHR, bool CMP, bool PAL = false,
-          class V, class StMid, class StLast>
+          int XIN = 0, class V, class StMid, class StLast>
 __device__ __forceinline__ void fft_range(V* buf, int rs, int nrows, const V* tw, const StMid& mid, const StLast& last) {
     constexpr int NP = n_passes(LG);
     if constexpr (Q < QEND) {
@@ -421,9 +433,9 @@ __device__ __forceinline__ void fft_range(V* buf, int rs, int nrows, const V* tw
         constexpr int NB = (PTS + R - 1) / R;
         const V* twq = tw + tw_pass_off(LG, Q, REV, CMP, PAL);
         if constexpr (Q == NP - 1)
-            sh_pass<R, INV, NB, SH, NTHR, LG, LGNS, CMP>(buf, rs, nrows, twq, last);
+            sh_pass<R, INV, NB, SH, NTHR, LG, LGNS, CMP, XIN>(buf, rs, nrows, twq, last);
         else
-            sh_pass<R, INV, NB, SH, NTHR, LG, LGNS, CMP>(buf, rs, nrows, twq, mid);
+            sh_pass<R, INV, NB, SH, NTHR, LG, LGNS, CMP, XIN>(buf, rs, nrows, twq, mid);
         fft_range<LG, Q + 1, QEND, LGNS + RB, PTS, INV, REV, SH, NTHR, CMP, PAL>(buf, rs, nrows, tw, mid, last);
     }
 }
@@ -439,30 +451,32 @@ __device__ __forceinline__ void fft_passes(V* buf, int rs, int nrows, const V* t
 // Same formulation as sh_load / sh_store with L, R, Ns compile-time constants that need not be
 // powers of two: divisions by them become multiply-shifts, and every LDS index is padded per
 // element (lidx of the full position).
-template <int R, bool INV, int NB, int SH, int NTHR, int L, int NS, bool CMP, class V>
+template <int R, bool INV, int NB, int SH, int NTHR, int L, int NS, bool CMP, int XL = 0, class V>
 __device__ __forceinline__ void shg_load(const V* buf, int rs, int nrows, const V* tw, V (&v)[NB][R]) {
     constexpr int nb = L / R;
+    static_assert(!XL || nb % 128 == 0, "XOR-swizzled input needs r nb to keep the swizzle bits");
     const int total = nb * nrows;
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
         const int beta = threadIdx.x + t * NTHR;
         if (beta < total) {
             const int row = beta / nb, j = beta - row * nb;
-            const V* src = buf + row * rs;
+            const V* src = XL ? buf + row * L + (j ^ ((j >> 4) & 7)) : buf + row * rs;
             V w[R];
             if (NS > 1) load_tw<R, INV, CMP, NS>(tw + (CMP ? j % NS : (j % NS) * tw_row(R, CMP)), w);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                V x = src[lidx<SH>(j + r * nb)];
+                V x = XL ? src[r * nb] : src[lidx<SH>(j + r * nb)];
                 if (r > 0 && NS > 1) x = vmul(x, w[r]);
                 v[t][r] = x;
             }
         }
     }
 }
-template <int R, bool INV, int NB, int SH, int NTHR, int L, int NS, class V, class St>
+template <int R, bool INV, int NB, int SH, int NTHR, int L, int NS, int XL = 0, class V, class St>
 __device__ __forceinline__ void shg_store(V (&v)[NB][R], int rs, int nrows, const St& st) {
     constexpr int nb = L / R;
+    static_assert(!XL || (NS == 1 && R == 16), "XOR-swizzled output: Ns = 1 radix-16 passes");
     const int total = nb * nrows;
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
@@ -471,15 +485,22 @@ __device__ __forceinline__ void shg_store(V (&v)[NB][R], int rs, int nrows, cons
             const int row = beta / nb, j = beta - row * nb;
             Dft<R, INV, V>::run(v[t]);
             const int idxD = (j / NS) * (NS * R) + j % NS;
+            if constexpr (XL) {
+                const int wbase = row * L + idxD, c = j & 7;
 #pragma unroll
-            for (int r = 0; r < R; ++r) st.put(t * R + r, row, idxD + r * NS, row * rs + lidx<SH>(idxD + r * NS), v[t][r]);
+                for (int r = 0; r < R; ++r) st.put(t * R + r, row, idxD + r, wbase + (r & 8) + ((r & 7) ^ c), v[t][r]);
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    st.put(t * R + r, row, idxD + r * NS, row * rs + lidx<SH>(idxD + r * NS), v[t][r]);
+            }
         }
     }
 }
-template <int R, bool INV, int NB, int SH, int NTHR, int L, int NS, bool CMP, class V, class St>
+template <int R, bool INV, int NB, int SH, int NTHR, int L, int NS, bool CMP, int XL = 0, class V, class St>
 __device__ __forceinline__ void shg_pass(V* buf, int rs, int nrows, const V* tw, const St& st) {
     V v[NB][R];
-    shg_load<R, INV, NB, SH, NTHR, L, NS, CMP>(buf, rs, nrows, tw, v);
+    shg_load<R, INV, NB, SH, NTHR, L, NS, CMP, XL>(buf, rs, nrows, tw, v);
     __syncthreads();
     shg_store<R, INV, NB, SH, NTHR, L, NS>(v, rs, nrows, st);
     __syncthreads();
@@ -1008,10 +1029,12 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     const V* twF = twL;
     const V* twI = k2_tw_sym(LGM) ? twL : twL + NTWF;
     // forward pass 0 (Ns = 1, no twiddles) straight from the loaded samples
-    sh_store<R0, false, NB0, SH, K2_THREADS, LGM, 0>(v0, rs, rows, StoreLds<V>{L});
+    // the Ns = 1 passes' outputs XOR-swizzled (sh_store) when a middle pass reads them (3 passes)
+    constexpr int XZ = (NP == 3 && R0 == 16 && RL == 16 && RSP_K2_XOR) ? 1 : 0;
+    sh_store<R0, false, NB0, SH, K2_THREADS, LGM, 0, XZ>(v0, rs, rows, StoreLds<V>{L});
     __syncthreads();
     // forward passes 1 .. NP-2
-    fft_range<LGM, 1, NP - 1, RB0, 16, false, false, SH, K2_THREADS, CMP, PAL>(L, rs, rows, twF, StoreLds<V>{L},
+    fft_range<LGM, 1, NP - 1, RB0, 16, false, false, SH, K2_THREADS, CMP, PAL, XZ>(L, rs, rows, twF, StoreLds<V>{L},
                                                                                StoreLds<V>{L});
     // fused: forward last pass, x H (1/M folded in), inverse pass 0 of the reversed plan
     {
@@ -1025,13 +1048,13 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
 #pragma unroll
             for (int r = 0; r < RL; ++r) v[t][r] = vmul(v[t][r], hreg[(t % NHT) * RL + r]);
         }
-        sh_store<RL, true, NBL, SH, K2_THREADS, LGM, 0>(v, rs, rows, StoreLds<V>{L});
+        sh_store<RL, true, NBL, SH, K2_THREADS, LGM, 0, XZ>(v, rs, rows, StoreLds<V>{L});
         __syncthreads();
     }
     // inverse passes 1 .. NP-1 (reversed radices); the last keeps the valid overlap-save
     // outputs = stitched gates
     const int gend = min(sd.gb, g0 + sd.V);
-    fft_range<LGM, 1, NP, RBL, 16, true, true, SH, K2_THREADS, CMP, PAL>(
+    fft_range<LGM, 1, NP, RBL, 16, true, true, SH, K2_THREADS, CMP, PAL, XZ>(
         L, rs, rows, twI, StoreLds<V>{L},
         StoreRdm<V>{buf_rsrc(rdm, (unsigned)(rows_total * G * sizeof(V))),
                     buf_rsrc(mag, (unsigned)(rows_total * g.Gp * sizeof(T))), G, g.Gp, row0, rows_total, Lh1, g0,
@@ -1099,9 +1122,10 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
     for (int e = tid; e < NTWF; e += K2_THREADS) twL[e] = twl[e];
     const V* twF = twL;
     const V* twI = twF;   // palindrome: the reversed plan's table is the forward one
-    shg_store<R0, false, NB0, SH, K2_THREADS, M, 1>(v0, rs, rows, StoreLds<V>{L});
+    constexpr int XZ = RSP_K2_XOR;   // Ns = 1 outputs XOR-swizzled (see sh_store)
+    shg_store<R0, false, NB0, SH, K2_THREADS, M, 1, XZ>(v0, rs, rows, StoreLds<V>{L});
     __syncthreads();
-    shg_pass<R1, false, NB1, SH, K2_THREADS, M, NS1, CMP>(L, rs, rows, twF, StoreLds<V>{L});
+    shg_pass<R1, false, NB1, SH, K2_THREADS, M, NS1, CMP, XZ>(L, rs, rows, twF, StoreLds<V>{L});
     {
         V v[NB0][R0];
         shg_load<R0, false, NB0, SH, K2_THREADS, M, NS2, CMP>(L, rs, rows, twF + TW2, v);
@@ -1112,10 +1136,10 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
 #pragma unroll
             for (int r = 0; r < R0; ++r) v[t][r] = vmul(v[t][r], hreg[t][r]);
         }
-        shg_store<R0, true, NB0, SH, K2_THREADS, M, 1>(v, rs, rows, StoreLds<V>{L});
+        shg_store<R0, true, NB0, SH, K2_THREADS, M, 1, XZ>(v, rs, rows, StoreLds<V>{L});
         __syncthreads();
     }
-    shg_pass<R1, true, NB1, SH, K2_THREADS, M, NS1, CMP>(L, rs, rows, twI, StoreLds<V>{L});
+    shg_pass<R1, true, NB1, SH, K2_THREADS, M, NS1, CMP, XZ>(L, rs, rows, twI, StoreLds<V>{L});
     const int gend = min(sd.gb, g0 + sd.V);
     {
         V v[NB0][R0];
