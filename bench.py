@@ -8,7 +8,7 @@ frame cubes (ring > 256 MiB Infinity Cache, so every step reads its cube from HB
 One step = one batch of ``--fpl`` distinct frames (one launch of each kernel) through
 DBF -> MTD -> pulse compression -> GOCA-CFAR -> S9 estimation (device) -> S10/S11
 clustering (host); batches rotate over the plan's lanes (3 HIP streams).  Warm-up
-always runs at least 20 batches (every lane, settled clocks) whatever ``--warmup`` says.
+always runs at least WARM_MIN = 100 batches (every lane, settled clocks) whatever ``--warmup`` says.
 ``value`` is frames/s = steps x fpl / time; inside the timed region the frames are
 queued with one C call and every frame's final targets come back as packed rows.
 
@@ -34,6 +34,9 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 NLANES = 3              # streams of the plan's throughput queue (rsp_plan.cpp)
+# untimed warm-up floor in batches (~55 ms at x2): a 20-step timed region after 20 warm-up batches ran
+# 11.7-11.9 ms, after 60 or 200 batches 11.4 ms on the same box (the GPU's clocks still ramping)
+WARM_MIN = 100
 
 
 def host_cpu():
@@ -283,7 +286,7 @@ def main():
             cube[...] = plan.device_download(p, cube.size, plan.cdtype).reshape(cube.shape, order='F')
             hring.append(h)
 
-    nfr = max(a.warmup, 2 * NLANES, 20, a.steps) * a.fpl   # the queue's argument lists, built before timing
+    nfr = max(a.warmup, 2 * NLANES, WARM_MIN, a.steps) * a.fpl   # the queue's argument lists, built before timing
     seq_cubes = [ring[i % len(ring)] for i in range(nfr)]
 
     def run(nbatches, base):   # nbatches full batches of fpl frames
@@ -299,9 +302,9 @@ def main():
         plan.enqueue_many(ring, range(1 + f0, 1 + f0 + len(ring)))
         plan.drain()
 
-    # warm-up: every lane (stream) with full batches, and >= 20 batches (~12 ms) so that the clocks
-    # have settled before the timed region, whatever --warmup says
-    run(max(a.warmup, 2 * NLANES, 20), 0)
+    # warm-up: every lane (stream) with full batches, and >= WARM_MIN batches so that the clocks
+    # and power state have settled before the timed region, whatever --warmup says
+    run(max(a.warmup, 2 * NLANES, WARM_MIN), 0)
     plan.results_rows(clear=True)
 
     if dist is not None:
