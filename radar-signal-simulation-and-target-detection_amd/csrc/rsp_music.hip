@@ -750,9 +750,11 @@ int32_t rsp_music_create(const rsp_music_config* cfg, int32_t device, rsp_music_
         }
     if (hipMemcpy(p->d_S1T, s1.data(), s1.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess)
         return bail(rsp_set_error(RSP_ERR_DEVICE, "steering upload failed"));
+#ifdef RSP_DEBUG_KNOBS   // diagnostic builds only: the shipped library reads no environment variable
     const char* tr = getenv("RSP_MUSIC_TRACE");
     if (tr && atoi(tr) && hipMalloc(&p->d_trace, B * 8 * sizeof(unsigned long long)) != hipSuccess)
         return bail(rsp_set_error(RSP_ERR_NOMEM, "trace buffer"));
+#endif
     *out = p;
     return RSP_OK;
 }
