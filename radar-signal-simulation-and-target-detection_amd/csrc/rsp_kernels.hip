@@ -1378,6 +1378,9 @@ __device__ __forceinline__ void s9_estimate(const DevConsts& k, const T* S, int 
 #ifndef K3_VEC
 #define K3_VEC 12   // 16-B loads per beam per thread in flight
 #endif
+#ifndef RSP_K3_PREFILTER
+#define RSP_K3_PREFILTER 1   // exact left-slice prefilter before the full GOCA test (0: A/B builds)
+#endif
 
 constexpr int floor4(int x) { return x >= 0 ? (x & ~3) : -((-x + 3) & ~3); }
 
@@ -1561,6 +1564,51 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
         // every ds_read_b128 on disjoint banks (2-way conflicted with 64-cell rows)
         const int rgp = lgT == 4 ? (rg & ~3) | ((rg & 1) << 1) | ((rg >> 1) & 1)
                                  : 2 * (rg >> 2) + ((rg & 1) << 4) + ((rg >> 1) & 1);
+#if RSP_K3_PREFILTER
+        // Exact prefilter.  A hit needs CUT > T mean(max of the four slices) >= T mean(left range
+        // slice): quot() is the correctly rounded (double) or a monotone (float) quotient and the
+        // product with T > 0 rounds monotonically, so a cell with CUT <= T quot(lr) cannot be a
+        // hit.  That test needs the left range slice alone (4 of the 27 ld4 per 4 cells: the CFAR
+        // phase was bound by LDS bandwidth); the rare survivors (T = 8 on amplitude sums: cells
+        // near targets) run the full test below with the same sums in the same order, so the
+        // detection list is the one the full test gives.  A NaN sum never rejects (the
+        // comparison is false).
+        if (Tc > 0.0) {
+            const T Tt = (T)Tc;
+#pragma unroll 1
+            for (int v = v0 + rgp; v < v1; v += RSP_THREADS >> lgT) {
+                const T* row = Sv + v * WC + c;
+                T xl[4 * NL], cv[4];
+#pragma unroll
+                for (int j = 0; j < NL; ++j) {
+                    T t[4];
+                    ld4(row + BL + 4 * j, t);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) xl[4 * j + i] = t[i];
+                }
+                ld4(row, cv);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    T lr = 0;
+#pragma unroll
+                    for (int qq = 0; qq < RR; ++qq) lr += xl[i + DL - BL + qq];
+                    const int ri = r + i;
+                    if (ri >= cut_lo && ri < cut_hi && !(cv[i] <= Tt * quot(lr, fR, iR))) {
+                        const T* cp = row + i;
+                        T tr = 0, lv = 0, tv = 0;
+#pragma unroll
+                        for (int qq = 0; qq < RR; ++qq) tr += cp[DR + qq];
+#pragma unroll
+                        for (int qq = 0; qq < RV; ++qq) {
+                            lv += cp[(qq - GV - RV) * WC];
+                            tv += cp[(qq + GV + 1) * WC];
+                        }
+                        K3_HIT(v, c + i, cv[i], lr, tr, lv, tv);
+                    }
+                }
+            }
+        } else
+#endif
 #pragma unroll 1
         for (int v = v0 + rgp; v < v1; v += RSP_THREADS >> lgT) {
             const T* row = Sv + v * WC + c;
