@@ -118,6 +118,14 @@ struct Geometry {
     K2Job jobs[RSP_MAX_JOBS];
 };
 
+// K3's compile-time path: the reference's cfar_params (v8:45-46) and a 32/64-cell tile
+__host__ __device__ inline bool k3_fast_params(const Geometry& g) {
+    return g.refR == 5 && g.refV == 5 && g.guardR == 10 && g.guardV == 10 && (g.cfar_RT == 32 || g.cfar_RT == 64);
+}
+#ifndef RSP_K3_NOHALO
+#define RSP_K3_NOHALO 1   // fast-path K3 tiles without the right range halo and the Doppler halo rows
+#endif
+
 // K3 tiles: range cells from the first cell under test rounded down to 4, cfar_RT per tile
 // (k3_cfar, launch_k3, rsp_profile_stages).
 __host__ __device__ inline int k3_ntiles(const Geometry& g) {

@@ -1339,19 +1339,18 @@ __device__ __forceinline__ double spline_peak(const double* y, int n) {
 }
 
 // S9 of one detection from the workgroup's S tile (fsf:237-290).
-template <class T>
-__device__ __forceinline__ void s9_estimate(const DevConsts& k, const T* S, int W, int c0, int P, int G, int Gp, int v,
-                                            int r, int pair, const T* __restrict__ MA, const T* __restrict__ MB,
-                                            DevDet* out) {
-    const int c = r - c0;
+// sval(v, r) = S at Doppler row v, range cell r (the tile, or the maps when the tile lacks it).
+template <class T, class SF>
+__device__ __forceinline__ void s9_estimate(const DevConsts& k, SF sval, int P, int G, int Gp, int v, int r, int pair,
+                                            const T* __restrict__ MA, const T* __restrict__ MB, DevDet* out) {
     // the 5-cell windows clipped to the map (fsf:241-250): cells first .. first + n - 1
     const int rfirst = max(r - 2, 0), nrc = min(r + 2, G - 1) - rfirst + 1;
     const int vfirst = max(v - 2, 0), nvc = min(v + 2, P - 1) - vfirst + 1;
     double yr[5], yv[5];
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
-        yr[j] = j < nrc ? (double)S[v * W + (rfirst - c0) + j] : 0.0;
-        yv[j] = j < nvc ? (double)S[(vfirst + j) * W + c] : 0.0;
+        yr[j] = j < nrc ? (double)sval(v, rfirst + j) : 0.0;
+        yv[j] = j < nvc ? (double)sval(vfirst + j, r) : 0.0;
     }
     const double rmax = (nrc < 3) ? (double)r : rfirst + spline_peak<8>(yr, nrc);
     const double vmax = (nvc < 3) ? (double)v : vfirst + spline_peak<4>(yv, nvc);
@@ -1364,7 +1363,7 @@ __device__ __forceinline__ void s9_estimate(const DevConsts& k, const T* S, int 
     d.r_idx = r + 1;
     d.pair_idx = pair + 1;
     d.reserved = 0;
-    d.amp = (double)S[v * W + c];
+    d.amp = (double)sval(v, r);
     d.range = k.range_axis[r] + (rmax - r) * k.deltaR;
     d.velocity = k.velocity_axis[v] + (vmax - v) * k.deltaV;
     d.angle = 0.5 * (k.beam_angles[pair] + k.beam_angles[pair + 1]) + k.klut[pair] * ratio;
@@ -1412,7 +1411,11 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
     constexpr int HRC = ((RR + GR > 2 ? RR + GR : 2) + 3) & ~3;   // = g.cfar_hR (rsp_plan.cpp)
     // = g.cfar_W; complex double rows get 2 extra cells (stride 132 dwords = 4 mod 64 banks), see
     // the row-group order of the CFAR loop
-    constexpr int WC = ((RTC + 2 * HRC + 3) & ~3) + (sizeof(T) == 8 ? 2 : 0);
+    // NOH (RSP_K3_NOHALO, fast path): the tile holds the left range halo and the band's own rows
+    // only; the prefilter needs no more, survivors and S9 read the rest from the maps
+    constexpr bool NOH = FAST && RSP_K3_NOHALO;
+    static_assert(!NOH || RSP_K3_PREFILTER, "halo-less K3 tiles need the prefilter path");
+    constexpr int WC = ((RTC + (NOH ? 1 : 2) * HRC + 3) & ~3) + (sizeof(T) == 8 ? 2 : 0);
     // XCD-aware order (bijective swizzle, cdna_hip_programming.md T1): the workgroups that
     // share an XCD take consecutive (tile, pair) ids with pairs fastest, so beam b's tile --
     // read by pairs b-1 and b -- and the range halos of neighbouring tiles are L2 hits
@@ -1435,13 +1438,18 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
     // band plus the rV + gV window rows on each side; bands of one tile column tile the map)
     const int hV = rV + gV;
     const int v0 = hV + band * g.cfar_VB, v1 = min(hV + (band + 1) * g.cfar_VB, P - hV);
-    const int vt0 = max(v0 - hV, 0), vt1 = min(v1 + hV, P), nv = vt1 - vt0;
+    const int vt0 = NOH ? v0 : max(v0 - hV, 0), vt1 = NOH ? max(v1, v0) : min(v1 + hV, P), nv = vt1 - vt0;
     int* queue = reinterpret_cast<int*>(S + g.cfar_rows * W);
     int* qn = queue + K3_QCAP;
     const T* Sv = S - vt0 * W;                         // row v of the map at Sv + v W
     const int Gp = g.Gp;
     const T* __restrict__ MA = static_cast<const T*>(fp.mag[f]) + (size_t)pair * P * Gp;   // |RDM| of beams pair, pair+1
     const T* __restrict__ MB = MA + (size_t)P * Gp;
+    // S(v, r) from the maps: the same two values and the same add as the tile load below
+    auto sg = [&](int vv, int rr) -> T {
+        const size_t o = (size_t)vv * Gp + rr;
+        return MA[o] + MB[o];
+    };
     if (threadIdx.x == 0) qn[0] = 0;
     // ---- load S = |A| + |B| (fsf:184-187) from the magnitude maps: 16 B per lane,
     //      K3_VEC units of each beam in flight per thread
@@ -1507,7 +1515,7 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
         const int nwc = whi - wlo;
         for (int e = threadIdx.x; e < (vhi - vlo) * nwc; e += RSP_THREADS) {
             const int v = vlo + e / nwc, r = wlo + (e - (v - vlo) * nwc);
-            sm[(size_t)v * G + r] = Sv[v * W + (r - c0)];
+            sm[(size_t)v * G + r] = NOH ? sg(v, r) : Sv[v * W + (r - c0)];
         }
     }
     if (v1 <= v0 || cut_hi <= cut_lo || (RSP_K3_ABLATE & 1)) return;
@@ -1573,8 +1581,9 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
         // near targets) run the full test below with the same sums in the same order, so the
         // detection list is the one the full test gives.  A NaN sum never rejects (the
         // comparison is false).
-        if (Tc > 0.0) {
+        if (NOH || Tc > 0.0) {
             const T Tt = (T)Tc;
+            const bool pf = Tc > 0.0;   // the bound needs T > 0; otherwise every cell takes the full test
 #pragma unroll 1
             for (int v = v0 + rgp; v < v1; v += RSP_THREADS >> lgT) {
                 const T* row = Sv + v * WC + c;
@@ -1593,15 +1602,23 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
 #pragma unroll
                     for (int qq = 0; qq < RR; ++qq) lr += xl[i + DL - BL + qq];
                     const int ri = r + i;
-                    if (ri >= cut_lo && ri < cut_hi && !(cv[i] <= Tt * quot(lr, fR, iR))) {
-                        const T* cp = row + i;
+                    if (ri >= cut_lo && ri < cut_hi && (!pf || !(cv[i] <= Tt * quot(lr, fR, iR)))) {
                         T tr = 0, lv = 0, tv = 0;
+                        if constexpr (NOH) {
+                            for (int qq = 0; qq < RR; ++qq) tr += sg(v, ri + DR + qq);
+                            for (int qq = 0; qq < RV; ++qq) {
+                                lv += sg(v + qq - GV - RV, ri);
+                                tv += sg(v + qq + GV + 1, ri);
+                            }
+                        } else {
+                            const T* cp = row + i;
 #pragma unroll
-                        for (int qq = 0; qq < RR; ++qq) tr += cp[DR + qq];
+                            for (int qq = 0; qq < RR; ++qq) tr += cp[DR + qq];
 #pragma unroll
-                        for (int qq = 0; qq < RV; ++qq) {
-                            lv += cp[(qq - GV - RV) * WC];
-                            tv += cp[(qq + GV + 1) * WC];
+                            for (int qq = 0; qq < RV; ++qq) {
+                                lv += cp[(qq - GV - RV) * WC];
+                                tv += cp[(qq + GV + 1) * WC];
+                            }
                         }
                         K3_HIT(v, c + i, cv[i], lr, tr, lv, tv);
                     }
@@ -1692,7 +1709,11 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
         if (idx >= g.max_dets) break;
         const int e = queue[i];
         const int v = e >> 16, c = e & 0xFFFF;
-        s9_estimate<T>(k, Sv, W, c0, P, G, Gp, v, c0 + c, pair, MA, MB, &fp.dets[f][idx]);
+        if constexpr (NOH)
+            s9_estimate<T>(k, sg, P, G, Gp, v, c0 + c, pair, MA, MB, &fp.dets[f][idx]);
+        else
+            s9_estimate<T>(k, [&](int vv, int rr) -> T { return Sv[vv * W + (rr - c0)]; }, P, G, Gp, v, c0 + c, pair,
+                           MA, MB, &fp.dets[f][idx]);
     }
 }
 
@@ -1890,7 +1911,7 @@ static hipError_t launch_k3_p(const Geometry& g, const DevConsts& k, const Frame
     const size_t lds = (size_t)g.cfar_rows * g.cfar_W * sizeof(T) + (K3_QCAP + 4) * sizeof(int);
     const dim3 grid(k3_ntiles(g) * g.cfar_nband * (g.B - 1) * nf);   // 1-D; k3_cfar remaps it XCD-aware
     hipError_t e;
-    const bool ref = g.refR == 5 && g.refV == 5 && g.guardR == 10 && g.guardV == 10;   // the reference's cfar_params (v8:45-46)
+    const bool ref = k3_fast_params(g);   // the reference's cfar_params (v8:45-46); the plan sized the tile for it
     if (ref && g.cfar_RT == 64) {
         if ((e = allow_lds(k3_cfar<T, 5, 5, 10, 10, 64>, lds)) != hipSuccess) return e;
         hipLaunchKernelGGL((k3_cfar<T, 5, 5, 10, 10, 64>), grid, dim3(RSP_THREADS), lds, s, g, k, fp);

@@ -447,6 +447,9 @@ FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const void* const* in, int
 #ifndef RSP_K3_TILE_KB
 #define RSP_K3_TILE_KB 48   // KB of S per K3 tile (48: 2 Doppler bands at P = 128, 3 workgroups per CU)
 #endif
+#ifndef RSP_K3_RT_C128
+#define RSP_K3_RT_C128 32   // K3 tile width in range cells, complex double (32 or 64)
+#endif
 #ifndef RSP_K12_SUB
 #define RSP_K12_SUB 0
 #endif
@@ -911,16 +914,22 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
     // Doppler rows, <= RSP_K3_TILE_KB of S per tile (48 KB: 3 workgroups per CU; at P = 128 two
     // bands measured 78 vs 85 us per 8 x2 frames for one band at 2 workgroups per CU): at P = 128 one band holds every row; longer P (x4's 256)
     // splits the rows into bands, each with the rV + gV window rows on either side
-    g.cfar_RT = p->rsz == 4 ? 64 : 32;
+    g.cfar_RT = p->rsz == 4 ? 64 : RSP_K3_RT_C128;
     // LDS row stride, 16-B aligned; complex double + 2 cells (bank spread, k3_cfar)
-    g.cfar_W = ((g.cfar_RT + 2 * g.cfar_hR + 3) & ~3) + (p->rsz == 8 ? 2 : 0);
+    // k3_cfar's compile-time path (the reference's 5/5/10/10) with RSP_K3_NOHALO holds only the
+    // left range halo and the band's own rows (its prefilter reads the left range slice; the
+    // rare survivors and S9 read the other windows from the magnitude maps)
+    const bool k3_nohalo = RSP_K3_NOHALO && k3_fast_params(g);
+    const int hx = k3_nohalo ? 1 : 2;
+    g.cfar_W = ((g.cfar_RT + hx * g.cfar_hR + 3) & ~3) + (p->rsz == 8 ? 2 : 0);
     {
         const int hV = g.refV + g.guardV, ncut = std::max(P - 2 * hV, 1);
+        const int hrows = k3_nohalo ? 0 : 2 * hV;
         const int rows_max = (int)((RSP_K3_TILE_KB * 1024) / ((size_t)g.cfar_W * p->rsz));
-        if (rows_max - 2 * hV < 1) return bail(fail(RSP_ERR_UNSUPPORTED, "CFAR window %d x %d exceeds the LDS tile", hV, g.cfar_hR));
-        g.cfar_nband = (ncut + rows_max - 2 * hV - 1) / (rows_max - 2 * hV);
+        if (rows_max - hrows < 1) return bail(fail(RSP_ERR_UNSUPPORTED, "CFAR window %d x %d exceeds the LDS tile", hV, g.cfar_hR));
+        g.cfar_nband = (ncut + rows_max - hrows - 1) / (rows_max - hrows);
         g.cfar_VB = (ncut + g.cfar_nband - 1) / g.cfar_nband;
-        g.cfar_rows = std::min(P, g.cfar_VB + 2 * hV);
+        g.cfar_rows = std::min(P, g.cfar_VB + hrows);
     }
 
     // ---- constants to the device, in the plan's precision
