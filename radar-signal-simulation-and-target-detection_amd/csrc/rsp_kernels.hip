@@ -1411,11 +1411,12 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
     constexpr int HRC = ((RR + GR > 2 ? RR + GR : 2) + 3) & ~3;   // = g.cfar_hR (rsp_plan.cpp)
     // = g.cfar_W; complex double rows get 2 extra cells (stride 132 dwords = 4 mod 64 banks), see
     // the row-group order of the CFAR loop
-    // NOH (RSP_K3_NOHALO, fast path): the tile holds the left range halo and the band's own rows
-    // only; the prefilter needs no more, survivors and S9 read the rest from the maps
+    // NOH (RSP_K3_NOHALO, fast path): the tile holds the band's own cells only, no halo; the
+    // prefilter takes whichever range slice lies inside the tile, survivors and S9 read the rest
+    // from the maps
     constexpr bool NOH = FAST && RSP_K3_NOHALO;
     static_assert(!NOH || RSP_K3_PREFILTER, "halo-less K3 tiles need the prefilter path");
-    constexpr int WC = ((RTC + (NOH ? 1 : 2) * HRC + 3) & ~3) + (sizeof(T) == 8 ? 2 : 0);
+    constexpr int WC = ((RTC + (NOH ? 0 : 2) * HRC + 3) & ~3) + (sizeof(T) == 8 ? 2 : 0);
     // XCD-aware order (bijective swizzle, cdna_hip_programming.md T1): the workgroups that
     // share an XCD take consecutive (tile, pair) ids with pairs fastest, so beam b's tile --
     // read by pairs b-1 and b -- and the range halos of neighbouring tiles are L2 hits
@@ -1432,7 +1433,7 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
     const int rR = RR ? RR : g.refR, gR = GR ? GR : g.guardR, rV = RV ? RV : g.refV, gV = GV ? GV : g.guardV;
     const int rc0 = rR + gR;                           // first cell under test (0-based)
     const int tstart = (rc0 & ~3) + tile * RT;         // multiple of 4
-    const int c0 = tstart - hR;                        // tile column 0 (multiple of 4; may be < 0)
+    const int c0 = tstart - (NOH ? 0 : hR);            // tile column 0 (multiple of 4; may be < 0)
     const int cut_lo = max(tstart, rc0), cut_hi = min(tstart + RT, G - rc0);
     // Doppler band: cells under test in rows [v0, v1), the tile holds rows [vt0, vt1) (the
     // band plus the rV + gV window rows on each side; bands of one tile column tile the map)
@@ -1560,7 +1561,7 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
         constexpr int NL = (DL + 3 + RR - BL + 3) / 4, NR = (DR + 3 + RR - BR + 3) / 4;
         constexpr int lgT = RTC == 64 ? 4 : 3;                    // log2 threads per row (RT / 4)
         const int q = threadIdx.x & ((1 << lgT) - 1);
-        const int c = hR + 4 * q;                                 // first tile column of the group
+        const int c = (NOH ? 0 : hR) + 4 * q;                     // first tile column of the group
         const int r = c0 + c;
         // 16-lane row groups of a wave take rows {0, 2, 1, 3} + 4w: the ds_read_b128 lane groups
         // ({0-3,12-15,20-27}, ... MI355X_MICROARCH.md §LDS) then pair rows 2 apart, 2W = 192
@@ -1584,6 +1585,15 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
         if (NOH || Tc > 0.0) {
             const T Tt = (T)Tc;
             const bool pf = Tc > 0.0;   // the bound needs T > 0; otherwise every cell takes the full test
+            // NOH: lanes whose 4 cells start in the first 16 tile columns test the right range
+            // slice (cells c + 11 .. c + 15 + 3 <= 30 < RT), the others the left one (c - 15 >= 1):
+            // either is a lower bound of the max.  The right slice's loads start at c + OR so
+            // that both slices sit at the same register offsets when the alignment allows (ld4 of
+            // double: 2 cells; of float: 4 cells, so float selects between offsets 1 and 3)
+            static_assert(!NOH || (RR == 5 && GR == 10 && NL == 3 && BL == -16), "NOH constants for the 5/10 window");
+            constexpr int OR = sizeof(T) == 8 ? 10 : 8, XR = DR - OR;   // XR: register offset of the right slice
+            const bool useR = NOH && q < 4;
+            const int base = useR ? OR : BL;
 #pragma unroll 1
             for (int v = v0 + rgp; v < v1; v += RSP_THREADS >> lgT) {
                 const T* row = Sv + v * WC + c;
@@ -1591,20 +1601,26 @@ __global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts 
 #pragma unroll
                 for (int j = 0; j < NL; ++j) {
                     T t[4];
-                    ld4(row + BL + 4 * j, t);
+                    ld4(row + base + 4 * j, t);
 #pragma unroll
                     for (int i = 0; i < 4; ++i) xl[4 * j + i] = t[i];
                 }
                 ld4(row, cv);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    T lr = 0;
+                    T lr = 0;   // NOH: the left or the right slice sum (a lower bound either way)
 #pragma unroll
-                    for (int qq = 0; qq < RR; ++qq) lr += xl[i + DL - BL + qq];
+                    for (int qq = 0; qq < RR; ++qq) {
+                        const T xa = xl[i + DL - BL + qq];
+                        if constexpr (NOH && XR != DL - BL) lr += useR ? xl[i + XR + qq] : xa;
+                        else lr += xa;
+                    }
                     const int ri = r + i;
                     if (ri >= cut_lo && ri < cut_hi && (!pf || !(cv[i] <= Tt * quot(lr, fR, iR)))) {
                         T tr = 0, lv = 0, tv = 0;
-                        if constexpr (NOH) {
+                        if constexpr (NOH) {   // every slice from the maps, in sum() order
+                            lr = 0;
+                            for (int qq = 0; qq < RR; ++qq) lr += sg(v, ri + DL + qq);
                             for (int qq = 0; qq < RR; ++qq) tr += sg(v, ri + DR + qq);
                             for (int qq = 0; qq < RV; ++qq) {
                                 lv += sg(v + qq - GV - RV, ri);

@@ -917,10 +917,10 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
     g.cfar_RT = p->rsz == 4 ? 64 : RSP_K3_RT_C128;
     // LDS row stride, 16-B aligned; complex double + 2 cells (bank spread, k3_cfar)
     // k3_cfar's compile-time path (the reference's 5/5/10/10) with RSP_K3_NOHALO holds only the
-    // left range halo and the band's own rows (its prefilter reads the left range slice; the
-    // rare survivors and S9 read the other windows from the magnitude maps)
+    // band's own cells (its prefilter reads whichever range slice lies in the tile; the rare
+    // survivors and S9 read the windows from the magnitude maps)
     const bool k3_nohalo = RSP_K3_NOHALO && k3_fast_params(g);
-    const int hx = k3_nohalo ? 1 : 2;
+    const int hx = k3_nohalo ? 0 : 2;
     g.cfar_W = ((g.cfar_RT + hx * g.cfar_hR + 3) & ~3) + (p->rsz == 8 ? 2 : 0);
     {
         const int hV = g.refV + g.guardV, ncut = std::max(P - 2 * hV, 1);
