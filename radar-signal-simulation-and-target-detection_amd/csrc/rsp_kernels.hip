@@ -1375,7 +1375,10 @@ __device__ __forceinline__ void s9_estimate(const DevConsts& k, SF sval, int P, 
 #define RSP_K3_ABLATE 0   // timing ablations (A/B builds only): 1 = no CFAR, 2 = no map loads
 #endif
 #ifndef K3_VEC
-#define K3_VEC 12   // 16-B loads per beam per thread in flight
+#define K3_VEC 8   // 16-B loads per beam per thread in flight (halo-less 98-row tiles: 8 -> 120 rows per sweep; 12 measured 43.7 vs 36.8 us)
+#endif
+#ifndef RSP_K3_WGS
+#define RSP_K3_WGS 3   // k3_cfar workgroups per CU the register budget is sized for
 #endif
 #ifndef RSP_K3_PREFILTER
 #define RSP_K3_PREFILTER 1   // exact left-slice prefilter before the full GOCA test (0: A/B builds)
@@ -1403,7 +1406,7 @@ template <> struct U16<double> { typedef d2 U; static constexpr int E = 2; };
 // range cells x all P Doppler cells of one beam pair, tile starts aligned to 4 cells so that
 // the magnitude rows load as 16-B units.
 template <class T, int RR, int RV, int GR, int GV, int RTC>
-__global__ __launch_bounds__(RSP_THREADS, 3) void k3_cfar(Geometry g, DevConsts k, FramePtrs fp) {
+__global__ __launch_bounds__(RSP_THREADS, RSP_K3_WGS) void k3_cfar(Geometry g, DevConsts k, FramePtrs fp) {
     T* S = reinterpret_cast<T*>(rsp_lds);   // [P][W] | queue[K3_QCAP] | qn, base
     typedef typename U16<T>::U U;
     constexpr int EPU = U16<T>::E;
