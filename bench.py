@@ -326,7 +326,8 @@ def main():
 
     # warm-up: every lane (stream) with full batches, and >= WARM_MIN batches so that the clocks
     # and power state have settled before the timed region, whatever --warmup says
-    run(max(a.warmup, 2 * NLANES, WARM_MIN), 0)
+    warm_batches = max(a.warmup, 2 * NLANES, WARM_MIN)
+    run(warm_batches, 0)
     plan.results_rows(clear=True)
 
     if dist is not None:
@@ -404,6 +405,7 @@ def main():
         out = {
             'metric': metric,
             'value': fps, 'unit': 'frames/s', 'n_gpus': world, 'steps': steps, 'warmup': a.warmup,
+            'warmup_effective': warm_batches,   # untimed batches that actually ran (>= WARM_MIN)
             'ms_per_step': el / steps * 1e3, 'higher_is_better': True,
             'scaling': 'strong' if a.frames_total else 'weak',
             'vs_baseline': None,
