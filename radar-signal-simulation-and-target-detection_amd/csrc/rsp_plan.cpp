@@ -1198,7 +1198,14 @@ int32_t rsp_process_targets_multi(rsp_plan* const* plans, int32_t n_plans, const
             return RSP_OK;
         };
         work[i].rc = body();
-        if (work[i].rc) work[i].err = rsp_last_error();
+        if (work[i].rc) {
+            // leave the plan reusable: finish what was queued, then drop the partial share
+            work[i].err = rsp_last_error();
+            (void)drain_all(p);
+            p->npend = 0;
+            p->results.clear();
+            p->overflow_seen = false;
+        }
     };
     std::vector<std::thread> th;
     for (int i = 1; i < n_plans; ++i) th.emplace_back(run, i);
@@ -1307,6 +1314,9 @@ int32_t rsp_process_stage2_gated(rsp_plan* p, const void* iq, int32_t dtype, int
         if (c[2 * k] < 1 || c[2 * k + 1] < c[2 * k] || c[2 * k + 1] > N)
             return fail(RSP_ERR_INVALID, "gate columns %d..%d of segment %d outside the %d-sample PRT", c[2 * k],
                         c[2 * k + 1], k, N);
+        if (k > 0 && c[2 * k] <= c[2 * k - 1])   // ascending and disjoint, like v2:257-264
+            return fail(RSP_ERR_INVALID, "gate columns of segment %d (%d..%d) overlap or precede segment %d (..%d)", k,
+                        c[2 * k], c[2 * k + 1], k - 1, c[2 * k - 1]);
         total += c[2 * k + 1] - c[2 * k] + 1;
     }
     if (total != n_gated) return fail(RSP_ERR_INVALID, "gated input has %d columns, the gate columns cover %d", n_gated, total);

@@ -149,6 +149,27 @@ static void read_precomputed(const mxArray* pre, Inputs* in, int with_tx) {   /*
     p->k_slopes_LUT = real_arr(field(pre, "k_slopes_LUT"), &in->n_k);
     if ((int32_t)in->n_med != p->N_fft_med || (int32_t)in->n_long != p->N_fft_long)
         mexErrMsgIdAndTxt("radar:rsp", "MF_*_fft lengths differ from N_fft_*");
+    {   /* rsp_plan_create_ex copies fixed counts through these pointers: check every length
+           against config before the library reads them */
+        const mwSize N = (mwSize)in->cfg.point_PRT, P = (mwSize)in->cfg.prtNum, B = (mwSize)in->cfg.beam_num;
+        const mwSize C = (mwSize)in->cfg.channel_num, G = (mwSize)(p->N_total_gate > 0 ? p->N_total_gate : 0);
+        if (in->cfg.point_PRT < 1 || in->cfg.prtNum < 1 || in->cfg.beam_num < 1 || in->cfg.channel_num < 1)
+            mexErrMsgIdAndTxt("radar:rsp", "config sizes must be positive");
+        if (with_tx && in->n_tx < N)
+            mexErrMsgIdAndTxt("radar:rsp", "tx_pulse has %d entries, point_PRT is %d", (int)in->n_tx, (int)N);
+        if (in->n_win != P) mexErrMsgIdAndTxt("radar:rsp", "MTD_win has %d entries, prtNum is %d", (int)in->n_win, (int)P);
+        if (in->n_va != P)
+            mexErrMsgIdAndTxt("radar:rsp", "velocity_axis has %d entries, prtNum is %d", (int)in->n_va, (int)P);
+        if (in->n_ra != G)
+            mexErrMsgIdAndTxt("radar:rsp", "range_axis has %d entries, N_total_gate is %d", (int)in->n_ra, (int)G);
+        if (in->n_ang < B)
+            mexErrMsgIdAndTxt("radar:rsp", "beam_angles_deg has %d entries, beam_num is %d", (int)in->n_ang, (int)B);
+        if (B > 1 && in->n_k < B - 1)
+            mexErrMsgIdAndTxt("radar:rsp", "k_slopes_LUT has %d entries, beam_num - 1 is %d", (int)in->n_k, (int)(B - 1));
+        if (in->n_w != B * C)
+            mexErrMsgIdAndTxt("radar:rsp", "DBF_coeffs_data_C has %d entries, beam_num x channel_num is %d", (int)in->n_w,
+                              (int)(B * C));
+    }
 }
 
 static void read_opts(const mxArray* o, rsp_plan_options* opt, uint64_t* seed, int32_t cols[6], int* has_cols) {

@@ -19,7 +19,7 @@ import hashlib
 import numpy as np
 
 from .config import (named_config, make_config, default_cfar_params, default_cluster_params,
-                     v8_2_targets, evolve_targets, V8_FIR)
+                     v8_2_targets, evolve_targets, V8_FIR, stage2_config, debug_v3_config)
 from .precompute import precompute
 from .plan import Plan, process_targets_multi
 from ._abi import RspError
@@ -87,10 +87,10 @@ def fun_process_single_frame(targets, config, cfar_params, cluster_params, preco
 def _stage2_precompute(config):
     """precomputed_data for the stage-2 path built from ``config`` alone (the 3-argument call):
     waveform, matched filters, segment geometry and MTD window of v8:79-135; the DBF weights,
-    beam angles and K-LUT are not used by stage 2 and are zero."""
+    beam angles and K-LUT are not used by stage 2 and are zero.  ``config`` is already in the
+    v8 form (config.stage2_config)."""
     sc = config['Sig_Config']
-    B = int(config.get('mtd', {}).get('beam_num', sc['beam_num']))
-    C = int(sc['channel_num'])
+    B, C = int(sc['beam_num']), int(sc['channel_num'])
     return precompute(config, np.zeros((B, C), complex), np.zeros(B), np.zeros(max(B - 1, 0)), V8_FIR)
 
 
@@ -110,6 +110,7 @@ def process_stage2_mtd(iq_data, angle, config, precomputed_data=None, gate_cols=
     debug_simulated_data_processing_v2.m:259-405) is un-vendored; this backs it with the
     per-frame chain's own S6 pulse compression + S7 MTD (fsf:99-136).  ``precomputed_data``
     defaults to the one v8:79-135 builds from ``config``."""
+    config = stage2_config(config)   # the v3 debug script's config form too (point_PRT = 3404, no gaps / Array)
     if precomputed_data is None:
         precomputed_data = _stage2_precompute(config)
     p = _plan_for(config, default_cfar_params(), default_cluster_params(), precomputed_data, device, precision)

@@ -52,6 +52,47 @@ def make_config(*, prtNum, point_PRT=None, prt=None, channel_num, beam_num,
     return {'Sig_Config': sc, 'Array': {'element_spacing': element_spacing}}
 
 
+def debug_v3_config():
+    """The ``config`` of debug_simulated_data_processing_v3.m:55-106 (the caller of the 3-argument
+    process_stage2_mtd at :189), the fields the stage-2 path reads: a Sig_Config with
+    point_PRT = 3404 (the gated sample count of the v2 .mat frames), point_prt = [3404 228 723
+    2453], no gap_duration, no point_prt_segments and no Array, plus config.mtd.beam_num = 13."""
+    sc = dict(c=C_LIGHT, fs=25e6, fc=9450e6, prtNum=332, point_PRT=3404, channel_num=16, beam_num=13,
+              prt=232.76e-6, B=20e6, tao=[0.16e-6, 8e-6, 28e-6], point_prt=[3404, 228, 723, 2453])
+    sc['prf'] = 1 / sc['prt']
+    sc['wavelength'] = sc['c'] / sc['fc']
+    sc['deltaR'] = sc['c'] / (2 * sc['fs'])
+    mtd = dict(win_size=4, prtNum=sc['prtNum'], beam_num=sc['beam_num'], fs=sc['fs'], fc=sc['fc'], prt=sc['prt'],
+               B=sc['B'], tao=list(sc['tao']), point_prt=list(sc['point_prt']))
+    return {'Sig_Config': sc, 'mtd': mtd}
+
+
+def stage2_config(config):
+    """A v8-style ``config`` (make_config) for the stage-2 path from any caller's config.
+
+    process_stage2_mtd.m:1 is called from debug_simulated_data_processing_v3.m:189, whose config
+    (debug_v3_config) differs from the v8 drivers': point_PRT is the gated count 3404, the segment
+    gate counts are point_prt(2:4), and there is no gap_duration or Array.  The full PRT is
+    round(prt fs) (v8:68), B is config.mtd.beam_num when present (process_stage2_mtd.m:15),
+    the segment gate counts come from point_prt_segments or else point_prt(2:4), and the pulse
+    gaps from gap_duration or else the reference waveform's (v8:61: 11.4 / 31.8 / 153.4 us).
+    Array.element_spacing is not used by stage 2 (kept when given)."""
+    sc = config['Sig_Config']
+    fs = float(sc['fs'])
+    prt = float(sc['prt']) if 'prt' in sc else float(sc['point_PRT']) / fs
+    if 'point_prt_segments' in sc:
+        segs = [int(x) for x in sc['point_prt_segments']]
+    elif 'point_prt' in sc and len(sc['point_prt']) >= 4:
+        segs = [int(x) for x in list(sc['point_prt'])[1:4]]
+    else:
+        raise KeyError('config.Sig_Config needs point_prt_segments or point_prt = [total narrow medium long]')
+    B = int(config.get('mtd', {}).get('beam_num', sc['beam_num']))
+    d = config.get('Array', {}).get('element_spacing', 0.0138)
+    return make_config(prtNum=int(sc['prtNum']), prt=prt, channel_num=int(sc.get('channel_num', B)), beam_num=B,
+                       tao=tuple(sc['tao']), gap_duration=tuple(sc.get('gap_duration', (11.4e-6, 31.8e-6, 153.4e-6))),
+                       point_prt_segments=segs, fs=fs, fc=float(sc['fc']), B=float(sc['B']), element_spacing=d)
+
+
 def default_cfar_params():
     """v8:45-47."""
     return dict(refCells_V=5, guardCells_V=10, refCells_R=5, guardCells_R=10, T_CFAR=8.0, method='GOCA')

@@ -193,6 +193,15 @@ def test_process_stage2_mtd_dropin_reference_gated():
     pc_o = chain.pulse_compress(full, s['pre_o'])
     _map_close(pc, pc_o, MAP_TOL['c128'])
     _map_close(mtd, chain.mtd(pc_o, s['pre_o']), MAP_TOL['c128'])
+    # the caller's own config (debug_simulated_data_processing_v3.m:55-106: point_PRT = 3404 gated
+    # samples, point_prt = [3404 228 723 2453], no gap_duration / Array, config.mtd.beam_num)
+    # describes the same waveform and gating: identical results
+    mtd3, pc3 = rsp.process_stage2_mtd(gated, np.zeros(332), rsp.debug_v3_config())
+    np.testing.assert_array_equal(mtd3, mtd)
+    np.testing.assert_array_equal(pc3, pc)
+    # gate columns must be ascending and disjoint (v2:257-264)
+    with pytest.raises(rsp.RspError):
+        rsp.process_stage2_mtd(gated, np.zeros(332), s['cfg'], gate_cols=((83, 310), (300, 1022), (1023, 3475)))
 
 
 @pytest.mark.parametrize('prec', ['c128', 'c64'])

@@ -5,7 +5,10 @@ K3 rejects a cell when CUT <= T mean(left range slice) and runs the full GOCA te
 survives, so the default-threshold parity cases never exercise the full-test branch much.
 Here T is lowered until a large share of the cells survive the prefilter and many are hits;
 the device's detection list must still be the oracle's, cell for cell and in find() order
-(complex double).
+(complex double).  Complex single takes the other branch of the halo-less tiles (64-cell
+tiles, the right range slice read at a register offset that differs from the left one's): its
+list is checked against the oracle on the complex64-rounded cube, with decision flips allowed
+only at cells whose oracle margin is below 1e-4 (the test_gpu_parity rule).
 """
 import numpy as np
 import pytest
@@ -18,16 +21,25 @@ from _scen import scenario, targets_for, noisy_cube
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize('prec', ['c128', 'c64'])
 @pytest.mark.parametrize('name,T', [('small', 2.0), ('small', 3.0), ('x2', 3.0), ('x2', 4.0)])
-def test_low_threshold_detections_match_oracle(name, T):
+def test_low_threshold_detections_match_oracle(name, T, prec):
     s = scenario(name)
-    cube = noisy_cube(s, targets_for(name), dtype=np.complex128)
+    cube = noisy_cube(s, targets_for(name), dtype=np.complex128 if prec == 'c128' else np.complex64)
     cfar = dict(s['cfar'], T_CFAR=T)
-    _, st = chain.process_cube(cube, s['cfg'], cfar, s['clus'], s['pre_o'], keep=True)
-    plan = Plan(s['cfg'], cfar, s['clus'], s['pre_p'], precision='c128')
+    _, st = chain.process_cube(cube.astype(np.complex128), s['cfg'], cfar, s['clus'], s['pre_o'], keep=True)
+    plan = Plan(s['cfg'], cfar, s['clus'], s['pre_p'], precision=prec)
     gpu = plan.process_cube(cube, frame_idx=1)
     plan.close()
     want = [(int(d[0]), int(d[1]), int(d[2])) for d in st['dets']]
     got = [(d['v_idx'], d['r_idx'], d['pair_idx']) for d in gpu['detections']]
     assert len(want) > 100, 'threshold too high to exercise the full-test branch (%d hits)' % len(want)
-    assert got == want
+    if prec == 'c128':
+        assert got == want
+        return
+    assert got == sorted(got, key=lambda k: (k[2], k[1], k[0])), 'not in fsf find() order'
+    mg = chain.cfar_margin(st['rdm'], cfar)
+    flips = set(got) ^ set(want)
+    for (v, r, p) in flips:
+        assert mg[v - 1, r - 1, p - 1] < 1e-4, 'CFAR decision differs at (v=%d r=%d pair=%d)' % (v, r, p)
+    assert len(flips) <= max(2, 0.01 * len(want))

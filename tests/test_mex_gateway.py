@@ -44,3 +44,30 @@ def test_matlab_wrappers_keep_the_reference_signatures():
     s2 = open(os.path.join(d, 'process_stage2_mtd.m')).read()
     assert re.search(r'^function \[MTD_results, PC_results\] = process_stage2_mtd\(iq_data, angle, config\)', s2,
                      re.M)                                                           # process_stage2_mtd.m:1
+
+
+INTEGRATION = os.path.join(ROOT, 'INTEGRATION.md')
+
+
+@pytest.mark.skipif(shutil.which('gcc') is None, reason='needs gcc')
+def test_integration_c_snippets_compile(tmp_path):
+    """Every C block of INTEGRATION.md is a self-contained unit that compiles against include/rsp.h."""
+    blocks = re.findall(r'```c\n(.*?)```', open(INTEGRATION).read(), re.S)
+    assert len(blocks) >= 2
+    for i, b in enumerate(blocks):
+        f = tmp_path / ('snippet%d.c' % i)
+        f.write_text(b)
+        subprocess.run(['gcc', '-std=c99', '-fsyntax-only', '-Wall', '-Werror', '-I', os.path.join(ROOT, 'include'),
+                        str(f)], check=True)
+
+
+def test_integration_matlab_wrappers_match_committed_files():
+    """The MATLAB wrapper shown in INTEGRATION.md is the committed one, line for line (no stale copy)."""
+    doc = open(INTEGRATION).read()
+    d = os.path.dirname(MEX)
+    committed = open(os.path.join(d, 'fun_process_single_frame.m')).read()
+    block = [b for b in re.findall(r'```matlab\n(.*?)```', doc, re.S) if 'function final_targets' in b]
+    assert len(block) == 1
+    code = [ln for ln in committed.splitlines() if ln.strip() and not ln.lstrip().startswith('%')]
+    assert [ln for ln in block[0].splitlines() if ln.strip()] == code
+    assert 'persistent inited' not in doc and "rsp_mex('init'" not in doc
