@@ -47,7 +47,7 @@ typedef enum rsp_status {
     RSP_ERR_UNSUPPORTED = -2,  /* config outside what the kernels implement      */
     RSP_ERR_DEVICE = -3,       /* HIP runtime failure                            */
     RSP_ERR_NOMEM = -4,        /* device or host allocation failed               */
-    RSP_ERR_OVERFLOW = -5      /* detection list longer than the plan's capacity */
+    RSP_ERR_OVERFLOW = -5      /* a caller-sized output buffer is too small      */
 } rsp_status;
 
 typedef enum rsp_dtype {
@@ -143,7 +143,9 @@ typedef struct rsp_sizes {
     int64_t cfar_map_elems;   /* P*G*(B-1)                                  */
     int32_t P, N, C, B, G;
     int32_t used_samples;     /* fast-time samples the chain actually reads */
-    int32_t max_detections;   /* per frame device capacity                  */
+    int32_t max_detections;   /* most detections a frame can have (cells under
+                                 test of every beam pair); the device lists
+                                 start smaller and grow on demand           */
     int32_t n_stages;         /* device stages (for rsp_profile_stages)     */
     int32_t precision;        /* RSP_C128 or RSP_C64: device cube / map type */
     int32_t elem_bytes;       /* bytes of one device complex element (16/8) */
@@ -185,6 +187,15 @@ int32_t rsp_query_sizes(const rsp_plan* plan, rsp_sizes* out);
  * thresholds on the device (rdm_for_cfar_all, fsf:184-187). */
 int32_t rsp_process_cube(rsp_plan* plan, const void* cube, int32_t dtype, int32_t layout,
                          int32_t frame_idx, rsp_frame_out* out);
+
+/* Every detection of the last synchronous frame (rsp_process_cube / rsp_process_targets), in the
+ * reference's order.  A frame's list has no fixed capacity (all_raw_detections(end+1,:),
+ * fsf:215-221); a caller that passed out->dets == NULL or a dets_cap below out->n_dets reads the
+ * whole list here.  *n = its length; RSP_ERR_OVERFLOW if cap < *n (the first cap are copied). */
+int32_t rsp_last_detections(const rsp_plan* plan, rsp_detection* dets, int32_t cap, int32_t* n);
+/* The final targets of the last synchronous frame, likewise (for out->targets == NULL or a
+ * targets_cap below out->n_targets). */
+int32_t rsp_last_targets(const rsp_plan* plan, rsp_target* targets, int32_t cap, int32_t* n);
 
 /* Reference-signature path (fsf:13): S4 echo synthesis + S4.1 Philox noise
  * (seed, frame_idx) on the device, then S5..S11.  Needs tx_pulse in the plan. */

@@ -106,7 +106,7 @@ struct Geometry {
     int cfar_VB, cfar_nband, cfar_rows;   // K3 Doppler bands: cells under test per band, bands, tile rows
     int refR, guardR, refV, guardV;
     double T;        // T_CFAR
-    int max_dets;
+    int max_dets;    // detection-list capacity per frame of the launch (grows on demand, rsp_plan.cpp)
     int ncu;         // compute units of the device (persistent K1 grid)
     int k1_tiled;    // force the one-tile-per-workgroup K1 (RSP_PLAN_K1_TILED, parity tests)
     // used fast-time samples as <= RSP_MAX_IVL intervals: compacted n' in [ivl_start[q],
@@ -176,5 +176,8 @@ hipError_t launch_k3(const Geometry& g, const DevConsts& k, const FramePtrs& fp,
 hipError_t launch_mtd_cols(const Geometry& g, const DevConsts& k, const void* pc, void* rdm, hipStream_t s);
 hipError_t launch_synth(const Geometry& g, const double* tx, const SynthTarget* tg, int nt, int frame_idx,
                         uint64_t seed, double noise_scale, void* cube, hipStream_t s);
+// Queue read-back: count record + the detections of nf frames (device stride dcap + 1 records) into
+// mapped pinned host memory (stride hcap + 1), only the records that exist.
+hipError_t launch_dets_to_host(const void* dets, int dcap, void* host, int hcap, int nf, hipStream_t s);
 // K1 tile geometry the launcher will use (persistent or tiled) for the plan's NT choice
 bool k1_persistent_fits(const Geometry& g);

@@ -1338,10 +1338,17 @@ __device__ __forceinline__ double spline_peak(const double* y, int n) {
     return bx;
 }
 
+// The axes, angles and K-LUT S9 reads (DevConsts fields), by value so that the out-of-line
+// spill path below takes them in registers.
+struct S9Consts {
+    const double *range_axis, *velocity_axis, *beam_angles, *klut;
+    double deltaR, deltaV;
+};
+
 // S9 of one detection from the workgroup's S tile (fsf:237-290).
 // sval(v, r) = S at Doppler row v, range cell r (the tile, or the maps when the tile lacks it).
 template <class T, class SF>
-__device__ __forceinline__ void s9_estimate(const DevConsts& k, SF sval, int P, int G, int Gp, int v, int r, int pair,
+__device__ __forceinline__ void s9_estimate(const S9Consts& k, SF sval, int P, int G, int Gp, int v, int r, int pair,
                                             const T* __restrict__ MA, const T* __restrict__ MB, DevDet* out) {
     // the 5-cell windows clipped to the map (fsf:241-250): cells first .. first + n - 1
     const int rfirst = max(r - 2, 0), nrc = min(r + 2, G - 1) - rfirst + 1;
@@ -1371,6 +1378,25 @@ __device__ __forceinline__ void s9_estimate(const DevConsts& k, SF sval, int P, 
 }
 
 #define K3_QCAP 1024
+
+// A hit past the workgroup's LDS queue (more than K3_QCAP in one tile: a cluttered frame or a low
+// T_CFAR) reserves its slot in the frame's list itself and runs S9 in place, so the list holds
+// every hit like all_raw_detections(end+1, :) (fsf:215-221).  Slots at or past `cap` are counted
+// but not written: the host sees count > cap, grows the list and runs K3 again (rsp_plan.cpp).
+// Out of line: the common path keeps its registers.
+template <class T, bool NOH>
+__device__ __attribute__((noinline)) void k3_spill_hit(S9Consts k, const T* Sv, int W, int c0, int P, int G, int Gp,
+                                                      int v, int r, int pair, const T* MA, const T* MB, DevDet* dets,
+                                                      int* count, int cap) {
+    const int idx = atomicAdd(count, 1);
+    if (idx >= cap) return;
+    if constexpr (NOH)
+        s9_estimate<T>(k, [&](int vv, int rr) -> T { const size_t o = (size_t)vv * Gp + rr; return MA[o] + MB[o]; },
+                       P, G, Gp, v, r, pair, MA, MB, &dets[idx]);
+    else
+        s9_estimate<T>(k, [&](int vv, int rr) -> T { return Sv[vv * W + (rr - c0)]; }, P, G, Gp, v, r, pair, MA, MB,
+                       &dets[idx]);
+}
 #ifndef RSP_K3_ABLATE
 #define RSP_K3_ABLATE 0   // timing ablations (A/B builds only): 1 = no CFAR, 2 = no map loads
 #endif
@@ -1545,13 +1571,14 @@ __global__ __launch_bounds__(RSP_THREADS, RSP_K3_WGS) void k3_cfar(Geometry g, D
         const T nR = quot(fmax(lr, tr), fR, iR), nV = quot(fmax(lv, tv), fV, iV);
         return nR > nV ? nR : nV;
     };
-    bool overflow = false;
+    const S9Consts s9c{k.range_axis, k.velocity_axis, k.beam_angles, k.klut, k.deltaR, k.deltaV};
 #define K3_HIT(V, C, CUT, LR, TR, LV, TV)                                                               \
     do {                                                                                                \
         if ((CUT) > (T)Tc * noise2(LR, TR, LV, TV)) {                                                   \
             const int qi = atomicAdd(qn, 1);                                                            \
             if (qi < K3_QCAP) queue[qi] = ((V) << 16) | (C);                                            \
-            else overflow = true;                                                                       \
+            else k3_spill_hit<T, NOH>(s9c, Sv, W, c0, P, G, Gp, V, c0 + (C), pair, MA, MB, fp.dets[f],  \
+                                      fp.count[f], g.max_dets);                                         \
         }                                                                                               \
     } while (0)
     // ---- cross GOCA-CFAR (fsf:192-213); hits go to an LDS queue so that the S9 work is
@@ -1714,9 +1741,6 @@ __global__ __launch_bounds__(RSP_THREADS, RSP_K3_WGS) void k3_cfar(Geometry g, D
         }
     }
 #undef K3_HIT
-    // queue overflow (> K3_QCAP hits in one tile, a pathological detection density): the frame's
-    // count is pushed past the plan capacity so that the host reports RSP_ERR_OVERFLOW
-    if (overflow) atomicAdd(fp.count[f], g.max_dets + 1);
     __syncthreads();
     const int n = min(qn[0], K3_QCAP);
     if (n == 0) return;
@@ -1729,9 +1753,9 @@ __global__ __launch_bounds__(RSP_THREADS, RSP_K3_WGS) void k3_cfar(Geometry g, D
         const int e = queue[i];
         const int v = e >> 16, c = e & 0xFFFF;
         if constexpr (NOH)
-            s9_estimate<T>(k, sg, P, G, Gp, v, c0 + c, pair, MA, MB, &fp.dets[f][idx]);
+            s9_estimate<T>(s9c, sg, P, G, Gp, v, c0 + c, pair, MA, MB, &fp.dets[f][idx]);
         else
-            s9_estimate<T>(k, [&](int vv, int rr) -> T { return Sv[vv * W + (rr - c0)]; }, P, G, Gp, v, c0 + c, pair,
+            s9_estimate<T>(s9c, [&](int vv, int rr) -> T { return Sv[vv * W + (rr - c0)]; }, P, G, Gp, v, c0 + c, pair,
                            MA, MB, &fp.dets[f][idx]);
     }
 }
@@ -1834,7 +1858,32 @@ __global__ __launch_bounds__(RSP_THREADS) void k_synth(Geometry g, const double*
     cube[o] = cx<T>{(T)re, (T)im};
 }
 
+// ======================================================================================
+// Detection lists -> pinned host memory (the queue's read-back, after K3)
+// ======================================================================================
+// Frame f = blockIdx.x: record 0 (the count) and the first min(count, dcap, hcap) detections
+// from the device list (stride dcap + 1 records) into the mapped host list (stride hcap + 1), so
+// only the records that exist cross PCIe, whatever the count (a fixed-size async copy moved the
+// first 512 and left the rest to a synchronous tail copy).
+__global__ __launch_bounds__(RSP_THREADS) void k_dets_to_host(const DevDet* __restrict__ dets, int dcap,
+                                                             DevDet* __restrict__ host, int hcap) {
+    const int f = blockIdx.x;
+    const u32x4* src = reinterpret_cast<const u32x4*>(dets + (size_t)f * (dcap + 1));
+    u32x4* dst = reinterpret_cast<u32x4*>(host + (size_t)f * (hcap + 1));
+    const int cnt = *reinterpret_cast<const int*>(src);
+    const int n = 1 + min(cnt, min(dcap, hcap));   // records, the count record included
+    constexpr int U = sizeof(DevDet) / 16;        // 16-B units per record
+    for (int e = threadIdx.x; e < n * U; e += RSP_THREADS) dst[e] = src[e];
+}
+
 }  // namespace
+
+hipError_t launch_dets_to_host(const void* dets, int dcap, void* host, int hcap, int nf, hipStream_t s) {
+    static_assert(sizeof(DevDet) % 16 == 0, "16-B units");
+    hipLaunchKernelGGL(k_dets_to_host, dim3(nf), dim3(RSP_THREADS), 0, s, static_cast<const DevDet*>(dets), dcap,
+                       static_cast<DevDet*>(host), hcap);
+    return hipGetLastError();
+}
 
 // ---------------------------------------------------------------------------------------
 // Dynamic LDS above 64 KiB must be opted in per kernel (gfx950 has 160 KiB per CU).

@@ -150,8 +150,12 @@ struct Lane {
     void* z = nullptr;          // F frames
     void* rdm = nullptr;        // F frames
     void* mag = nullptr;        // F frames
-    DevDet* dets = nullptr;     // F x (1 + max_dets): record 0 of each frame holds its count
-    DevDet* h_dets = nullptr;   // pinned F x (1 + async_cap), same layout
+    DevDet* dets = nullptr;     // F x (1 + dcap): record 0 of each frame holds its count
+    int dcap = 0;               // device detection-list capacity per frame (grows on demand)
+    DevDet* h_dets = nullptr;   // mapped pinned F x (1 + hcap), same layout, written by k_dets_to_host
+    DevDet* h_dets_dev = nullptr;
+    int hcap = 0;               // host read-back capacity per frame (grows on demand)
+    FramePtrs fp{};             // the batch in flight (K3 runs again after a device-list growth)
     int nf = 0;
     int frame_ids[RSP_MAX_F];
     bool busy = false;
@@ -214,7 +218,6 @@ private:
 struct FrameResult {
     int frame_idx;
     int n_dets;
-    bool overflow;
     std::vector<rsp_target> targets;
 };
 
@@ -228,7 +231,7 @@ struct rsp_plan {
     double deltaR = 0, deltaV = 0;
     double p_signal_unscaled = 0, c = 0, fs = 0, wavelength = 0, d = 0, prt = 0;
     int F = 1;
-    int async_cap = 512;
+    int det_bound = 1;   // cells under test per frame: the most detections a frame can have
     size_t esz = 16;   // bytes of one complex element (16: complex128, 8: complex64)
     size_t rsz = 8;    // bytes of one real element
     size_t z_elems = 0, rdm_elems = 0, mag_elems = 0;
@@ -265,7 +268,8 @@ struct rsp_plan {
     std::vector<char> slot_used;
     int ring_next = 0;
     std::deque<FrameResult> results;   // deque: push_back keeps the elements the pool writes in place
-    bool overflow_seen = false;
+    std::vector<rsp_detection> last_dets;   // detections of the last synchronous frame (rsp_last_detections)
+    std::vector<rsp_target> last_targets;   // its final targets (rsp_last_targets)
     // clustering workers of the queue (created with the first batch of F > 1 frames); every
     // reader of `results` calls results_ready() first.  Declared after `results`: destroyed first.
     std::unique_ptr<ClusterPool> pool;
@@ -333,6 +337,7 @@ rsp_plan::~rsp_plan() {
     for (auto& L : lanes) {
         if (L.stream) (void)hipStreamSynchronize(L.stream);
         if (L.h_dets) (void)hipHostFree(L.h_dets);
+        if (L.dets) (void)hipFree(L.dets);
         if (L.done) (void)hipEventDestroy(L.done);
         for (auto& e : L.tev)
             if (e) (void)hipEventDestroy(e);
@@ -415,6 +420,35 @@ int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga,
     return RSP_OK;
 }
 
+// Device detection lists of a lane: F x (1 + cap) records (record 0 of a frame = its count).
+int lane_dets_alloc(rsp_plan* p, Lane& L, int cap) {
+    if (L.dets) HIPCHK(hipFree(L.dets));
+    L.dets = nullptr;
+    L.dcap = std::max(cap, 1);
+    if (hipMalloc((void**)&L.dets, sizeof(DevDet) * (size_t)(L.dcap + 1) * p->F) != hipSuccess)
+        return fail(RSP_ERR_NOMEM, "hipMalloc of %d-detection lists failed", L.dcap);
+    return RSP_OK;
+}
+
+// Mapped, coherent pinned read-back lists of a lane: F x (1 + cap) records, written by
+// k_dets_to_host over PCIe after K3 (only the records that exist).
+int lane_host_alloc(rsp_plan* p, Lane& L, int cap) {
+    if (L.h_dets) HIPCHK(hipHostFree(L.h_dets));
+    L.h_dets = L.h_dets_dev = nullptr;
+    L.hcap = std::max(cap, 1);
+    if (hipHostMalloc((void**)&L.h_dets, sizeof(DevDet) * (size_t)(L.hcap + 1) * p->F,
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        return fail(RSP_ERR_NOMEM, "pinned %d-detection read-back lists failed", L.hcap);
+    HIPCHK(hipHostGetDevicePointer((void**)&L.h_dets_dev, L.h_dets, 0));
+    return RSP_OK;
+}
+
+int pow2_at_least(int x) {
+    int c = 1;
+    while (c < x && c < (1 << 30)) c <<= 1;
+    return c;
+}
+
 int setup_lane(rsp_plan* p, Lane& L) {
     HIPCHK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&L.done, hipEventDisableTiming));
@@ -423,9 +457,8 @@ int setup_lane(rsp_plan* p, Lane& L) {
     if ((rc = p->dalloc_bytes(&L.z, p->z_elems * p->F * p->esz))) return rc;
     if ((rc = p->dalloc_bytes(&L.rdm, p->rdm_elems * p->F * p->esz))) return rc;
     if ((rc = p->dalloc_bytes(&L.mag, p->mag_elems * p->F * p->rsz))) return rc;
-    if ((rc = p->dalloc(&L.dets, (size_t)(p->g.max_dets + 1) * p->F))) return rc;
-    HIPCHK(hipHostMalloc((void**)&L.h_dets, sizeof(DevDet) * (p->async_cap + 1) * p->F, hipHostMallocDefault));
-    return RSP_OK;
+    if ((rc = lane_dets_alloc(p, L, std::min(p->det_bound, 4096)))) return rc;
+    return lane_host_alloc(p, L, std::min(p->det_bound, 1024));
 }
 
 FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const void* const* in, int nf) {
@@ -435,7 +468,7 @@ FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const void* const* in, int
         fp.z[f] = (char*)L.z + p->z_elems * p->esz * f;
         fp.rdm[f] = (char*)L.rdm + p->rdm_elems * p->esz * f;
         fp.mag[f] = (char*)L.mag + p->mag_elems * p->rsz * f;
-        DevDet* rec = L.dets + (size_t)(p->g.max_dets + 1) * f;
+        DevDet* rec = L.dets + (size_t)(L.dcap + 1) * f;
         fp.count[f] = reinterpret_cast<int*>(rec);   // zeroed by K1, bumped by K3
         fp.dets[f] = rec + 1;
     }
@@ -490,20 +523,25 @@ int launch_batch(rsp_plan* p, Lane& L, const void* const* in, const int* ids, in
     HIPCHK(launch_k2(p->g, p->k, fp, nf, p->g.B * p->g.P, L.stream));
     if (L.timed) HIPCHK(hipEventRecord(L.tev[2], L.stream));
 #endif
-    HIPCHK(launch_k3(p->g, p->k, fp, nf, L.stream));
+    Geometry g3 = p->g;
+    g3.max_dets = L.dcap;
+    HIPCHK(launch_k3(g3, p->k, fp, nf, L.stream));
     if (L.timed) HIPCHK(hipEventRecord(L.tev[3], L.stream));
-    // one copy: count record + the first async_cap detections of every frame
-    HIPCHK(hipMemcpy2DAsync(L.h_dets, sizeof(DevDet) * (p->async_cap + 1), L.dets,
-                            sizeof(DevDet) * (p->g.max_dets + 1), sizeof(DevDet) * (p->async_cap + 1), nf,
-                            hipMemcpyDeviceToHost, L.stream));
+    // every frame's count and detections into the lane's mapped pinned lists (only what exists)
+    HIPCHK(launch_dets_to_host(L.dets, L.dcap, L.h_dets_dev, L.hcap, nf, L.stream));
     HIPCHK(hipEventRecord(L.done, L.stream));
+    L.fp = fp;
     L.nf = nf;
     for (int f = 0; f < nf; ++f) L.frame_ids[f] = ids[f];
     L.busy = true;
     return RSP_OK;
 }
 
-// Wait for lane L, gather its detections (sync copy of any tail past async_cap) and cluster.
+// Wait for lane L, gather its detections and cluster.  The lists have no fixed capacity, like
+// all_raw_detections(end+1, :) (fsf:215-221): a frame with more detections than the lane's device
+// list grows the list and runs K3 again on the batch (its magnitude maps are still in the lane),
+// and a frame with more than the host read-back holds is copied directly once and the read-back
+// grown, so that later batches come back whole through k_dets_to_host.
 int harvest(rsp_plan* p, Lane& L, std::vector<std::vector<rsp_detection>>* keep_dets = nullptr) {
     if (!L.busy) return RSP_OK;
     HIPCHK(hipEventSynchronize(L.done));
@@ -517,23 +555,40 @@ int harvest(rsp_plan* p, Lane& L, std::vector<std::vector<rsp_detection>>* keep_
         p->stage_launches += 1;
         p->stage_frames += L.nf;
     }
+    int cnt[RSP_MAX_F], maxc = 0, rc;
+    for (int f = 0; f < L.nf; ++f) {
+        cnt[f] = *reinterpret_cast<const int*>(L.h_dets + (size_t)f * (L.hcap + 1));
+        maxc = std::max(maxc, cnt[f]);
+    }
+    const bool regrow = maxc > L.dcap;
+    if (regrow) {   // rare: grow the device lists, run K3 again with them, read back directly
+        if ((rc = lane_dets_alloc(p, L, std::min(p->det_bound, pow2_at_least(maxc))))) return rc;
+        FramePtrs fp = L.fp;
+        for (int f = 0; f < L.nf; ++f) {
+            DevDet* rec = L.dets + (size_t)(L.dcap + 1) * f;
+            fp.count[f] = reinterpret_cast<int*>(rec);
+            fp.dets[f] = rec + 1;
+        }
+        HIPCHK(hipMemset2DAsync(L.dets, sizeof(DevDet) * (L.dcap + 1), 0, sizeof(int), L.nf, L.stream));
+        Geometry g3 = p->g;
+        g3.max_dets = L.dcap;
+        HIPCHK(launch_k3(g3, p->k, fp, L.nf, L.stream));
+        HIPCHK(hipStreamSynchronize(L.stream));
+        L.fp = fp;
+    }
     if (keep_dets) keep_dets->assign(L.nf, {});
     for (int f = 0; f < L.nf; ++f) {
-        const DevDet* hrec = L.h_dets + (size_t)f * (p->async_cap + 1);
-        const int cnt = *reinterpret_cast<const int*>(hrec);
+        const DevDet* hrec = L.h_dets + (size_t)f * (L.hcap + 1);
+        const DevDet* drec = L.dets + (size_t)(L.dcap + 1) * f;
         FrameResult fr;
         fr.frame_idx = L.frame_ids[f];
-        fr.overflow = cnt > p->g.max_dets;
-        const int n = std::min(cnt, p->g.max_dets);
+        const int n = cnt[f];
         fr.n_dets = n;
         std::vector<rsp_detection> dets(n);
-        const int na = std::min(n, p->async_cap);
         static_assert(sizeof(DevDet) == sizeof(rsp_detection), "layout");
+        const int na = regrow ? 0 : std::min(n, L.hcap);   // already in host memory
         if (na) memcpy(dets.data(), hrec + 1, sizeof(DevDet) * na);
-        if (n > na)
-            HIPCHK(hipMemcpy(dets.data() + na, L.dets + (size_t)(p->g.max_dets + 1) * f + 1 + na,
-                             sizeof(DevDet) * (n - na), hipMemcpyDeviceToHost));
-        if (fr.overflow) p->overflow_seen = true;
+        if (n > na) HIPCHK(hipMemcpy(dets.data() + na, drec + 1 + na, sizeof(DevDet) * (n - na), hipMemcpyDeviceToHost));
         if (keep_dets || L.nf == 1) {   // synchronous frame paths: cluster here
             rsp_cluster_frame(p->cl, dets, fr.targets);
             if (keep_dets) (*keep_dets)[f] = dets;
@@ -546,6 +601,7 @@ int harvest(rsp_plan* p, Lane& L, std::vector<std::vector<rsp_detection>>* keep_
             p->pool->submit([cl, slot, d = std::move(dets)]() mutable { rsp_cluster_frame(cl, d, slot->targets); });
         }
     }
+    if (maxc > L.hcap && (rc = lane_host_alloc(p, L, std::min(p->det_bound, pow2_at_least(maxc))))) return rc;
     return RSP_OK;
 }
 
@@ -703,10 +759,10 @@ int run_sync_frame(rsp_plan* p, const void* d_in, int frame_idx, rsp_frame_out* 
     if ((rc = harvest(p, L, &dets))) return rc;
     FrameResult fr = p->results.back();
     p->results.resize(nres);   // synchronous frames do not enter the queue's result list
-    if (fr.overflow) return fail(RSP_ERR_OVERFLOW, "frame %d: detections exceed capacity %d (or > %d in one CFAR tile)",
-                                 frame_idx, p->g.max_dets, 1024);
+    p->last_dets = std::move(dets[0]);
+    p->last_targets = fr.targets;
     if (out) {
-        std::vector<rsp_detection>& d = dets[0];
+        const std::vector<rsp_detection>& d = p->last_dets;
         out->n_dets = (int)d.size();
         if (out->dets) memcpy(out->dets, d.data(), sizeof(rsp_detection) * std::min<int>(out->dets_cap, (int)d.size()));
         out->n_targets = (int)fr.targets.size();
@@ -715,9 +771,11 @@ int run_sync_frame(rsp_plan* p, const void* d_in, int frame_idx, rsp_frame_out* 
         if (out->rdm && (rc = rdm_to_matlab(p, L.rdm, out->rdm))) return rc;
         if (smap && (rc = smap_to_matlab(p, smap, out->cfar_maps))) return rc;   // device-produced (fsf:184-187)
         if (out->dets && (int)d.size() > out->dets_cap)
-            return fail(RSP_ERR_OVERFLOW, "%d detections exceed dets_cap %d", (int)d.size(), out->dets_cap);
+            return fail(RSP_ERR_OVERFLOW, "%d detections exceed dets_cap %d (all of them: rsp_last_detections)",
+                        (int)d.size(), out->dets_cap);
         if (out->targets && (int)fr.targets.size() > out->targets_cap)
-            return fail(RSP_ERR_OVERFLOW, "%d targets exceed targets_cap %d", (int)fr.targets.size(), out->targets_cap);
+            return fail(RSP_ERR_OVERFLOW, "%d targets exceed targets_cap %d (all of them: rsp_last_targets)",
+                        (int)fr.targets.size(), out->targets_cap);
     }
     return RSP_OK;
 }
@@ -793,7 +851,11 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
     g.cpitch = N * P;
     g.refR = cfar->refCells_R; g.guardR = cfar->guardCells_R; g.refV = cfar->refCells_V; g.guardV = cfar->guardCells_V;
     g.T = cfar->T_CFAR;
-    g.max_dets = 1 << 16;
+    g.max_dets = 1;   // per launch: the lane's list capacity (launch_batch)
+    {   // the most detections a frame can have: every cell under test of every beam pair (fsf:192-213)
+        const int64_t nv = std::max(P - 2 * (g.refV + g.guardV), 0), nr = std::max(G - 2 * (g.refR + g.guardR), 0);
+        p->det_bound = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)std::max(B - 1, 0) * nv * nr, 1 << 30));
+    }
     if (hipDeviceGetAttribute(&g.ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) g.ncu = 0;
     auto bail = [&](int rc) { delete p; return rc; };
     if (g.refR < 1 || g.refV < 1 || g.guardR < 0 || g.guardV < 0) return bail(fail(RSP_ERR_INVALID, "bad CFAR window"));
@@ -1048,7 +1110,7 @@ int32_t rsp_query_sizes(const rsp_plan* p, rsp_sizes* s) {
     s->cfar_map_elems = (int64_t)g.P * g.G * std::max(g.B - 1, 0);
     s->P = g.P; s->N = g.N; s->C = g.C; s->B = g.B; s->G = g.G;
     s->used_samples = g.nU;
-    s->max_detections = g.max_dets;
+    s->max_detections = p->det_bound;
     s->n_stages = 3;
     s->precision = g.prec == RSP_PREC_F64 ? RSP_C128 : RSP_C64;
     s->elem_bytes = (int32_t)p->esz;
@@ -1183,10 +1245,6 @@ int32_t rsp_process_targets_multi(rsp_plan* const* plans, int32_t n_plans, const
                 if ((rc = enqueue_frame(p, p->ring[s], s, frame_idx[j]))) return rc;
             }
             if ((rc = drain_all(p))) return rc;
-            if (p->overflow_seen) {
-                p->overflow_seen = false;
-                return fail(RSP_ERR_OVERFLOW, "a frame exceeded the detection capacity %d", p->g.max_dets);
-            }
             for (int j = f0; j < f1; ++j) {   // results come back in enqueue order
                 const FrameResult& r = p->results[j - f0];
                 n_out[j] = (int32_t)r.targets.size();
@@ -1204,7 +1262,6 @@ int32_t rsp_process_targets_multi(rsp_plan* const* plans, int32_t n_plans, const
             (void)drain_all(p);
             p->npend = 0;
             p->results.clear();
-            p->overflow_seen = false;
         }
     };
     std::vector<std::thread> th;
@@ -1219,12 +1276,24 @@ int32_t rsp_process_targets_multi(rsp_plan* const* plans, int32_t n_plans, const
 int32_t rsp_drain(rsp_plan* p) {
     if (!p) return fail(RSP_ERR_INVALID, "null argument");
     HIPCHK(hipSetDevice(p->device));
-    int rc = drain_all(p);
-    if (rc) return rc;
-    if (p->overflow_seen) {
-        p->overflow_seen = false;
-        return fail(RSP_ERR_OVERFLOW, "a queued frame exceeded the detection capacity %d", p->g.max_dets);
-    }
+    return drain_all(p);
+}
+
+int32_t rsp_last_detections(const rsp_plan* p, rsp_detection* dets, int32_t cap, int32_t* n) {
+    if (!p || !n || cap < 0 || (cap > 0 && !dets)) return fail(RSP_ERR_INVALID, "bad argument");
+    const int m = (int)p->last_dets.size();
+    *n = m;
+    if (dets) memcpy(dets, p->last_dets.data(), sizeof(rsp_detection) * std::min(cap, m));
+    if (dets && m > cap) return fail(RSP_ERR_OVERFLOW, "%d detections > cap %d", m, cap);
+    return RSP_OK;
+}
+
+int32_t rsp_last_targets(const rsp_plan* p, rsp_target* targets, int32_t cap, int32_t* n) {
+    if (!p || !n || cap < 0 || (cap > 0 && !targets)) return fail(RSP_ERR_INVALID, "bad argument");
+    const int m = (int)p->last_targets.size();
+    *n = m;
+    if (targets) memcpy(targets, p->last_targets.data(), sizeof(rsp_target) * std::min(cap, m));
+    if (targets && m > cap) return fail(RSP_ERR_OVERFLOW, "%d targets > cap %d", m, cap);
     return RSP_OK;
 }
 
@@ -1361,8 +1430,10 @@ int32_t rsp_profile_stages(rsp_plan* p, const void* const* d_cubes, int32_t n_cu
             if (s == 0) return launch_k1(g, p->k, fj, nf, 3, L.stream);
             if (s == 1) return launch_k2(g, p->k, fj, nf, g.B * g.P, L.stream);
             // counts are zeroed by K1 in the pipeline; here by a tiny 2-D memset per launch
-            hipError_t e = hipMemset2DAsync(L.dets, sizeof(DevDet) * (g.max_dets + 1), 0, sizeof(int), nf, L.stream);
-            return e != hipSuccess ? e : launch_k3(g, p->k, fj, nf, L.stream);
+            hipError_t e = hipMemset2DAsync(L.dets, sizeof(DevDet) * (L.dcap + 1), 0, sizeof(int), nf, L.stream);
+            Geometry g3 = g;
+            g3.max_dets = L.dcap;
+            return e != hipSuccess ? e : launch_k3(g3, p->k, fj, nf, L.stream);
         };
         HIPCHK(run());
         HIPCHK(hipEventRecord(e0, L.stream));

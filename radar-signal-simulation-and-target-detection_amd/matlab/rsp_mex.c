@@ -258,6 +258,16 @@ static mxArray* targets_struct(const rsp_target* t, int n) {   /* fsf:393-406 fi
     return s;
 }
 
+/* final_targets of the frame just run, all of them (rsp_last_targets: no fixed count) */
+static mxArray* last_targets_struct(void) {
+    int32_t n = 0;
+    rsp_target* t;
+    check(rsp_last_targets(g_plan, NULL, 0, &n));
+    t = (rsp_target*)mxCalloc(n > 0 ? n : 1, sizeof *t);
+    check(rsp_last_targets(g_plan, t, n, &n));
+    return targets_struct(t, n);
+}
+
 static mxArray* dets_matrix(const rsp_detection* d, int n) {   /* all_raw_detections, fsf:220 */
     mxArray* m = mxCreateDoubleMatrix(n, 4, mxREAL);
     double* v = mxGetDoubles(m);
@@ -300,7 +310,6 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         const mxArray* tg;
         int nt, k;
         rsp_target_in* t;
-        rsp_target* out_t;
         rsp_frame_out out;
         frame_inputs(nrhs, prhs, &in, &seed);
         if (!in.pre.tx_pulse) mexErrMsgIdAndTxt("radar:rsp", "precomputed_data.tx_pulse is needed to synthesise echoes");
@@ -314,19 +323,15 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
             t[k].ElevationAngle = mxGetScalar(mxGetField(tg, k, "ElevationAngle"));
             t[k].SNR_dB = mxGetScalar(mxGetField(tg, k, "SNR_dB"));
         }
-        out_t = (rsp_target*)mxCalloc(4096, sizeof *out_t);
-        memset(&out, 0, sizeof out);
-        out.targets = out_t;
-        out.targets_cap = 4096;
+        memset(&out, 0, sizeof out);   /* targets / detections read after the frame (rsp_last_*) */
         check(rsp_process_targets(g_plan, t, nt, (int32_t)mxGetScalar(prhs[6]), seed, 1.0, &out));   /* P_noise_floor = 1, fsf:16 */
-        plhs[0] = targets_struct(out_t, out.n_targets);
+        plhs[0] = last_targets_struct();
         return;
     }
     if (!strcmp(cmd, "cube")) {    /* fsf:90-407 on raw_iq_data */
         const mxArray* x = prhs[1];
         rsp_frame_out out;
         rsp_detection* dets;
-        rsp_target* out_t;
         int32_t dtype;
         const void* data;
         frame_inputs(nrhs, prhs, &in, &seed);
@@ -337,13 +342,7 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         if (mxIsDouble(x) && mxIsComplex(x)) { dtype = RSP_C128; data = mxGetComplexDoubles(x); }
         else if (mxIsSingle(x) && mxIsComplex(x)) { dtype = RSP_C64; data = mxGetComplexSingles(x); }
         else mexErrMsgIdAndTxt("radar:rsp", "raw_iq_data must be complex double or single");
-        memset(&out, 0, sizeof out);
-        dets = (rsp_detection*)mxCalloc(sz.max_detections, sizeof *dets);
-        out_t = (rsp_target*)mxCalloc(4096, sizeof *out_t);
-        out.dets = dets;
-        out.dets_cap = sz.max_detections;
-        out.targets = out_t;
-        out.targets_cap = 4096;
+        memset(&out, 0, sizeof out);   /* the lists have no fixed length: read after the frame (rsp_last_*) */
         if (nlhs > 2) {
             mwSize d[3] = {(mwSize)sz.P, (mwSize)sz.G, (mwSize)sz.B};
             plhs[2] = mxCreateNumericArray(3, d, mxDOUBLE_CLASS, mxCOMPLEX);
@@ -355,8 +354,13 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
             out.cfar_maps = mxGetDoubles(plhs[3]);
         }
         check(rsp_process_cube(g_plan, data, dtype, RSP_LAYOUT_PNC, (int32_t)mxGetScalar(prhs[6]), &out));
-        plhs[0] = targets_struct(out_t, out.n_targets);
-        if (nlhs > 1) plhs[1] = dets_matrix(dets, out.n_dets);
+        plhs[0] = last_targets_struct();
+        if (nlhs > 1) {
+            int32_t n = 0;
+            dets = (rsp_detection*)mxCalloc(out.n_dets > 0 ? out.n_dets : 1, sizeof *dets);
+            check(rsp_last_detections(g_plan, dets, out.n_dets, &n));
+            plhs[1] = dets_matrix(dets, n);
+        }
         if (nlhs > 3 && sz.B <= 1) plhs[3] = mxCreateDoubleMatrix(0, 0, mxREAL);
         return;
     }

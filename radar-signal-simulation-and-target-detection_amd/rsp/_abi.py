@@ -150,6 +150,8 @@ PROTOTYPES = {
                                                ct.POINTER(ct.c_int32), ct.POINTER(ct.c_int32), ct.c_int32, ct.c_uint64,
                                                ct.c_double, ct.POINTER(Target), ct.c_int32, ct.POINTER(ct.c_int32)]),
     'rsp_drain': (ct.c_int32, [_P]),
+    'rsp_last_detections': (ct.c_int32, [_P, ct.POINTER(Detection), ct.c_int32, ct.POINTER(ct.c_int32)]),
+    'rsp_last_targets': (ct.c_int32, [_P, ct.POINTER(Target), ct.c_int32, ct.POINTER(ct.c_int32)]),
     'rsp_results_count': (ct.c_int32, [_P, ct.POINTER(ct.c_int32), ct.POINTER(ct.c_int64)]),
     'rsp_results_get': (ct.c_int32, [_P, ct.c_int32, ct.POINTER(ct.c_int32), ct.POINTER(Target), ct.c_int32,
                                      ct.POINTER(ct.c_int32), ct.POINTER(ct.c_int32)]),

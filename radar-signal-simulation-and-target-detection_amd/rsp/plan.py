@@ -105,7 +105,7 @@ class Plan:
             pass
 
     # ---- synchronous frame paths ---------------------------------------------------------
-    def _frame_out(self, want_rdm, want_cfar, dets_cap=1 << 16, tcap=4096):
+    def _frame_out(self, want_rdm, want_cfar):
         o = _abi.FrameOut()
         bufs = {}
         if want_rdm:
@@ -114,15 +114,29 @@ class Plan:
         if want_cfar and self.B > 1:
             bufs['cfar'] = np.empty((self.P, self.G, self.B - 1), np.float64, order='F')
             o.cfar_maps = _dptr(bufs['cfar'])
-        dets = (_abi.Detection * dets_cap)()
-        tg = (_abi.Target * tcap)()
-        o.dets, o.dets_cap, o.targets, o.targets_cap = dets, dets_cap, tg, tcap
-        return o, bufs, dets, tg
+        # detections and final targets have no fixed count: read after the frame (rsp_last_*)
+        o.dets, o.dets_cap, o.targets, o.targets_cap = None, 0, None, 0
+        return o, bufs, None, None
 
-    @staticmethod
-    def _collect(o, bufs, dets, tg):
-        res = {'final_targets': [_tgt_dict(tg[i]) for i in range(o.n_targets)],
-               'detections': [_det_dict(dets[i]) for i in range(o.n_dets)]}
+    def last_detections(self):
+        """Every detection of the last synchronous frame (rsp_last_detections; no capacity limit)."""
+        n = ct.c_int32()
+        check(lib().rsp_last_detections(self.h, None, 0, ct.byref(n)))
+        dets = (_abi.Detection * max(n.value, 1))()
+        check(lib().rsp_last_detections(self.h, dets, n.value, ct.byref(n)))
+        return [_det_dict(dets[i]) for i in range(n.value)]
+
+    def last_targets(self):
+        """The final targets of the last synchronous frame (rsp_last_targets)."""
+        n = ct.c_int32()
+        check(lib().rsp_last_targets(self.h, None, 0, ct.byref(n)))
+        tg = (_abi.Target * max(n.value, 1))()
+        check(lib().rsp_last_targets(self.h, tg, n.value, ct.byref(n)))
+        return [_tgt_dict(tg[i]) for i in range(n.value)]
+
+    def _collect(self, o, bufs, dets, tg):
+        res = {'final_targets': self.last_targets(), 'detections': self.last_detections()}
+        assert len(res['detections']) == o.n_dets and len(res['final_targets']) == o.n_targets
         if 'rdm' in bufs:
             res['rdm'] = bufs['rdm']
         if 'cfar' in bufs:
@@ -258,10 +272,15 @@ class Plan:
         nf, nt = ct.c_int32(), ct.c_int64()
         check(lib().rsp_results_count(self.h, ct.byref(nf), ct.byref(nt)))
         out = []
-        buf = (_abi.Target * 4096)()
+        cap = 4096
+        buf = (_abi.Target * cap)()
         for i in range(nf.value):
             fi, n, nd = ct.c_int32(), ct.c_int32(), ct.c_int32()
-            check(lib().rsp_results_get(self.h, i, ct.byref(fi), buf, 4096, ct.byref(n), ct.byref(nd)))
+            check(lib().rsp_results_get(self.h, i, ct.byref(fi), None, 0, ct.byref(n), ct.byref(nd)))
+            if n.value > cap:
+                cap = n.value
+                buf = (_abi.Target * cap)()
+            check(lib().rsp_results_get(self.h, i, ct.byref(fi), buf, cap, ct.byref(n), ct.byref(nd)))
             out.append({'frame_idx': fi.value, 'n_dets': nd.value,
                         'final_targets': [_tgt_dict(buf[j]) for j in range(n.value)]})
         if clear:
