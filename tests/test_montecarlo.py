@@ -8,18 +8,26 @@ trials each under parfor with fresh MATLAB randn noise (:167-211), records final
 
 Here every trial is rsp_process_targets on the device (complex double): S4 synthesis + S4.1
 Philox noise with seed 20250101 + 1000 * i_snr + trial (MATLAB randn is irreproducible), then
-S5-S11.  Checks:
-  * on a subset of trials (-4, 10 and 30 dB, 2 trials each) the device's final targets equal the
-    oracle's on the same noisy cube (complex double tolerances of test_gpu_parity.py);
+S5-S11.  What is checked is the per-frame kernel's estimator -- S9's AMPLITUDE monopulse on the
+integer cell, (|A| - |B|) / (|A| + |B| + eps) (fsf:280-290) -- and not the script's own inline
+copy of S9, which uses the complex ratio real((A - B) / (A + B)) (main_plot_snr_vs_angle_error.m:
+455-458): this build replaces fun_process_single_frame, so its statistics are the kernel's.
+
+Checks:
+  * oracle on the same seeds: at -4, 4, 12 and 24 dB the first 8 trials' noisy cubes (downloaded
+    from the device) go through oracle.chain in 8 worker processes; every trial's final targets
+    must equal the device's (complex double tolerances of test_gpu_parity.py), and the device's
+    100-trial angle-error std and mean must agree with the oracle's 8-trial ones within a 99.9 %
+    two-sided F bound (variance ratio, F(99, 7)) and |z| < 4 (mean difference);
   * Pd = 1 from 0 dB up and never decreases by more than 0.1 between SNR steps; the first final
     target is the true target (|range error| < 15 m) in every detected trial from 0 dB up;
-  * the angle-error std stays below the script's curve |k| sqrt(2)/sqrt(SNR) wherever Pd >= 0.9,
-    below 0.1 deg everywhere, and the mean error below 0.05 deg.  The curve is per-sample: the
-    16-channel DBF, the 200/700-tap pulse compression and the 332-pulse MTD put the measured
-    error 1-3 orders of magnitude under it, and what is left is set by which cells of which beam
-    pairs cross the threshold and merge in S10/S11 (the power-weighted cluster means), not by
-    noise -- so the std is not monotone in SNR (measured on the MI355X: 0.03-0.09 deg up to
-    20 dB, 0.0005-0.0009 deg at 22-28 dB, 0.034 deg at 30 dB where an extra pair's cells join).
+  * the angle-error std stays below the script's curve |k| sqrt(2)/sqrt(SNR) wherever Pd >= 0.9.
+    The curve is per-sample: the 16-channel DBF, the 200/700-tap pulse compression and the
+    332-pulse MTD put the measured error 1-3 orders of magnitude under it, and what is left is set
+    by which cells of which beam pairs cross the threshold and merge in S10/S11 (the
+    power-weighted cluster means), not by noise -- so the std is not monotone in SNR (measured on
+    the MI355X: 0.03-0.09 deg up to 20 dB, 0.0005-0.0009 deg at 22-28 dB, 0.034 deg at 30 dB
+    where an extra pair's cells join).
 The per-SNR table is printed (and written to gpurun_out/montecarlo.json when that directory
 exists).
 """
@@ -48,19 +56,55 @@ def _seed(i_snr, trial):
     return SEED0 + 1000 * i_snr + trial
 
 
-def test_snr_vs_angle_error():
+ORACLE_SNRS = (-4, 4, 12, 24)
+ORACLE_TRIALS = 8
+
+
+def _oracle_worker(path):
+    """One oracle trial on a downloaded device cube (a worker process: no GPU use)."""
+    from threadpoolctl import threadpool_limits
+    from _scen import scenario as sc_
+    from oracle import chain as ch
+    s = sc_('reference')
+    cube = np.load(path)
+    with threadpool_limits(2):   # 8 workers x 2 BLAS threads: the box's 16-core share
+        return ch.process_cube(cube, s['cfg'], s['cfar'], s['clus'], s['pre_o'])
+
+
+def _oracle_trials(plan, todo, tmpdir, workers=8):
+    """{(snr, trial): oracle final targets} on the device's own noisy cubes, `workers` at a time."""
+    import multiprocessing as mp
+    out = {}
+    ctx = mp.get_context('spawn')
+    with ctx.Pool(workers) as pool:
+        for k in range(0, len(todo), workers):
+            chunk = todo[k:k + workers]
+            paths = []
+            for snr, t in chunk:
+                cube = device_cube(plan, [dict(TRUE, SNR_dB=float(snr))], frame_idx=1, seed=_seed(SNRS.index(snr), t))
+                pth = os.path.join(tmpdir, 'cube_%d_%d.npy' % (snr + 100, t))
+                np.save(pth, cube)
+                paths.append(pth)
+            for key, fo, pth in zip(chunk, pool.map(_oracle_worker, paths), paths):
+                out[key] = fo
+                os.remove(pth)
+    return out
+
+
+def test_snr_vs_angle_error(tmp_path):
+    from scipy import stats
     s = scenario('reference')
     plan = Plan(s['cfg'], s['cfar'], s['clus'], s['pre_p'])
     table = []
-    first = {}
+    dev = {}
     try:
         for i, snr in enumerate(SNRS):
             tg = [dict(TRUE, SNR_dB=float(snr))]
             errs, rng_errs, n_det = [], [], 0
             for t in range(TRIALS):
                 fin = plan.process_targets(tg, frame_idx=1, seed=_seed(i, t))['final_targets']
-                if (snr, t) in ((-4, 0), (-4, 1), (10, 0), (10, 1), (30, 0), (30, 1)):
-                    first[(snr, t)] = fin
+                if snr in ORACLE_SNRS and t < ORACLE_TRIALS:
+                    dev[(snr, t)] = fin
                 if fin:
                     n_det += 1
                     errs.append(fin[0]['Angle'] - TRUE['ElevationAngle'])     # :274-275
@@ -69,21 +113,37 @@ def test_snr_vs_angle_error():
             theory = abs(K_PAIR5) * np.sqrt(2) / np.sqrt(10 ** (snr / 10))      # :306-308
             table.append(dict(snr_db=snr, pd=n_det / TRIALS, angle_err_std=std, theory=theory,
                               angle_err_mean=float(np.mean(errs)) if errs else float('nan'),
-                              max_abs_range_err=float(np.max(np.abs(rng_errs))) if rng_errs else float('nan')))
-        # device vs oracle on the same noisy cubes (subset)
-        for (snr, t), fin in sorted(first.items()):
-            cube = device_cube(plan, [dict(TRUE, SNR_dB=float(snr))], frame_idx=1, seed=_seed(SNRS.index(snr), t))
-            fo = chain.process_cube(cube, s['cfg'], s['cfar'], s['clus'], s['pre_o'])
-            assert len(fo) == len(fin), (snr, t)
+                              max_abs_range_err=float(np.max(np.abs(rng_errs))) if rng_errs else float('nan'),
+                              n_detected=len(errs)))
+        # the oracle on the same seeds (the device's own cubes), per trial and per SNR
+        orc = _oracle_trials(plan, sorted(dev), str(tmp_path))
+        for key, fin in sorted(dev.items()):
+            fo = orc[key]
+            assert len(fo) == len(fin), key
             for a, b in zip(fo, fin):
                 for f in ('Range', 'Velocity', 'Angle', 'Power'):
-                    assert b[f] == pytest.approx(a[f], rel=1e-9, abs=1e-9), (snr, t, f)
+                    assert b[f] == pytest.approx(a[f], rel=1e-9, abs=1e-9), (key, f)
+        for r in table:
+            if r['snr_db'] not in ORACLE_SNRS:
+                continue
+            e = [orc[(r['snr_db'], t)][0]['Angle'] - TRUE['ElevationAngle'] for t in range(ORACLE_TRIALS)
+                 if orc[(r['snr_db'], t)]]
+            so, mo, no = float(np.std(e, ddof=1)), float(np.mean(e)), len(e)
+            r.update(oracle_std=so, oracle_mean=mo, oracle_n=no)
+            lo, hi = stats.f.ppf([0.0005, 0.9995], r['n_detected'] - 1, no - 1)
+            ratio = (r['angle_err_std'] / so) ** 2
+            r.update(f_ratio=ratio, f_bounds=[float(lo), float(hi)])
+            assert lo <= ratio <= hi, r
+            z = (r['angle_err_mean'] - mo) / np.sqrt(r['angle_err_std'] ** 2 / r['n_detected'] + so ** 2 / no)
+            assert abs(z) < 4, r
     finally:
         plan.close()
     print()
     for r in table:
-        print('SNR %+3d dB  Pd %.2f  std %.4f deg  (curve %.4f)  mean %+.4f  max|dR| %.2f m' % (
-            r['snr_db'], r['pd'], r['angle_err_std'], r['theory'], r['angle_err_mean'], r['max_abs_range_err']))
+        print('SNR %+3d dB  Pd %.2f  std %.4f deg  (curve %.4f)  mean %+.4f  max|dR| %.2f m%s' % (
+            r['snr_db'], r['pd'], r['angle_err_std'], r['theory'], r['angle_err_mean'], r['max_abs_range_err'],
+            '  oracle (%d trials) std %.4f mean %+.4f' % (r['oracle_n'], r['oracle_std'], r['oracle_mean'])
+            if 'oracle_std' in r else ''))
     out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'gpurun_out')
     if os.path.isdir(out):
         json.dump(table, open(os.path.join(out, 'montecarlo.json'), 'w'), indent=1)
@@ -94,8 +154,6 @@ def test_snr_vs_angle_error():
             assert r['max_abs_range_err'] < 15.0, r
         if r['pd'] >= 0.9:
             assert r['angle_err_std'] < r['theory'], r
-        if r['pd'] > 0:
-            assert r['angle_err_std'] < 0.1 and abs(r['angle_err_mean']) < 0.05, r
     for a, b in zip(table, table[1:]):
         assert b['pd'] >= a['pd'] - 0.1, (a, b)
     assert by[30]['pd'] == 1.0
