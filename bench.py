@@ -130,6 +130,7 @@ def cpu_baseline(cfg, cfar, clus, W, ang, k, targets, budget_s=15.0, nframes=0, 
 
 
 MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense peak
+F64_PEAK_TFLOPS = 78.6         # MI355X FP64 peak, vector and matrix alike (v_fma_f64, v_mfma_f64_16x16x4_f64)
 
 
 def _music_cpu_worker(args):
@@ -167,14 +168,15 @@ def music_cpu_baseline(scene, scan, dl, N, K, M, per_core=48):
                       'instances, one BLAS thread each, slowest %.2f s' % (n, cores, per_core, el)}
 
 
-def music_traffic():
+def music_traffic(prec):
     """k_music_cov HBM bytes per 1024-instance launch from the PMC passes (profiles/, made by
     tools/pmc_traffic.py over tools/music_prof.py 1024), or None."""
-    tf = os.path.join(ROOT, 'profiles', 'pmc_traffic_music5.json')
+    tf = os.path.join(ROOT, 'profiles', 'pmc_traffic_music5%s.json' % ('' if prec == 'c64' else '_c128'))
     if not os.path.exists(tf):
         return None
     with open(tf) as f:
-        return json.load(f).get('k_music_cov')
+        tj = json.load(f)
+    return tj.get('k_music_cov64', tj.get('k_music_cov'))
 
 
 def main_music(a):
@@ -194,8 +196,11 @@ def main_music(a):
     from rsp.music import MusicPlan, music_1d_scene
     N, K, M, I = 64, 1024, 3, a.batch
     scene, scan, dl = music_1d_scene()
-    plan = MusicPlan(N, K, M, scan, dl, max_batch=I, device=local if world > 1 else 0)
-    ring = [plan.device_alloc(I) for _ in range(2)]   # 2 x 512 MiB > Infinity Cache
+    plan = MusicPlan(N, K, M, scan, dl, max_batch=I, device=local if world > 1 else 0, precision=a.precision)
+    f64 = a.precision == 'c128'
+    mfma_peak = F64_PEAK_TFLOPS if f64 else MFMA_F32_PEAK_TFLOPS
+    valu_peak = F64_PEAK_TFLOPS if f64 else MFMA_F32_PEAK_TFLOPS
+    ring = [plan.device_alloc(I) for _ in range(2)]   # 2 x 1 GiB (c128) > Infinity Cache
     for r, d in enumerate(ring):
         plan.synthesize_device(d, scene, I, inst0=(rank * 2 + r) * I)
     peaks = np.zeros((I, M), np.int32)
@@ -220,32 +225,42 @@ def main_music(a):
         pr = plan.profile(ring[0], I, iters=a.profile_iters)
         flops = 8.0 * N * (N + 1) / 2 * K * I   # Hermitian X X^H: N(N+1)/2 entries x K complex MACs
         cov_tf = flops / (pr['cov_ms'] * 1e-3) / 1e12
-        bytes_ = 8.0 * N * K * I
+        bytes_ = (16.0 if f64 else 8.0) * N * K * I
         eig_flops = (16.0 / 3.0 * N ** 3 + 8.0 * M * N * N + 8.0 * len(scan) * M * N) * I
-        stages = [{'stage': 'k_music_cov', 'ms_per_launch': pr['cov_ms'], 'instances_per_launch': I,
+        sfx = '64' if f64 else ''
+        stages = [{'stage': 'k_music_cov' + sfx, 'ms_per_launch': pr['cov_ms'], 'instances_per_launch': I,
                    'alg_flops_per_launch': flops, 'achieved_TFLOPs': cov_tf,
                    'achieved_GBps': bytes_ / (pr['cov_ms'] * 1e-3) / 1e9},
-                  {'stage': 'k_music_eig', 'ms_per_launch': pr['eig_ms'], 'instances_per_launch': I,
+                  {'stage': 'k_music_eig' + sfx, 'ms_per_launch': pr['eig_ms'], 'instances_per_launch': I,
                    # algorithmic model: complex Householder tridiagonalisation 16/3 N^3, back-transform
                    # of the M signal vectors 8 M N^2, pseudo-spectrum 8 n_scan M N real flop
                    'alg_flops_per_launch': eig_flops,
                    'achieved_TFLOPs': eig_flops / (pr['eig_ms'] * 1e-3) / 1e12,
-                   'frac_of_f32_vector_peak': eig_flops / (pr['eig_ms'] * 1e-3) / 1e12 / MFMA_F32_PEAK_TFLOPS,
-                   'note': 'the dominant kernel: one wave per instance, Householder + bisection + inverse '
-                           'iteration + spectrum, latency-bound (neither HBM nor MFMA), see DESIGN.md'}]
+                   'frac_of_vector_peak': eig_flops / (pr['eig_ms'] * 1e-3) / 1e12 / valu_peak,
+                   'vector_peak_TFLOPs': valu_peak,
+                   'note': ('one 256-thread workgroup per instance, the matrix in registers (quad = column): '
+                            'Householder + multisection + inverse iteration + spectrum in double' if f64 else
+                            'one wave per instance, Householder + bisection + inverse iteration + spectrum in '
+                            'single') + '; latency-bound (neither HBM nor MFMA), see DESIGN.md'}]
+        dom = max(stages, key=lambda st: st['ms_per_launch'])
         out = {'metric': 'MUSIC_1D DOA instances/sec, 64ch x 1024 snapshots (BASELINE config #5)',
                'value': I * a.steps * world / el, 'unit': 'instances/s', 'n_gpus': world, 'steps': a.steps,
                'warmup': a.warmup, 'ms_per_step': el / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
-               'vs_baseline': None, 'dtype': 'fp32 (complex64)',
+               'vs_baseline': None, 'dtype': 'fp64 (complex128)' if f64 else 'fp32 (complex64)',
                'data': 'synthetic (device Philox snapshots, MUSIC_1D.m scene: -10/-30/60 deg, 10 dB measured)',
                'config': {'workload': 'BASELINE config #5: N=64 K=1024 M=3 scan=200, %d instances per step' % I,
                           'parallelism': 'instance-sharded x%d' % world},
-               'roofline': {'bound': 'mfma', 'kernel': 'k_music_cov', 'achieved': cov_tf,
-                            'peak': MFMA_F32_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': cov_tf / MFMA_F32_PEAK_TFLOPS,
-                            'traffic': music_traffic(), 'kernel_ms': pr['cov_ms'],
+               'roofline': {'bound': 'mfma' if dom is stages[0] else 'valu', 'kernel': dom['stage'],
+                            'achieved': dom['achieved_TFLOPs'],
+                            'peak': mfma_peak if dom is stages[0] else valu_peak, 'unit': 'TFLOP/s',
+                            'frac': dom['achieved_TFLOPs'] / (mfma_peak if dom is stages[0] else valu_peak),
+                            'traffic': music_traffic(a.precision) if dom is stages[0] else None,
+                            'kernel_ms': dom['ms_per_launch'],
                             'timing': 'HIP events on the plan stream, %d launches' % a.profile_iters,
-                            'note': 'roofline of the MFMA kernel (k_music_cov); the dominant kernel is k_music_eig, '
-                                    'latency-bound: its algorithmic fraction of the f32 vector peak is in stages',
+                            'note': 'the dominant kernel of the step; k_music_cov%s: %.3f of the %s MFMA peak, '
+                                    'k_music_eig: %.3f of the vector peak (stages)' % (
+                                        '64' if f64 else '', cov_tf / mfma_peak, 'f64' if f64 else 'f32',
+                                        stages[1]['frac_of_vector_peak']),
                             'stages': stages},
                'cpu_baseline': music_cpu_baseline(scene, scan, dl, N, K, M) if (world == 1 and not a.no_cpu_baseline)
                else None}

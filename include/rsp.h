@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RSP_ABI_VERSION 2
+#define RSP_ABI_VERSION 3
 
 typedef enum rsp_status {
     RSP_OK = 0,
@@ -384,8 +384,10 @@ int32_t rsp_mat_save_frame(const char* path, const double* cube, int32_t P, int3
  *   Q_n = EV(:, M+1:N) (:33); P = 1./sum(abs(Q_n'*S1).^2) over the scan grid (:35-37);
  *   P_dB = 10*log10(P/max(P)) (:39-41); findpeaks(P_dB), the M largest (:43-47).
  * The reference scripts have no function signature; these entry points take the scripts'
- * variables (N, K, M, d/lambda, phi_list) as the plan and X as the data.  fp32 on the device
- * (MFMA covariance, Householder + bisection eigensolver); tolerance vs the fp64 oracle in tests/test_music.py. */
+ * variables (N, K, M, d/lambda, phi_list) as the plan and X as the data.  Arithmetic: complex
+ * double by default, like MATLAB (f64 MFMA covariance, Householder + multisection + inverse
+ * iteration in double); complex single on request (precision = RSP_C64).  Outputs are double
+ * either way.  Tolerances vs the complex128 oracle: tests/test_music.py. */
 typedef struct rsp_music_config {
     int32_t channel_num;      /* N, 2..64 (MUSIC_1D.m:10; BASELINE #5: 64)                 */
     int32_t num_snapshots;    /* K (MUSIC_1D.m:18; BASELINE #5: 1024)                      */
@@ -394,6 +396,8 @@ typedef struct rsp_music_config {
     double d_over_lambda;     /* element spacing / wavelength (MUSIC_1D.m:11: 0.5)         */
     const double* scan_rad;   /* phi_list in radians, n_scan entries (borrowed for create) */
     int32_t max_batch;        /* instances per call (device buffers sized for it)          */
+    int32_t precision;        /* RSP_C128 (complex double, MATLAB's; default) or RSP_C64:
+                                 the device snapshots, covariance and eigensolver            */
 } rsp_music_config;
 
 /* Synthetic signal model of MUSIC_1D.m:14-24 / run_music_algorithm.m:14-39; MATLAB randn is
@@ -412,8 +416,8 @@ typedef struct rsp_music_scene {
 
 /* Caller-owned outputs for n_inst instances; any pointer may be NULL (not produced). */
 typedef struct rsp_music_out {
-    float* spectrum_db;       /* [n_scan x I] P_MUSIC_dB (MUSIC_1D.m:41)                      */
-    float* eigenvalues;       /* [N x I] descending (MUSIC_1D.m:30-31)                         */
+    double* spectrum_db;      /* [n_scan x I] P_MUSIC_dB (MUSIC_1D.m:41)                      */
+    double* eigenvalues;      /* [N x I] descending (MUSIC_1D.m:30-31)                         */
     int32_t* peak_idx;        /* [M x I] 1-based scan indices of the M largest peaks (:43-47), 0 = none */
     int32_t* n_peaks;         /* [I] number of findpeaks peaks                                 */
     double* covariance;       /* complex [N x N x I] R (MUSIC_1D.m:28), column-major           */
@@ -425,7 +429,8 @@ int32_t rsp_music_create(const rsp_music_config* cfg, int32_t device, rsp_music_
 int32_t rsp_music_destroy(rsp_music_plan* plan);
 /* Host snapshots X [N x K x n_inst] (RSP_C64 or RSP_C128), synchronous. */
 int32_t rsp_music_process(rsp_music_plan* plan, const void* X, int32_t dtype, int32_t n_inst, rsp_music_out* out);
-/* Device-resident complex64 snapshots; results copied to `out` (NULL: results stay on the device). */
+/* Device-resident snapshots in the plan's precision ([N x K x n_inst], complex double or single);
+ * results copied to `out` (NULL: results stay on the device). */
 int32_t rsp_music_process_device(rsp_music_plan* plan, const void* d_X, int32_t n_inst, rsp_music_out* out);
 /* Synthesise n_inst instances (instance ids inst0..) into device memory d_X [N x K x n_inst]. */
 int32_t rsp_music_synthesize_device(rsp_music_plan* plan, const rsp_music_scene* scene, int32_t n_inst,

@@ -1379,24 +1379,6 @@ __device__ __forceinline__ void s9_estimate(const S9Consts& k, SF sval, int P, i
 
 #define K3_QCAP 1024
 
-// A hit past the workgroup's LDS queue (more than K3_QCAP in one tile: a cluttered frame or a low
-// T_CFAR) reserves its slot in the frame's list itself and runs S9 in place, so the list holds
-// every hit like all_raw_detections(end+1, :) (fsf:215-221).  Slots at or past `cap` are counted
-// but not written: the host sees count > cap, grows the list and runs K3 again (rsp_plan.cpp).
-// Out of line: the common path keeps its registers.
-template <class T, bool NOH>
-__device__ __attribute__((noinline)) void k3_spill_hit(S9Consts k, const T* Sv, int W, int c0, int P, int G, int Gp,
-                                                      int v, int r, int pair, const T* MA, const T* MB, DevDet* dets,
-                                                      int* count, int cap) {
-    const int idx = atomicAdd(count, 1);
-    if (idx >= cap) return;
-    if constexpr (NOH)
-        s9_estimate<T>(k, [&](int vv, int rr) -> T { const size_t o = (size_t)vv * Gp + rr; return MA[o] + MB[o]; },
-                       P, G, Gp, v, r, pair, MA, MB, &dets[idx]);
-    else
-        s9_estimate<T>(k, [&](int vv, int rr) -> T { return Sv[vv * W + (rr - c0)]; }, P, G, Gp, v, r, pair, MA, MB,
-                       &dets[idx]);
-}
 #ifndef RSP_K3_ABLATE
 #define RSP_K3_ABLATE 0   // timing ablations (A/B builds only): 1 = no CFAR, 2 = no map loads
 #endif
@@ -1572,13 +1554,13 @@ __global__ __launch_bounds__(RSP_THREADS, RSP_K3_WGS) void k3_cfar(Geometry g, D
         return nR > nV ? nR : nV;
     };
     const S9Consts s9c{k.range_axis, k.velocity_axis, k.beam_angles, k.klut, k.deltaR, k.deltaV};
+    // hits past the LDS queue are only counted here (qn keeps counting); the overflow pass below
+    // finds them again
 #define K3_HIT(V, C, CUT, LR, TR, LV, TV)                                                               \
     do {                                                                                                \
         if ((CUT) > (T)Tc * noise2(LR, TR, LV, TV)) {                                                   \
             const int qi = atomicAdd(qn, 1);                                                            \
             if (qi < K3_QCAP) queue[qi] = ((V) << 16) | (C);                                            \
-            else k3_spill_hit<T, NOH>(s9c, Sv, W, c0, P, G, Gp, V, c0 + (C), pair, MA, MB, fp.dets[f],  \
-                                      fp.count[f], g.max_dets);                                         \
         }                                                                                               \
     } while (0)
     // ---- cross GOCA-CFAR (fsf:192-213); hits go to an LDS queue so that the S9 work is
@@ -1742,21 +1724,63 @@ __global__ __launch_bounds__(RSP_THREADS, RSP_K3_WGS) void k3_cfar(Geometry g, D
     }
 #undef K3_HIT
     __syncthreads();
-    const int n = min(qn[0], K3_QCAP);
+    const int nhit = qn[0], n = min(nhit, K3_QCAP);
     if (n == 0) return;
     if (threadIdx.x == 0) qn[1] = atomicAdd(fp.count[f], n);   // one global reservation per workgroup
     __syncthreads();
     const int base = qn[1];
+    // S(v, r) as the CFAR test read it: the tile, or the maps where a halo-less tile lacks it
+    auto st = [&](int vv, int rr) -> T {
+        if constexpr (NOH) return sg(vv, rr);
+        else return Sv[vv * W + (rr - c0)];
+    };
     for (int i = threadIdx.x; i < n; i += RSP_THREADS) {
         const int idx = base + i;
-        if (idx >= g.max_dets) break;
+        if (idx >= g.max_dets) break;   // counted; the host grows the list and runs K3 again
         const int e = queue[i];
         const int v = e >> 16, c = e & 0xFFFF;
-        if constexpr (NOH)
-            s9_estimate<T>(s9c, sg, P, G, Gp, v, c0 + c, pair, MA, MB, &fp.dets[f][idx]);
-        else
-            s9_estimate<T>(s9c, [&](int vv, int rr) -> T { return Sv[vv * W + (rr - c0)]; }, P, G, Gp, v, c0 + c, pair,
-                           MA, MB, &fp.dets[f][idx]);
+        s9_estimate<T>(s9c, st, P, G, Gp, v, c0 + c, pair, MA, MB, &fp.dets[f][idx]);
+    }
+    if (nhit <= K3_QCAP) return;   // uniform
+    // Overflow pass (more than K3_QCAP hits in this tile: a cluttered frame or a low T_CFAR).  The
+    // list holds every hit, like all_raw_detections(end+1, :) (fsf:215-221): the queued cells are
+    // marked in a bitmap over the tile's cells under test (in the queue's LDS), and every other
+    // cell is tested again, with the same sums in the same order as above, so the same cells hit;
+    // each unmarked hit reserves its slot and runs S9.  Outside the CFAR loop, so the common path
+    // keeps its registers and schedule (an in-loop spill call cost K3 25 %).
+    constexpr int HELD = K3_QCAP / RSP_THREADS;
+    int held[HELD];
+#pragma unroll
+    for (int u = 0; u < HELD; ++u) held[u] = queue[threadIdx.x + u * RSP_THREADS];
+    __syncthreads();
+    unsigned* bm = reinterpret_cast<unsigned*>(queue);   // ncr x (v1 - v0) bits <= K3_QCAP x 32
+    const int ncr = cut_hi - cut_lo, ncell = (v1 - v0) * ncr;
+#pragma unroll
+    for (int u = 0; u < HELD; ++u) bm[threadIdx.x + u * RSP_THREADS] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < HELD; ++u) {
+        const int v = held[u] >> 16, r = c0 + (held[u] & 0xFFFF);
+        const int bit = (v - v0) * ncr + (r - cut_lo);
+        atomicOr(&bm[bit >> 5], 1u << (bit & 31));
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < ncell; e += RSP_THREADS) {
+        if (bm[e >> 5] >> (e & 31) & 1u) continue;
+        const int v = v0 + e / ncr, r = cut_lo + (e - (e / ncr) * ncr);
+        T lr = 0, tr = 0, lv = 0, tv = 0;
+        for (int qq = 0; qq < rR; ++qq) {
+            lr += st(v, r - gR - rR + qq);
+            tr += st(v, r + gR + 1 + qq);
+        }
+        for (int qq = 0; qq < rV; ++qq) {
+            lv += st(v + qq - gV - rV, r);
+            tv += st(v + qq + gV + 1, r);
+        }
+        if (st(v, r) > (T)Tc * noise2(lr, tr, lv, tv)) {
+            const int idx = atomicAdd(fp.count[f], 1);
+            if (idx < g.max_dets) s9_estimate<T>(s9c, st, P, G, Gp, v, r, pair, MA, MB, &fp.dets[f][idx]);
+        }
     }
 }
 

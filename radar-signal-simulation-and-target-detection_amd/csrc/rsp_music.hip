@@ -56,18 +56,22 @@ __device__ __forceinline__ double2 mu_normal(uint64_t i, uint32_t inst, uint64_t
 // the signal power (awgn 'measured'), pass 1 adds the noise and stores.
 // ---------------------------------------------------------------------------------------
 #define MU_SYN_KC 128
+__device__ __forceinline__ void mu_store(float2* p, double re, double im) { *p = make_float2((float)re, (float)im); }
+__device__ __forceinline__ void mu_store(double2* p, double re, double im) { *p = make_double2(re, im); }
 // snr_measured: awgn(X, SNR, 'measured') (MUSIC_1D.m:24), the noise scale follows from pass 0;
 // otherwise nsc_fixed = sqrt(noise_power / 2) (run_music_algorithm.m:35-36) and pass 0 is skipped.
+// CX: the plan's snapshot type (double2: complex double, MATLAB's; float2: complex single).
+template <class CX>
 __global__ __launch_bounds__(MU_THREADS) void k_music_synth(int N, int K, int M, int inst0, uint64_t seed,
                                                           const double2* __restrict__ Ssrc, const double* __restrict__ amp,
                                                           int complex_src, int snr_measured, double snr_db,
-                                                          double nsc_fixed, float2* __restrict__ X) {
+                                                          double nsc_fixed, CX* __restrict__ X) {
     __shared__ double2 al[MU_MMAX][MU_SYN_KC];
     __shared__ double2 Sl[MU_MMAX][MU_NMAX];
     __shared__ double red[MU_THREADS];
     const int tid = threadIdx.x;
     const uint32_t inst = (uint32_t)(inst0 + blockIdx.x);
-    float2* __restrict__ Xi = X + (size_t)blockIdx.x * K * N;
+    CX* __restrict__ Xi = X + (size_t)blockIdx.x * K * N;
     for (int e = tid; e < M * N; e += MU_THREADS) Sl[e / N][e % N] = Ssrc[e];
     double nsc = nsc_fixed;
     for (int pass = snr_measured ? 0 : 1; pass < 2; ++pass) {
@@ -95,7 +99,7 @@ __global__ __launch_bounds__(MU_THREADS) void k_music_synth(int N, int K, int M,
                 } else {   // noise: stream index c + N k
                     const uint64_t lin = (uint64_t)c + (uint64_t)N * (k0 + kk);
                     const double2 z = mu_normal(lin, inst, seed, MU_TAG_NOISE);
-                    Xi[lin] = make_float2((float)(xr + nsc * z.x), (float)(xi + nsc * z.y));
+                    mu_store(Xi + lin, xr + nsc * z.x, xi + nsc * z.y);
                 }
             }
         }
@@ -602,6 +606,522 @@ __global__ __launch_bounds__(64) void k_music_eig(int N, int S, const float2* __
 #undef MU_STAMP
 }
 
+// =======================================================================================
+// Complex double (MATLAB's arithmetic, MUSIC_1D.m:28-48 in double): the default precision.
+// =======================================================================================
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double2 zm(double2 a, double2 b) { return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
+__device__ __forceinline__ double2 zmc(double2 a, double2 b) {   // conj(a) * b
+    return make_double2(a.x * b.x + a.y * b.y, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ double2 zadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 zsub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double2 zsc(double s, double2 a) { return make_double2(s * a.x, s * a.y); }
+__device__ __forceinline__ double2 zconj(double2 a) { return make_double2(a.x, -a.y); }
+
+// DPP moves of a double (two 32-bit halves), and the quad / row / wave reductions built on them
+template <int C>
+__device__ __forceinline__ double dppd(double v) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)b, C, 0xF, 0xF, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), C, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ double rdld(double v, int l) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ double qsumd(double v) {   // over the 4 lanes of a quad, every lane
+    v += dppd<0xB1>(v);
+    return v + dppd<0x4E>(v);
+}
+__device__ __forceinline__ double wsumd(double v) {   // over the wave, uniform (fixed order)
+    v = qsumd(v);
+    v += dppd<0x141>(v);
+    v += dppd<0x140>(v);
+    return (rdld(v, 0) + rdld(v, 16)) + (rdld(v, 32) + rdld(v, 48));
+}
+__device__ __forceinline__ double wmaxd(double v) {
+    v = fmax(v, dppd<0xB1>(v));
+    v = fmax(v, dppd<0x4E>(v));
+    v = fmax(v, dppd<0x141>(v));
+    v = fmax(v, dppd<0x140>(v));
+    return fmax(fmax(rdld(v, 0), rdld(v, 16)), fmax(rdld(v, 32), rdld(v, 48)));
+}
+template <int C>
+__device__ __forceinline__ int dppi(int v) { return __builtin_amdgcn_update_dpp(0, v, C, 0xF, 0xF, false); }
+// ordering of LDS traffic between the lanes of one wave (phases run by a single wave)
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---------------------------------------------------------------------------------------
+// R = X X^H / K on the f64 matrix cores (MUSIC_1D.m:28 in double).  Same decomposition as
+// k_music_cov: one workgroup per instance, split-K over the 4 waves, lane l loads channels
+// 4(l&15)..+3 of snapshot 4s + (l>>4) (64 B), and that register is both the A and the B operand
+// of v_mfma_f64_16x16x4_f64 (A[r][kk] = x_I, B[kk][r] = x_J; tile (I, J) holds R[4r+I][4s+J]);
+// 10 Hermitian tiles, 4 MFMAs each per step.  The f64 C/D layout puts row (l>>4) + 4i, column
+// l&15 in accumulator element i.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(MU_THREADS, 2) void k_music_cov64(int N, int K, const double2* __restrict__ X,
+                                                              double2* __restrict__ R) {
+    __shared__ double red[10][2][256];   // per tile, Re/Im, D[row][col] row-major
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r = lane & 15, kk = lane >> 4;
+    const double2* __restrict__ Xi = X + (size_t)blockIdx.x * K * N;
+    f64x4 ar[10], ai[10];
+#pragma unroll
+    for (int t = 0; t < 10; ++t) {
+        ar[t] = f64x4{0.0, 0.0, 0.0, 0.0};
+        ai[t] = ar[t];
+    }
+    const int nsteps = (K + 3) >> 2;
+    auto load = [&](int s, double (&xr)[4], double (&xi)[4]) {
+        const int k = 4 * s + kk, c0 = 4 * r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            double2 x = make_double2(0.0, 0.0);
+            if (k < K && c0 + i < N) x = Xi[(size_t)k * N + c0 + i];
+            xr[i] = x.x;
+            xi[i] = x.y;
+        }
+    };
+    auto step = [&](const double (&xr)[4], const double (&xi)[4]) {
+        double nr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) nr[i] = -xr[i];
+        int t = 0;
+#pragma unroll
+        for (int I = 0; I < 4; ++I)
+#pragma unroll
+            for (int J = I; J < 4; ++J, ++t) {
+                ar[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(xr[I], xr[J], ar[t], 0, 0, 0);
+                ar[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(xi[I], xi[J], ar[t], 0, 0, 0);
+                ai[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(xi[I], xr[J], ai[t], 0, 0, 0);
+                ai[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(nr[I], xi[J], ai[t], 0, 0, 0);
+            }
+    };
+    double xr0[4], xi0[4], xr1[4], xi1[4];
+    int s = w;
+    if (s < nsteps) load(s, xr0, xi0);
+    if (s + 4 < nsteps) load(s + 4, xr1, xi1);
+    for (; s + 4 < nsteps; s += 8) {
+        step(xr0, xi0);
+        if (s + 8 < nsteps) load(s + 8, xr0, xi0);
+        step(xr1, xi1);
+        if (s + 12 < nsteps) load(s + 12, xr1, xi1);
+    }
+    if (s < nsteps) step(xr0, xi0);
+    for (int ww = 0; ww < 4; ++ww) {   // ordered cross-wave sum (deterministic)
+        if (w == ww) {
+#pragma unroll
+            for (int t = 0; t < 10; ++t)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int e = (kk + 4 * v) * 16 + r;   // D row (l>>4) + 4v, column l&15
+                    if (ww == 0) {
+                        red[t][0][e] = ar[t][v];
+                        red[t][1][e] = ai[t][v];
+                    } else {
+                        red[t][0][e] += ar[t][v];
+                        red[t][1][e] += ai[t][v];
+                    }
+                }
+        }
+        __syncthreads();
+    }
+    double2* __restrict__ Ri = R + (size_t)blockIdx.x * MU_NMAX * MU_NMAX;   // column-major, ld 64
+    int t = 0;
+    for (int I = 0; I < 4; ++I)
+        for (int J = I; J < 4; ++J, ++t) {
+            const int i = tid >> 4, j = tid & 15;
+            const int a = 4 * i + I, b = 4 * j + J;
+            const double re = red[t][0][tid] / K, im = red[t][1][tid] / K;   // X1*X1'/K: a division, as MATLAB
+            if (a < N && b < N) {
+                Ri[a + MU_NMAX * b] = make_double2(re, im);
+                if (I != J) Ri[b + MU_NMAX * a] = make_double2(re, -im);
+            }
+        }
+}
+
+// ---------------------------------------------------------------------------------------
+// eig + MUSIC spectrum + findpeaks in double (MUSIC_1D.m:29-48): ONE 256-THREAD WORKGROUP PER
+// INSTANCE, the matrix in registers.  Lane t holds column i = t >> 2, rows 16 (t & 3) .. +15
+// (16 complex doubles): a quad of lanes is a column, so a column's sums are two DPP steps and
+// the only LDS traffic of the reduction is the broadcast of v and w (and two partial sums).
+//  1. Householder reduction to a real tridiagonal T (LAPACK zhetd2, lower): column k's quad
+//     forms v_k (zlarfg) and keeps it; p = tau A v (lane = column, A Hermitian), w = p - tau/2
+//     (p^H v) v, A -= v w^H + w v^H -- three barriers per step.
+//  2. All eigenvalues of T by multisection, quad i -> the i-th smallest: the 4 lanes evaluate
+//     the Sturm count (LAPACK dstebz recurrence with pivmin) at 4 interior points, 24 rounds
+//     shrink the Gershgorin interval by 5^24 (below the rounding of the eigenvalue).
+//  3. The M signal eigenvectors of T by inverse iteration (dlagtf / dlagts, lane j = vector j,
+//     3 solves with modified Gram-Schmidt) in wave 0, then q_j = H_0 ... H_{n-2} y_j, the
+//     reflectors applied by their own quads.
+//  4. den(s) = |a(s) - Q_s Q_s^H a(s)|^2 = sum_j |Q_n^H a(s)|^2 (MUSIC_1D.m:37), lane = angle.
+//  5. P = 1 ./ den, P_dB = 10 log10(P / max P), findpeaks + the M largest (MUSIC_1D.m:37-47).
+// ---------------------------------------------------------------------------------------
+#define ME_THREADS 256
+#define ME_SECT 24   // multisection rounds: 5^24 > 2^55
+#ifndef ME_WPS
+#define ME_WPS 4     // waves per SIMD the register budget is sized for (4 instances per CU)
+#endif
+__host__ __device__ constexpr size_t me_lds_bytes(int M, int S) {
+    return (size_t)4 * 64 * 16 + 64 * 16 + 8 * 16 + 4 * 64 * 8 + (size_t)5 * 64 * M * 8 + (size_t)M * 64 * 16 +
+           ((size_t)S + 8) * 8 + 8 * 16;
+}
+
+template <int M>
+__global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S, const double2* __restrict__ R,
+                                                          const double2* __restrict__ S1T, int Spad,
+                                                          double* __restrict__ spec_db, double* __restrict__ eig_out,
+                                                          int* __restrict__ peaks_out) {
+    extern __shared__ __attribute__((aligned(16))) double2 lds64[];
+    double2* vb = lds64;                 // [2][64] v of the step (double-buffered by k parity)
+    double2* wb = vb + 128;              // [2][64] w
+    double2* taus = wb + 128;            // [64]
+    double2* red = taus + 64;            // [8] per-wave partial sums
+    double* dd = reinterpret_cast<double*>(red + 8);   // T diagonal
+    double* ee = dd + 64;                // T off-diagonal (beta_k, signed)
+    double* e2 = ee + 64;                // beta_k^2
+    double* lam = e2 + 64;               // ascending eigenvalues
+    double* lu = lam + 64;               // [5][64][M]: U diag, U super 1, U super 2, mult, y
+    double2* Qs = reinterpret_cast<double2*>(lu + 5 * 64 * M);   // [M][64]
+    double* den = reinterpret_cast<double*>(Qs + M * 64);        // [S]
+    int* ired = reinterpret_cast<int*>(den + S + 8);             // [8] + the peak selection
+    double* dred = den + S;                                      // [8]
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int i = t >> 2, q = t & 3;
+    const int n = N;
+    const double2 z2 = make_double2(0.0, 0.0);
+    double2 a[16];   // A(16 q + u, i)
+    {
+        const double2* __restrict__ Ri = R + (size_t)blockIdx.x * MU_NMAX * MU_NMAX;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int j = 16 * q + u;
+            a[u] = (i < n && j < n) ? Ri[j + MU_NMAX * i] : z2;
+        }
+    }
+    // ---- 1. tridiagonalisation
+    for (int k = 0; k < n - 1; ++k) {
+        double2* vk = vb + 64 * (k & 1);
+        double2* wk = wb + 64 * (k & 1);
+        if (w == (k >> 4)) {   // the wave holding column k (uniform)
+            const bool mine = i == k;
+            double xn = 0.0, dk = 0.0;
+            double2 al = z2;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int j = 16 * q + u;
+                if (mine && j >= k + 2 && j < n) xn += a[u].x * a[u].x + a[u].y * a[u].y;
+                if (mine && j == k + 1) al = a[u];
+                if (mine && j == k) dk = a[u].x;
+            }
+            xn = qsumd(xn);
+            al.x = qsumd(al.x);
+            al.y = qsumd(al.y);
+            dk = qsumd(dk);
+            double2 tau = z2, scale = z2;
+            double beta = al.x;
+            if (xn > 0.0 || al.y != 0.0) {   // zlarfg
+                beta = -copysign(sqrt(al.x * al.x + al.y * al.y + xn), al.x);
+                tau = make_double2((beta - al.x) / beta, -al.y / beta);
+                const double2 dn = make_double2(al.x - beta, al.y);
+                const double qd = 1.0 / (dn.x * dn.x + dn.y * dn.y);
+                scale = make_double2(dn.x * qd, -dn.y * qd);
+            }
+            if (mine) {
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int j = 16 * q + u;
+                    const double2 v = j == k + 1 ? make_double2(1.0, 0.0) : (j >= k + 2 && j < n ? zm(a[u], scale) : z2);
+                    a[u] = v;   // column k keeps v_k for the back-transformation
+                    vk[j] = v;
+                }
+                if (q == 0) {
+                    taus[k] = tau;
+                    dd[k] = dk;
+                    ee[k] = beta;
+                    e2[k] = beta * beta;
+                }
+            }
+        }
+        __syncthreads();
+        const double2 tau = taus[k];
+        if (tau.x == 0.0 && tau.y == 0.0) continue;   // H_k = I (uniform)
+        const bool act = i > k && i < n;
+        double2 p = z2;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) p = zadd(p, zmc(a[u], vk[16 * q + u]));   // sum_j conj(A(j,i)) v_j
+        p.x = qsumd(p.x);
+        p.y = qsumd(p.y);
+        p = act ? zm(tau, p) : z2;
+        const double2 vi = vk[i];
+        double2 pv = q == 0 ? zmc(p, vi) : z2;                                  // p^H v
+        pv.x = wsumd(pv.x);
+        pv.y = wsumd(pv.y);
+        if (lane == 0) red[w] = pv;
+        __syncthreads();
+        const double2 sp = zadd(zadd(red[0], red[1]), zadd(red[2], red[3]));
+        const double2 alpha = zsc(-0.5, zm(tau, sp));
+        const double2 wi = act ? zadd(p, zm(alpha, vi)) : z2;
+        if (q == 0) wk[i] = wi;
+        __syncthreads();
+        if (act) {   // A(j, i) -= v_j conj(w_i) + w_j conj(v_i) (v_j = w_j = 0 for j <= k)
+            const double2 cw = zconj(wi), cv = zconj(vi);
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int j = 16 * q + u;
+                a[u] = zsub(a[u], zadd(zm(vk[j], cw), zm(wk[j], cv)));
+            }
+        }
+    }
+    if (w == ((n - 1) >> 4)) {
+        double dl = 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+            if (i == n - 1 && 16 * q + u == n - 1) dl = a[u].x;
+        dl = qsumd(dl);
+        if (i == n - 1 && q == 0) dd[n - 1] = dl;
+    }
+    __syncthreads();
+    // ---- 2. eigenvalues by multisection (quad i -> the i-th smallest)
+    {
+        double glo = 1.0e300, ghi = -1.0e300, emax = 0.0;
+        for (int r = 0; r < n; ++r) {   // Gershgorin
+            const double rad = (r > 0 ? fabs(ee[r - 1]) : 0.0) + (r < n - 1 ? fabs(ee[r]) : 0.0);
+            glo = fmin(glo, dd[r] - rad);
+            ghi = fmax(ghi, dd[r] + rad);
+            if (r < n - 1) emax = fmax(emax, e2[r]);
+        }
+        const double tn = fmax(fabs(glo), fabs(ghi));
+        const double pivmin = 2.2250738585072014e-308 * fmax(1.0, emax);   // dstebz PIVMIN
+        double lo = glo - 4.4e-16 * tn - 2.0 * pivmin, hi = ghi + 4.4e-16 * tn + 2.0 * pivmin;
+        auto sturm = [&](double x) -> int {   // # eigenvalues of T below x
+            double qv = dd[0] - x;
+            if (fabs(qv) < pivmin) qv = -pivmin;
+            int c = qv < 0.0;
+            for (int r = 1; r < n; ++r) {
+                double rc = __builtin_amdgcn_rcp(qv);
+                rc = fma(fma(-qv, rc, 1.0), rc, rc);   // one Newton step: e2 / q to about an ulp
+                rc = fma(fma(-qv, rc, 1.0), rc, rc);
+                qv = (dd[r] - x) - e2[r - 1] * rc;
+                if (fabs(qv) < pivmin) qv = -pivmin;
+                c += qv < 0.0;
+            }
+            return c;
+        };
+        for (int it = 0; it < ME_SECT; ++it) {
+            const double h = (hi - lo) * 0.2;
+            const int c = sturm(lo + h * (q + 1));
+            const int m = (dppi<0x00>(c) <= i) + (dppi<0x55>(c) <= i) + (dppi<0xAA>(c) <= i) + (dppi<0xFF>(c) <= i);
+            const double nl = m == 0 ? lo : lo + h * m;
+            const double nh = m == 4 ? hi : lo + h * (m + 1);
+            lo = nl;
+            hi = nh;
+        }
+        if (i < n && q == 0) {
+            const double l = 0.5 * (lo + hi);
+            lam[i] = l;
+            eig_out[(size_t)blockIdx.x * N + (n - 1 - i)] = l;   // descending (MUSIC_1D.m:31)
+        }
+    }
+    __syncthreads();
+    // ---- 3. signal eigenvectors of T: inverse iteration in wave 0 (lane j = vector j, then
+    //         lane = component)
+    if (w == 0) {
+        double tnorm = 0.0;
+        for (int r = 0; r < n; ++r)
+            tnorm = fmax(tnorm, fabs(dd[r]) + (r > 0 ? fabs(ee[r - 1]) : 0.0) + (r < n - 1 ? fabs(ee[r]) : 0.0));
+        const double ptol = 2.2e-16 * tnorm + 1e-300;
+#define LU(arr, r) lu[((arr) * 64 + (r)) * M + lane]
+        unsigned long long swp = 0ull;
+        if (lane < M) {   // dlagtf on T - lambda_j I
+            const double lj = lam[n - 1 - lane];
+            double ak = dd[0] - lj;
+            double bk = n > 1 ? ee[0] : 0.0;
+            for (int k = 0; k < n - 1; ++k) {
+                const double ck = ee[k];
+                const double an = dd[k + 1] - lj;
+                const double bn = k < n - 2 ? ee[k + 1] : 0.0;
+                if (fabs(ak) >= fabs(ck)) {
+                    const double a0 = fabs(ak) < ptol ? copysign(ptol, ak) : ak;
+                    const double mult = ck / a0;
+                    LU(0, k) = a0; LU(1, k) = bk; LU(2, k) = 0.0; LU(3, k) = mult;
+                    ak = an - mult * bk;
+                    bk = bn;
+                } else {
+                    swp |= 1ull << k;
+                    const double mult = ak / ck;
+                    LU(0, k) = ck; LU(1, k) = an; LU(2, k) = bn; LU(3, k) = mult;
+                    ak = bk - mult * an;
+                    bk = -mult * bn;
+                }
+            }
+            LU(0, n - 1) = fabs(ak) < ptol ? copysign(ptol, ak) : ak;
+            for (int r = 0; r < n; ++r) LU(4, r) = 1.0 + 0.0625 * (double)((r * 37 + lane * 11) % 17);   // start
+        }
+        for (int it = 0; it < MU_ITER; ++it) {
+            if (lane < M) {   // dlagts
+                double yk = LU(4, 0);
+                for (int k = 0; k < n - 1; ++k) {
+                    const double yn = LU(4, k + 1), mult = LU(3, k);
+                    if (swp >> k & 1ull) {
+                        LU(4, k) = yn;
+                        yk = yk - mult * yn;
+                    } else {
+                        LU(4, k) = yk;
+                        yk = yn - mult * yk;
+                    }
+                }
+                double y1 = yk / LU(0, n - 1), y2 = 0.0;
+                LU(4, n - 1) = y1;
+                for (int k = n - 2; k >= 0; --k) {
+                    const double yk2 = (LU(4, k) - LU(1, k) * y1 - LU(2, k) * y2) / LU(0, k);
+                    LU(4, k) = yk2;
+                    y2 = y1;
+                    y1 = yk2;
+                }
+            }
+            wsync();
+            for (int j = 0; j < M; ++j) {   // modified Gram-Schmidt (lane = component)
+                double yj = lane < n ? lu[(4 * 64 + lane) * M + j] : 0.0;
+                for (int ii = 0; ii < j; ++ii) {
+                    const double yi = lane < n ? lu[(4 * 64 + lane) * M + ii] : 0.0;
+                    yj -= wsumd(yi * yj) * yi;
+                }
+                yj /= sqrt(wsumd(yj * yj));
+                if (lane < n) lu[(4 * 64 + lane) * M + j] = yj;
+                wsync();
+            }
+        }
+#undef LU
+        for (int j = 0; j < M; ++j) Qs[j * 64 + lane] = make_double2(lane < n ? lu[(4 * 64 + lane) * M + j] : 0.0, 0.0);
+    }
+    __syncthreads();
+    // q_j = H_0 H_1 ... H_{n-2} y_j, k descending: the reflectors of wave wv's 16 columns are
+    // applied by wave wv with lane = row and the M vectors in registers (a wave's turn starts and
+    // ends with them in Qs); v_k passes from its quad to the wave through a 1 KB LDS buffer
+    for (int wv = 3; wv >= 0; --wv) {
+        if (w == wv && 16 * wv <= n - 2) {
+            double2 y[M];
+#pragma unroll
+            for (int j = 0; j < M; ++j) y[j] = Qs[j * 64 + lane];
+            for (int k = min(n - 2, 16 * wv + 15); k >= 16 * wv; --k) {
+                if (i == k) {
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) vb[16 * q + u] = a[u];
+                }
+                wsync();
+                const double2 vl = vb[lane], tau = taus[k];
+#pragma unroll
+                for (int j = 0; j < M; ++j) {
+                    double2 d = zmc(vl, y[j]);   // v^H y
+                    d.x = wsumd(d.x);
+                    d.y = wsumd(d.y);
+                    y[j] = zsub(y[j], zm(vl, zm(tau, d)));
+                }
+                wsync();
+            }
+#pragma unroll
+            for (int j = 0; j < M; ++j) Qs[j * 64 + lane] = y[j];
+        }
+        __syncthreads();
+    }
+    // ---- 4. den(s) = |a(s) - Q_s (Q_s^H a(s))|^2, lane = angle
+    for (int s = t; s < S; s += ME_THREADS) {
+        double2 cf[M];
+#pragma unroll
+        for (int m = 0; m < M; ++m) cf[m] = z2;
+        for (int c = 0; c < n; ++c) {
+            const double2 av = S1T[(size_t)c * Spad + s];
+#pragma unroll
+            for (int m = 0; m < M; ++m) cf[m] = zadd(cf[m], zmc(Qs[m * 64 + c], av));
+        }
+        double r2 = 0.0;
+        for (int c = 0; c < n; ++c) {
+            double2 rr = S1T[(size_t)c * Spad + s];
+#pragma unroll
+            for (int m = 0; m < M; ++m) rr = zsub(rr, zm(Qs[m * 64 + c], cf[m]));
+            r2 += rr.x * rr.x + rr.y * rr.y;
+        }
+        den[s] = r2;
+    }
+    __syncthreads();
+    // ---- 5. P = 1 ./ den, P_dB = 10 log10(P / max P) (MUSIC_1D.m:37-41)
+    double pm = 0.0;
+    for (int s = t; s < S; s += ME_THREADS) pm = fmax(pm, 1.0 / den[s]);
+    pm = wmaxd(pm);
+    if (lane == 0) dred[w] = pm;
+    __syncthreads();
+    const double pmax = fmax(fmax(dred[0], dred[1]), fmax(dred[2], dred[3]));
+    double* __restrict__ out = spec_db + (size_t)blockIdx.x * S;
+    for (int s = t; s < S; s += ME_THREADS) {
+        const double db = 10.0 * log10((1.0 / den[s]) / pmax);
+        den[s] = db;
+        out[s] = db;
+    }
+    __syncthreads();
+    // findpeaks (MUSIC_1D.m:43) + the M largest, ties to the lower index (MUSIC_1D.m:44-47)
+    unsigned pkm = 0u;   // bit tt: s = t + 256 tt is a peak (S <= 4096)
+    int npk = 0;
+    for (int tt = 0; tt * ME_THREADS < S; ++tt) {
+        const int s = t + ME_THREADS * tt;
+        bool pk = false;
+        if (s >= 1 && s < S - 1 && den[s] > den[s - 1]) {
+            int u = s + 1;
+            while (u < S && den[u] == den[s]) ++u;
+            pk = u < S && den[u] < den[s];
+        }
+        if (pk) pkm |= 1u << tt;
+        npk += pk;
+    }
+    npk = (int)wsumd((double)npk);
+    if (lane == 0) ired[w] = npk;
+    __syncthreads();
+    int* po = peaks_out + (size_t)blockIdx.x * (MU_MMAX + 1);
+    if (t == 0) po[0] = (ired[0] + ired[1]) + (ired[2] + ired[3]);
+    __syncthreads();
+    for (int rk = 0; rk < M; ++rk) {
+        double bv = -1.0e300;
+        int bs = 1 << 30;
+        for (int tt = 0; tt * ME_THREADS < S; ++tt)
+            if (pkm >> tt & 1u) {
+                const int s = t + ME_THREADS * tt;
+                if (den[s] > bv) { bv = den[s]; bs = s; }   // tt ascending: ties keep the lower s
+            }
+        const double gv = wmaxd(bv);
+        int cand = bv == gv ? bs : (1 << 30);
+        cand = min(cand, dppi<0xB1>(cand));
+        cand = min(cand, dppi<0x4E>(cand));
+        cand = min(cand, dppi<0x141>(cand));
+        cand = min(cand, dppi<0x140>(cand));
+        cand = min(min(__builtin_amdgcn_readlane(cand, 0), __builtin_amdgcn_readlane(cand, 16)),
+                   min(__builtin_amdgcn_readlane(cand, 32), __builtin_amdgcn_readlane(cand, 48)));
+        if (lane == 0) {
+            dred[w] = gv;
+            ired[w] = cand;
+        }
+        __syncthreads();
+        double best = dred[0];
+        for (int ww = 1; ww < 4; ++ww) best = fmax(best, dred[ww]);
+        int gs = 1 << 30;
+        for (int ww = 0; ww < 4; ++ww)
+            if (dred[ww] == best) gs = min(gs, ired[ww]);
+        if (gs < (1 << 30) && (gs % ME_THREADS) == t) pkm &= ~(1u << (gs / ME_THREADS));
+        if (t == 0) po[1 + rk] = gs < (1 << 30) ? gs + 1 : 0;
+        __syncthreads();
+    }
+    if (t == 0)
+        for (int rk = M; rk < MU_MMAX; ++rk) po[1 + rk] = 0;
+}
+
 }  // namespace
 
 // =======================================================================================
@@ -610,17 +1130,19 @@ __global__ __launch_bounds__(64) void k_music_eig(int N, int S, const float2* __
 struct rsp_music_plan {
     int device = 0;
     int N = 0, K = 0, M = 0, S = 0, Spad = 0, max_batch = 0;
+    bool f64 = true;              // RSP_C128 (MATLAB's complex double, default) or RSP_C64
+    size_t xsz = 16;              // bytes of one snapshot sample
     double dl = 0.0;
     hipStream_t stream = nullptr;
-    float2* d_S1T = nullptr;     // steering table [64][Spad], zero rows for c >= N
-    float2* d_R = nullptr;       // [max_batch][64][64]
-    float2* d_X = nullptr;       // host-path staging [max_batch][K][N] (lazy)
-    float* d_spec = nullptr;     // [max_batch][S]
-    float* d_eig = nullptr;      // [max_batch][N]
-    int* d_peaks = nullptr;      // [max_batch][MU_MMAX + 1]
-    double2* d_src = nullptr;    // synthesis: source steering [MU_MMAX][N]
-    double* d_amp = nullptr;     // [MU_MMAX]
-    unsigned long long* d_trace = nullptr;   // RSP_MUSIC_TRACE: [max_batch][8] phase stamps
+    void* d_S1T = nullptr;        // steering table [64][Spad] (float2 / double2), zero rows for c >= N
+    void* d_R = nullptr;          // [max_batch][64][64] complex
+    void* d_X = nullptr;          // host-path staging [max_batch][K][N] (lazy)
+    void* d_spec = nullptr;       // [max_batch][S] float / double
+    void* d_eig = nullptr;        // [max_batch][N] float / double
+    int* d_peaks = nullptr;       // [max_batch][MU_MMAX + 1]
+    double2* d_src = nullptr;     // synthesis: source steering [MU_MMAX][N]
+    double* d_amp = nullptr;      // [MU_MMAX]
+    unsigned long long* d_trace = nullptr;   // RSP_MUSIC_TRACE: [max_batch][8] phase stamps (f32 eig)
     hipEvent_t ev[4] = {};
 };
 
@@ -634,25 +1156,54 @@ namespace {
                                  __FILE__, __LINE__);                                                  \
     } while (0)
 
-int music_run(rsp_music_plan* p, const float2* dX, int n_inst, bool timed, float* ms) {
+template <int MC>
+hipError_t launch_eig64(rsp_music_plan* p, int n_inst) {
+    const size_t lds = me_lds_bytes(MC, p->S);
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_music_eig64<MC>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_music_eig64<MC>, dim3(n_inst), dim3(ME_THREADS), lds, p->stream, p->N, p->S,
+                       (const double2*)p->d_R, (const double2*)p->d_S1T, p->Spad, (double*)p->d_spec,
+                       (double*)p->d_eig, p->d_peaks);
+    return hipGetLastError();
+}
+
+int music_run(rsp_music_plan* p, const void* dX, int n_inst, bool timed, float* ms) {
     if (n_inst < 1 || n_inst > p->max_batch)
         return rsp_set_error(RSP_ERR_INVALID, "n_inst %d outside 1..max_batch %d", n_inst, p->max_batch);
     MUCHK(hipSetDevice(p->device));
     if (timed) MUCHK(hipEventRecord(p->ev[0], p->stream));
-    if (p->N % 4 == 0)
-        hipLaunchKernelGGL(k_music_cov<true>, dim3(n_inst), dim3(MU_THREADS), 0, p->stream, p->N, p->K, dX, p->d_R);
+    if (p->f64)
+        hipLaunchKernelGGL(k_music_cov64, dim3(n_inst), dim3(MU_THREADS), 0, p->stream, p->N, p->K,
+                           (const double2*)dX, (double2*)p->d_R);
+    else if (p->N % 4 == 0)
+        hipLaunchKernelGGL(k_music_cov<true>, dim3(n_inst), dim3(MU_THREADS), 0, p->stream, p->N, p->K,
+                           (const float2*)dX, (float2*)p->d_R);
     else
-        hipLaunchKernelGGL(k_music_cov<false>, dim3(n_inst), dim3(MU_THREADS), 0, p->stream, p->N, p->K, dX, p->d_R);
+        hipLaunchKernelGGL(k_music_cov<false>, dim3(n_inst), dim3(MU_THREADS), 0, p->stream, p->N, p->K,
+                           (const float2*)dX, (float2*)p->d_R);
     MUCHK(hipGetLastError());
     if (timed) MUCHK(hipEventRecord(p->ev[1], p->stream));
-    switch (p->M) {
-#define MU_EIG(MC)                                                                                                \
-    case MC:                                                                                                      \
+    if (p->f64) {
+        switch (p->M) {
+#define MU_EIG64(MC) \
+    case MC: MUCHK(launch_eig64<MC>(p, n_inst)); break;
+            MU_EIG64(1) MU_EIG64(2) MU_EIG64(3) MU_EIG64(4) MU_EIG64(5) MU_EIG64(6) MU_EIG64(7) MU_EIG64(8)
+#undef MU_EIG64
+        }
+    } else {
+        switch (p->M) {
+#define MU_EIG(MC)                                                                                               \
+    case MC:                                                                                                     \
         hipLaunchKernelGGL(k_music_eig<MC>, dim3(n_inst), dim3(64), mu_eig_lds_bytes(MC), p->stream, p->N, p->S, \
-                           p->d_R, p->d_S1T, p->Spad, p->d_spec, p->d_eig, p->d_peaks, p->d_trace);                \
+                           (const float2*)p->d_R, (const float2*)p->d_S1T, p->Spad, (float*)p->d_spec,            \
+                           (float*)p->d_eig, p->d_peaks, p->d_trace);                                             \
         break;
-        MU_EIG(1) MU_EIG(2) MU_EIG(3) MU_EIG(4) MU_EIG(5) MU_EIG(6) MU_EIG(7) MU_EIG(8)
+            MU_EIG(1) MU_EIG(2) MU_EIG(3) MU_EIG(4) MU_EIG(5) MU_EIG(6) MU_EIG(7) MU_EIG(8)
 #undef MU_EIG
+        }
     }
     MUCHK(hipGetLastError());
     if (timed) {
@@ -664,24 +1215,42 @@ int music_run(rsp_music_plan* p, const float2* dX, int n_inst, bool timed, float
     return RSP_OK;
 }
 
+// device results -> caller (double; a complex-single plan's are widened)
 int music_fetch(rsp_music_plan* p, int n_inst, rsp_music_out* out) {
     if (!out) return RSP_OK;
     const int N = p->N, M = p->M, S = p->S;
-    if (out->spectrum_db)
-        MUCHK(hipMemcpyAsync(out->spectrum_db, p->d_spec, (size_t)n_inst * S * sizeof(float), hipMemcpyDeviceToHost, p->stream));
-    if (out->eigenvalues)
-        MUCHK(hipMemcpyAsync(out->eigenvalues, p->d_eig, (size_t)n_inst * N * sizeof(float), hipMemcpyDeviceToHost, p->stream));
+    const size_t rs = p->f64 ? 8 : 4;
+    std::vector<unsigned char> spec, eig, rc;
+    if (out->spectrum_db) {
+        if (p->f64)
+            MUCHK(hipMemcpyAsync(out->spectrum_db, p->d_spec, (size_t)n_inst * S * 8, hipMemcpyDeviceToHost, p->stream));
+        else {
+            spec.resize((size_t)n_inst * S * rs);
+            MUCHK(hipMemcpyAsync(spec.data(), p->d_spec, spec.size(), hipMemcpyDeviceToHost, p->stream));
+        }
+    }
+    if (out->eigenvalues) {
+        if (p->f64)
+            MUCHK(hipMemcpyAsync(out->eigenvalues, p->d_eig, (size_t)n_inst * N * 8, hipMemcpyDeviceToHost, p->stream));
+        else {
+            eig.resize((size_t)n_inst * N * rs);
+            MUCHK(hipMemcpyAsync(eig.data(), p->d_eig, eig.size(), hipMemcpyDeviceToHost, p->stream));
+        }
+    }
     std::vector<int> pk;
     if (out->peak_idx || out->n_peaks) {
         pk.resize((size_t)n_inst * (MU_MMAX + 1));
         MUCHK(hipMemcpyAsync(pk.data(), p->d_peaks, pk.size() * sizeof(int), hipMemcpyDeviceToHost, p->stream));
     }
-    std::vector<float2> rc;
     if (out->covariance) {
-        rc.resize((size_t)n_inst * MU_NMAX * MU_NMAX);
-        MUCHK(hipMemcpyAsync(rc.data(), p->d_R, rc.size() * sizeof(float2), hipMemcpyDeviceToHost, p->stream));
+        rc.resize((size_t)n_inst * MU_NMAX * MU_NMAX * 2 * rs);
+        MUCHK(hipMemcpyAsync(rc.data(), p->d_R, rc.size(), hipMemcpyDeviceToHost, p->stream));
     }
     MUCHK(hipStreamSynchronize(p->stream));
+    if (!spec.empty())
+        for (size_t e = 0; e < (size_t)n_inst * S; ++e) out->spectrum_db[e] = reinterpret_cast<const float*>(spec.data())[e];
+    if (!eig.empty())
+        for (size_t e = 0; e < (size_t)n_inst * N; ++e) out->eigenvalues[e] = reinterpret_cast<const float*>(eig.data())[e];
     for (int i = 0; i < n_inst && !pk.empty(); ++i) {
         if (out->n_peaks) out->n_peaks[i] = pk[(size_t)i * (MU_MMAX + 1)];
         if (out->peak_idx)
@@ -691,10 +1260,17 @@ int music_fetch(rsp_music_plan* p, int n_inst, rsp_music_out* out) {
         for (int i = 0; i < n_inst; ++i)
             for (int b = 0; b < N; ++b)
                 for (int a = 0; a < N; ++a) {
-                    const float2 v = rc[(size_t)i * MU_NMAX * MU_NMAX + a + MU_NMAX * b];
+                    const size_t e = (size_t)i * MU_NMAX * MU_NMAX + a + MU_NMAX * b;
                     double* o = out->covariance + 2 * ((size_t)i * N * N + a + (size_t)N * b);
-                    o[0] = v.x;
-                    o[1] = v.y;
+                    if (p->f64) {
+                        const double* v = reinterpret_cast<const double*>(rc.data()) + 2 * e;
+                        o[0] = v[0];
+                        o[1] = v[1];
+                    } else {
+                        const float* v = reinterpret_cast<const float*>(rc.data()) + 2 * e;
+                        o[0] = v[0];
+                        o[1] = v[1];
+                    }
                 }
     return RSP_OK;
 }
@@ -713,6 +1289,8 @@ int32_t rsp_music_create(const rsp_music_config* cfg, int32_t device, rsp_music_
     if (K < 1) return rsp_set_error(RSP_ERR_INVALID, "num_snapshots %d < 1", K);
     if (S < 3 || S > MU_SCAN_MAX) return rsp_set_error(RSP_ERR_UNSUPPORTED, "n_scan %d outside 3..%d", S, MU_SCAN_MAX);
     if (cfg->max_batch < 1) return rsp_set_error(RSP_ERR_INVALID, "max_batch %d < 1", cfg->max_batch);
+    if (cfg->precision != RSP_C128 && cfg->precision != RSP_C64)
+        return rsp_set_error(RSP_ERR_INVALID, "precision must be RSP_C128 or RSP_C64, got %d", cfg->precision);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
         return rsp_set_error(RSP_ERR_DEVICE, "HIP device %d not available (%d devices)", device, ndev);
@@ -721,18 +1299,20 @@ int32_t rsp_music_create(const rsp_music_config* cfg, int32_t device, rsp_music_
     p->N = N; p->K = K; p->M = M; p->S = S; p->Spad = (S + 7) & ~3;
     p->max_batch = cfg->max_batch;
     p->dl = cfg->d_over_lambda;
+    p->f64 = cfg->precision == RSP_C128;
+    p->xsz = p->f64 ? 16 : 8;
     auto bail = [&](int rc) { rsp_music_destroy(p); return rc; };
     if (hipSetDevice(device) != hipSuccess) return bail(rsp_set_error(RSP_ERR_DEVICE, "hipSetDevice(%d)", device));
     if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(rsp_set_error(RSP_ERR_DEVICE, "hipStreamCreate failed"));
     for (auto& e : p->ev)
         if (hipEventCreate(&e) != hipSuccess) return bail(rsp_set_error(RSP_ERR_DEVICE, "hipEventCreate failed"));
-    const size_t B = (size_t)p->max_batch;
+    const size_t B = (size_t)p->max_batch, cs = p->xsz, rs = p->xsz / 2;
     struct { void** ptr; size_t bytes; } allocs[] = {
-        {(void**)&p->d_S1T, (size_t)MU_NMAX * p->Spad * sizeof(float2)},
-        {(void**)&p->d_R, B * MU_NMAX * MU_NMAX * sizeof(float2)},
-        {(void**)&p->d_spec, B * S * sizeof(float)},
-        {(void**)&p->d_eig, B * N * sizeof(float)},
+        {&p->d_S1T, (size_t)MU_NMAX * p->Spad * cs},
+        {&p->d_R, B * MU_NMAX * MU_NMAX * cs},
+        {&p->d_spec, B * S * rs},
+        {&p->d_eig, B * N * rs},
         {(void**)&p->d_peaks, B * (MU_MMAX + 1) * sizeof(int)},
         {(void**)&p->d_src, (size_t)MU_MMAX * MU_NMAX * sizeof(double2)},
         {(void**)&p->d_amp, (size_t)MU_MMAX * sizeof(double)},
@@ -740,16 +1320,23 @@ int32_t rsp_music_create(const rsp_music_config* cfg, int32_t device, rsp_music_
     for (auto& a : allocs)
         if (hipMalloc(a.ptr, a.bytes) != hipSuccess)
             return bail(rsp_set_error(RSP_ERR_NOMEM, "hipMalloc(%zu bytes) failed", a.bytes));
-    // S1 = exp(1j k z sin(phi_list')) (MUSIC_1D.m:36), fp64 then rounded; stored transposed
-    // [channel][angle] so a thread's 4 consecutive angles are one 32 B load
-    std::vector<float2> s1((size_t)MU_NMAX * p->Spad, make_float2(0.f, 0.f));
+    // S1 = exp(1j k z sin(phi_list')) (MUSIC_1D.m:36) in double (rounded to float for a complex-single
+    // plan); stored transposed [channel][angle]
+    std::vector<double2> s1((size_t)MU_NMAX * p->Spad, make_double2(0.0, 0.0));
     for (int c = 0; c < N; ++c)
         for (int s = 0; s < S; ++s) {
             const double ph = 2.0 * M_PI * p->dl * c * std::sin(cfg->scan_rad[s]);
-            s1[(size_t)c * p->Spad + s] = make_float2((float)std::cos(ph), (float)std::sin(ph));
+            s1[(size_t)c * p->Spad + s] = make_double2(std::cos(ph), std::sin(ph));
         }
-    if (hipMemcpy(p->d_S1T, s1.data(), s1.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess)
-        return bail(rsp_set_error(RSP_ERR_DEVICE, "steering upload failed"));
+    hipError_t e;
+    if (p->f64) {
+        e = hipMemcpy(p->d_S1T, s1.data(), s1.size() * sizeof(double2), hipMemcpyHostToDevice);
+    } else {
+        std::vector<float2> s1f(s1.size());
+        for (size_t i = 0; i < s1.size(); ++i) s1f[i] = make_float2((float)s1[i].x, (float)s1[i].y);
+        e = hipMemcpy(p->d_S1T, s1f.data(), s1f.size() * sizeof(float2), hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess) return bail(rsp_set_error(RSP_ERR_DEVICE, "steering upload failed"));
 #ifdef RSP_DEBUG_KNOBS   // diagnostic builds only: the shipped library reads no environment variable
     const char* tr = getenv("RSP_MUSIC_TRACE");
     if (tr && atoi(tr) && hipMalloc(&p->d_trace, B * 8 * sizeof(unsigned long long)) != hipSuccess)
@@ -792,9 +1379,14 @@ int32_t rsp_music_synthesize_device(rsp_music_plan* p, const rsp_music_scene* sc
     MUCHK(hipMemcpyAsync(p->d_src, src.data(), src.size() * sizeof(double2), hipMemcpyHostToDevice, p->stream));
     MUCHK(hipMemcpyAsync(p->d_amp, amp, sizeof amp, hipMemcpyHostToDevice, p->stream));
     const double nsc_fixed = std::sqrt(1.0 / std::pow(10.0, sc->snr_db / 10.0) / 2.0);
-    hipLaunchKernelGGL(k_music_synth, dim3(n_inst), dim3(MU_THREADS), 0, p->stream, N, p->K, Ms, inst0, seed,
-                       p->d_src, p->d_amp, sc->complex_sources, sc->snr_measured ? 1 : 0, sc->snr_db, nsc_fixed,
-                       (float2*)d_X);
+    if (p->f64)
+        hipLaunchKernelGGL(k_music_synth<double2>, dim3(n_inst), dim3(MU_THREADS), 0, p->stream, N, p->K, Ms, inst0,
+                           seed, p->d_src, p->d_amp, sc->complex_sources, sc->snr_measured ? 1 : 0, sc->snr_db,
+                           nsc_fixed, (double2*)d_X);
+    else
+        hipLaunchKernelGGL(k_music_synth<float2>, dim3(n_inst), dim3(MU_THREADS), 0, p->stream, N, p->K, Ms, inst0,
+                           seed, p->d_src, p->d_amp, sc->complex_sources, sc->snr_measured ? 1 : 0, sc->snr_db,
+                           nsc_fixed, (float2*)d_X);
     MUCHK(hipGetLastError());
     MUCHK(hipStreamSynchronize(p->stream));   // the host staging above is stack memory
     return RSP_OK;
@@ -802,7 +1394,7 @@ int32_t rsp_music_synthesize_device(rsp_music_plan* p, const rsp_music_scene* sc
 
 int32_t rsp_music_process_device(rsp_music_plan* p, const void* d_X, int32_t n_inst, rsp_music_out* out) {
     if (!p || !d_X) return rsp_set_error(RSP_ERR_INVALID, "null argument");
-    int rc = music_run(p, (const float2*)d_X, n_inst, false, nullptr);
+    int rc = music_run(p, d_X, n_inst, false, nullptr);
     if (rc) return rc;
     if (!out) {
         MUCHK(hipStreamSynchronize(p->stream));
@@ -819,12 +1411,17 @@ int32_t rsp_music_process(rsp_music_plan* p, const void* X, int32_t dtype, int32
     MUCHK(hipSetDevice(p->device));
     const size_t elems = (size_t)n_inst * p->K * p->N;
     if (!p->d_X) {
-        const size_t bytes = (size_t)p->max_batch * p->K * p->N * sizeof(float2);
+        const size_t bytes = (size_t)p->max_batch * p->K * p->N * p->xsz;
         if (hipMalloc(&p->d_X, bytes) != hipSuccess)
             return rsp_set_error(RSP_ERR_NOMEM, "hipMalloc(%zu bytes) failed", bytes);
     }
-    if (dtype == RSP_C64) {
-        MUCHK(hipMemcpy(p->d_X, X, elems * sizeof(float2), hipMemcpyHostToDevice));
+    if ((dtype == RSP_C128) == p->f64) {
+        MUCHK(hipMemcpy(p->d_X, X, elems * p->xsz, hipMemcpyHostToDevice));
+    } else if (p->f64) {   // complex single snapshots into a complex-double plan: widen
+        std::vector<double2> h(elems);
+        const float* x = (const float*)X;
+        for (size_t i = 0; i < elems; ++i) h[i] = make_double2(x[2 * i], x[2 * i + 1]);
+        MUCHK(hipMemcpy(p->d_X, h.data(), elems * sizeof(double2), hipMemcpyHostToDevice));
     } else {
         std::vector<float2> h(elems);
         const double* x = (const double*)X;
@@ -839,7 +1436,7 @@ int32_t rsp_music_profile(rsp_music_plan* p, const void* d_X, int32_t n_inst, in
     double acc[2] = {0.0, 0.0};
     for (int it = 0; it < iters; ++it) {
         float ms[2];
-        int rc = music_run(p, (const float2*)d_X, n_inst, true, ms);
+        int rc = music_run(p, d_X, n_inst, true, ms);
         if (rc) return rc;
         acc[0] += ms[0];
         acc[1] += ms[1];

@@ -111,7 +111,8 @@ class Track(ct.Structure):
 
 class MusicConfig(ct.Structure):
     _fields_ = [('channel_num', ct.c_int32), ('num_snapshots', ct.c_int32), ('num_sources', ct.c_int32),
-                ('n_scan', ct.c_int32), ('d_over_lambda', ct.c_double), ('scan_rad', _dp), ('max_batch', ct.c_int32)]
+                ('n_scan', ct.c_int32), ('d_over_lambda', ct.c_double), ('scan_rad', _dp), ('max_batch', ct.c_int32),
+                ('precision', ct.c_int32)]
 
 
 class MusicScene(ct.Structure):
@@ -121,7 +122,7 @@ class MusicScene(ct.Structure):
 
 
 class MusicOut(ct.Structure):
-    _fields_ = [('spectrum_db', ct.POINTER(ct.c_float)), ('eigenvalues', ct.POINTER(ct.c_float)),
+    _fields_ = [('spectrum_db', _dp), ('eigenvalues', _dp),
                 ('peak_idx', ct.POINTER(ct.c_int32)), ('n_peaks', ct.POINTER(ct.c_int32)), ('covariance', _dp)]
 
 

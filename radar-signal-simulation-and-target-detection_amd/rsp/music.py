@@ -8,7 +8,8 @@ plan; ``process`` runs a batch of snapshot matrices X [N x K] through
 
 and returns what the scripts compute: ``P_MUSIC_dB``, the sorted eigenvalues ``EVA``, the M
 peak indices / angles ``phi_e`` (MUSIC_1D.m:48).  ``MUSIC_1D(X, ...)`` is the one-instance
-form of MUSIC_1D.m.  All compute runs in librsp.so; there is no CPU path.
+form of MUSIC_1D.m.  ``precision``: 'c128' (complex double, MATLAB's arithmetic; default) or
+'c64' (complex single).  All compute runs in librsp.so; there is no CPU path.
 """
 import ctypes as ct
 
@@ -19,13 +20,18 @@ from . import _abi
 
 class MusicPlan:
     def __init__(self, channel_num, num_snapshots, num_sources, scan_rad, d_over_lambda=0.5, max_batch=1,
-                 device=0):
+                 device=0, precision='c128'):
+        if precision not in ('c128', 'c64'):
+            raise ValueError("precision must be 'c128' or 'c64'")
         self._lib = _abi.lib()
+        self.precision = precision
+        self.cdtype = np.complex128 if precision == 'c128' else np.complex64   # device snapshots
         self.scan_rad = np.ascontiguousarray(scan_rad, np.float64)
         self.N, self.K, self.M, self.S = int(channel_num), int(num_snapshots), int(num_sources), len(self.scan_rad)
         self.max_batch = int(max_batch)
         cfg = _abi.MusicConfig(self.N, self.K, self.M, self.S, float(d_over_lambda),
-                               self.scan_rad.ctypes.data_as(_abi._dp), self.max_batch)
+                               self.scan_rad.ctypes.data_as(_abi._dp), self.max_batch,
+                               _abi.RSP_C128 if precision == 'c128' else _abi.RSP_C64)
         h = ct.c_void_p()
         _abi.check(self._lib.rsp_music_create(ct.byref(cfg), int(device), ct.byref(h)))
         self._h = h
@@ -43,12 +49,12 @@ class MusicPlan:
 
     # ---- outputs -------------------------------------------------------------------------
     def _out(self, n, want_cov):
-        o = {'spectrum_db': np.zeros((n, self.S), np.float32), 'eig': np.zeros((n, self.N), np.float32),
+        o = {'spectrum_db': np.zeros((n, self.S), np.float64), 'eig': np.zeros((n, self.N), np.float64),
              'peaks': np.zeros((n, self.M), np.int32), 'n_peaks': np.zeros(n, np.int32)}
         if want_cov:
             o['R'] = np.zeros((n, self.N, self.N, 2), np.float64)   # per instance: [b][a] = R(a, b)
-        st = _abi.MusicOut(o['spectrum_db'].ctypes.data_as(ct.POINTER(ct.c_float)),
-                           o['eig'].ctypes.data_as(ct.POINTER(ct.c_float)),
+        st = _abi.MusicOut(o['spectrum_db'].ctypes.data_as(_abi._dp),
+                           o['eig'].ctypes.data_as(_abi._dp),
                            o['peaks'].ctypes.data_as(ct.POINTER(ct.c_int32)),
                            o['n_peaks'].ctypes.data_as(ct.POINTER(ct.c_int32)),
                            o['R'].ctypes.data_as(_abi._dp) if want_cov else None)
@@ -82,14 +88,15 @@ class MusicPlan:
     # ---- device-resident path (bench) ------------------------------------------------------
     def device_alloc(self, n_inst):
         p = ct.c_void_p()
-        _abi.check(self._lib.rsp_music_device_alloc(self._h, n_inst * self.N * self.K * 8, ct.byref(p)))
+        _abi.check(self._lib.rsp_music_device_alloc(self._h, n_inst * self.N * self.K * np.dtype(self.cdtype).itemsize,
+                                                    ct.byref(p)))
         return p.value
 
     def device_free(self, p):
         _abi.check(self._lib.rsp_music_device_free(self._h, ct.c_void_p(p)))
 
     def download(self, d_X, n_inst):
-        h = np.zeros((n_inst, self.K, self.N), np.complex64)
+        h = np.zeros((n_inst, self.K, self.N), self.cdtype)
         _abi.check(self._lib.rsp_music_device_download(self._h, h.ctypes.data, ct.c_void_p(d_X), h.nbytes))
         return np.ascontiguousarray(np.transpose(h, (0, 2, 1)))
 
@@ -139,12 +146,13 @@ def run_music_scene():
             np.deg2rad(np.round(np.arange(-200, 201) * 0.1, 10)), 0.0138 / wl)
 
 
-def MUSIC_1D(X1, M, phi_list=None, d_over_lambda=0.5, device=0):
+def MUSIC_1D(X1, M, phi_list=None, d_over_lambda=0.5, device=0, precision='c128'):
     """MUSIC_1D.m:26-48 on one snapshot matrix X1 [N x K]: returns (phi_e [deg], P_MUSIC_dB, EVA)."""
     X1 = np.asarray(X1)
     if phi_list is None:
         phi_list = np.linspace(-np.pi / 2, np.pi / 2, 200)   # MUSIC_1D.m:35
-    plan = MusicPlan(X1.shape[0], X1.shape[1], M, phi_list, d_over_lambda, max_batch=1, device=device)
+    plan = MusicPlan(X1.shape[0], X1.shape[1], M, phi_list, d_over_lambda, max_batch=1, device=device,
+                     precision=precision)
     try:
         o = plan.process(X1)
     finally:

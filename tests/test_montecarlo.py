@@ -16,9 +16,11 @@ copy of S9, which uses the complex ratio real((A - B) / (A + B)) (main_plot_snr_
 Checks:
   * oracle on the same seeds: at -4, 4, 12 and 24 dB the first 8 trials' noisy cubes (downloaded
     from the device) go through oracle.chain in 8 worker processes; every trial's final targets
-    must equal the device's (complex double tolerances of test_gpu_parity.py), and the device's
-    100-trial angle-error std and mean must agree with the oracle's 8-trial ones within a 99.9 %
-    two-sided F bound (variance ratio, F(99, 7)) and |z| < 4 (mean difference);
+    must equal the device's (complex double tolerances of test_gpu_parity.py), and the oracle's
+    8-seed angle-error std and mean must lie inside the central 99.9 % of the std and mean of
+    random 8-trial subsets of the device's 100 trials (a distribution-free bound: the errors are
+    heavy-tailed, set by cluster merges, so a Gaussian F test does not apply -- it failed on
+    the MI355X at one SNR where one of the first 8 trials is an outlier);
   * Pd = 1 from 0 dB up and never decreases by more than 0.1 between SNR steps; the first final
     target is the true target (|range error| < 15 m) in every detected trial from 0 dB up;
   * the angle-error std stays below the script's curve |k| sqrt(2)/sqrt(SNR) wherever Pd >= 0.9.
@@ -92,11 +94,11 @@ def _oracle_trials(plan, todo, tmpdir, workers=8):
 
 
 def test_snr_vs_angle_error(tmp_path):
-    from scipy import stats
     s = scenario('reference')
     plan = Plan(s['cfg'], s['cfar'], s['clus'], s['pre_p'])
     table = []
     dev = {}
+    dev_errs = {}
     try:
         for i, snr in enumerate(SNRS):
             tg = [dict(TRUE, SNR_dB=float(snr))]
@@ -109,6 +111,7 @@ def test_snr_vs_angle_error(tmp_path):
                     n_det += 1
                     errs.append(fin[0]['Angle'] - TRUE['ElevationAngle'])     # :274-275
                     rng_errs.append(fin[0]['Range'] - TRUE['Range'])
+            dev_errs[snr] = errs
             std = float(np.std(errs, ddof=1)) if len(errs) > 1 else float('nan')   # std(..., 'omitnan')
             theory = abs(K_PAIR5) * np.sqrt(2) / np.sqrt(10 ** (snr / 10))      # :306-308
             table.append(dict(snr_db=snr, pd=n_det / TRIALS, angle_err_std=std, theory=theory,
@@ -130,12 +133,17 @@ def test_snr_vs_angle_error(tmp_path):
                  if orc[(r['snr_db'], t)]]
             so, mo, no = float(np.std(e, ddof=1)), float(np.mean(e)), len(e)
             r.update(oracle_std=so, oracle_mean=mo, oracle_n=no)
-            lo, hi = stats.f.ppf([0.0005, 0.9995], r['n_detected'] - 1, no - 1)
-            ratio = (r['angle_err_std'] / so) ** 2
-            r.update(f_ratio=ratio, f_bounds=[float(lo), float(hi)])
-            assert lo <= ratio <= hi, r
-            z = (r['angle_err_mean'] - mo) / np.sqrt(r['angle_err_std'] ** 2 / r['n_detected'] + so ** 2 / no)
-            assert abs(z) < 4, r
+            # distribution-free bound (the errors are heavy-tailed: cluster merges, not Gaussian
+            # noise): the oracle's std / mean over its no seeds must lie inside the central
+            # 99.9 % of the std / mean of random no-trial subsets of the device's trials
+            d = np.asarray(dev_errs[r['snr_db']])
+            rng = np.random.default_rng(r['snr_db'] + 1000)
+            sub = np.stack([rng.choice(d, no, replace=False) for _ in range(20000)])
+            sd_q = np.quantile(np.std(sub, axis=1, ddof=1), [0.0005, 0.9995])
+            mu_q = np.quantile(np.mean(sub, axis=1), [0.0005, 0.9995])
+            r.update(subset_std_q=[float(x) for x in sd_q], subset_mean_q=[float(x) for x in mu_q])
+            assert sd_q[0] <= so <= sd_q[1], r
+            assert mu_q[0] <= mo <= mu_q[1], r
     finally:
         plan.close()
     print()
