@@ -466,13 +466,14 @@ __device__ __forceinline__ void fft_passes(V* buf, int rs, int nrows, const V* t
 // powers of two: divisions by them become multiply-shifts, and every LDS index is padded per
 // element (lidx of the full position).
 template <int R, bool INV, int NB, int SH, int NTHR, int L, int NS, bool CMP, int XL = 0, class V>
-__device__ __forceinline__ void shg_load(const V* buf, int rs, int nrows, const V* tw, V (&v)[NB][R]) {
+__device__ __forceinline__ void shg_load(const V* buf, int rs, int nrows, const V* tw, V (&v)[NB][R],
+                                         int tix = threadIdx.x) {
     constexpr int nb = L / R;
     static_assert(!XL || nb % 128 == 0, "XOR-swizzled input needs r nb to keep the swizzle bits");
     const int total = nb * nrows;
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
-        const int beta = threadIdx.x + t * NTHR;
+        const int beta = tix + t * NTHR;
         if (beta < total) {
             const int row = beta / nb, j = beta - row * nb;
             const V* src = XL ? buf + row * L + (j ^ ((j >> 4) & 7)) : buf + row * rs;
@@ -488,13 +489,13 @@ __device__ __forceinline__ void shg_load(const V* buf, int rs, int nrows, const 
     }
 }
 template <int R, bool INV, int NB, int SH, int NTHR, int L, int NS, int XL = 0, class V, class St>
-__device__ __forceinline__ void shg_store(V (&v)[NB][R], int rs, int nrows, const St& st) {
+__device__ __forceinline__ void shg_store(V (&v)[NB][R], int rs, int nrows, const St& st, int tix = threadIdx.x) {
     constexpr int nb = L / R;
     static_assert(!XL || (NS == 1 && R == 16), "XOR-swizzled output: Ns = 1 radix-16 passes");
     const int total = nb * nrows;
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
-        const int beta = threadIdx.x + t * NTHR;
+        const int beta = tix + t * NTHR;
         if (beta < total) {
             const int row = beta / nb, j = beta - row * nb;
             Dft<R, INV, V>::run(v[t]);
@@ -800,7 +801,10 @@ template <class T> constexpr int k1p_pts() { return sizeof(T) == 4 ? 16 : 8; }
 // cube loads of the workgroup's next tile are already in flight in registers; the DBF of that
 // tile then fills the other buffer.  HBM reads and writes overlap instead of alternating
 // round by round.  Same arithmetic as k1_dbf_mtd (mode 3).
-template <class T, int BMAX, int CP, int LGP>
+// TPWX: sub-tiles a wave loads per tile (>= the tiled K1's TPW): 2 TPW when a tile holds more
+// sub-tiles than the 8 waves cover at TPW (config #4: 32 channels x 16 beams, NT = 1 sample x
+// 256 pulses = 16 sub-tiles, TPW = 1), so that one load round still covers a tile.
+template <class T, int BMAX, int CP, int LGP, int TPWX>
 __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevConsts k, FramePtrs fp, int nf) {
     typedef cx<T> V;
     typedef Dbf<T> D;
@@ -813,7 +817,7 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
     if (TT >= total) return;
     const V* __restrict__ twPp = static_cast<const V*>(k.twPp);
     for (int i = threadIdx.x; i < g.twPp_elems; i += K1_THREADS) twl[i] = twPp[i];
-    constexpr int NJ = CP / 4, MB = BMAX <= 8 ? 1 : 2, TPW = (16 / NJ) / MB > 0 ? (16 / NJ) / MB : 1;
+    constexpr int NJ = CP / 4, MB = BMAX <= 8 ? 1 : 2, TPW = TPWX;
     constexpr int PT = 16 * D::PPL;
     const int lane = threadIdx.x & 63, grp = lane >> 4, col = lane & 15;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: nlv[] and n are scalar
@@ -827,7 +831,7 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
             aim[mb][j] = At[((mb * NJ + j) * 2 + 1) * 64 + lane];
         }
     // this lane's sub-tiles are the same for every tile: (sample nl, pulses p ..) and their
-    // window values (k1_persistent_fits guarantees one round: NT * ptiles <= waves * TPW)
+    // window values (k1_persistent_fits guarantees one round: NT * ptiles <= waves * TPWX)
     const int ptiles = P / PT, ntp = NT * ptiles;
     const T* __restrict__ win = static_cast<const T*>(k.win);
     int nlv[TPW], pv[TPW];
@@ -1133,16 +1137,16 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
         for (int r = 0; r < R0; ++r) hreg[t][r] = H[sd.H_off + j + r * nb0];   // fused pass outputs j + r M/16
     }
     V* twL = L + K2_LDS_DATA(SH);
-    for (int e = tid; e < NTWF; e += K2_THREADS) twL[e] = twl[e];
+    for (int e = threadIdx.x; e < NTWF; e += K2_THREADS) twL[e] = twl[e];
     const V* twF = twL;
     const V* twI = twF;   // palindrome: the reversed plan's table is the forward one
     constexpr int XZ = RSP_K2_XOR;   // Ns = 1 outputs XOR-swizzled (see sh_store)
-    shg_store<R0, false, NB0, SH, K2_THREADS, M, 1, XZ>(v0, rs, rows, StoreLds<V>{L});
+    shg_store<R0, false, NB0, SH, K2_THREADS, M, 1, XZ>(v0, rs, rows, StoreLds<V>{L}, tid);
     __syncthreads();
     shg_pass<R1, false, NB1, SH, K2_THREADS, M, NS1, CMP, XZ>(L, rs, rows, twF, StoreLds<V>{L});
     {
         V v[NB0][R0];
-        shg_load<R0, false, NB0, SH, K2_THREADS, M, NS2, CMP>(L, rs, rows, twF + TW2, v);
+        shg_load<R0, false, NB0, SH, K2_THREADS, M, NS2, CMP>(L, rs, rows, twF + TW2, v, tid);
         __syncthreads();
 #pragma unroll
         for (int t = 0; t < NB0; ++t) {
@@ -1150,19 +1154,20 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
 #pragma unroll
             for (int r = 0; r < R0; ++r) v[t][r] = vmul(v[t][r], hreg[t][r]);
         }
-        shg_store<R0, true, NB0, SH, K2_THREADS, M, 1, XZ>(v, rs, rows, StoreLds<V>{L});
+        shg_store<R0, true, NB0, SH, K2_THREADS, M, 1, XZ>(v, rs, rows, StoreLds<V>{L}, tid);
         __syncthreads();
     }
     shg_pass<R1, true, NB1, SH, K2_THREADS, M, NS1, CMP, XZ>(L, rs, rows, twI, StoreLds<V>{L});
     const int gend = min(sd.gb, g0 + sd.V);
     {
         V v[NB0][R0];
-        shg_load<R0, true, NB0, SH, K2_THREADS, M, NS2, CMP>(L, rs, rows, twI + TW2, v);
+        shg_load<R0, true, NB0, SH, K2_THREADS, M, NS2, CMP>(L, rs, rows, twI + TW2, v, tid);
         shg_store<R0, true, NB0, SH, K2_THREADS, M, NS2>(
             v, rs, rows,
             StoreRdm<V>{buf_rsrc(rdm, (unsigned)(rows_total * G * sizeof(V))),
                         buf_rsrc(mag, (unsigned)(rows_total * g.Gp * sizeof(T))), G, g.Gp, row0, rows_total, Lh1, g0,
-                        gend});
+                        gend},
+            tid);
     }
 }
 
@@ -1926,11 +1931,17 @@ static int k1_tpw(const Geometry& g) {
 }
 static size_t k1p_lds(const Geometry& g) { return ((size_t)2 * g.B * g.NT * g.Ppad + g.P) * cplx_bytes(g); }
 
-bool k1_persistent_fits(const Geometry& g) {
+// sub-tiles per wave of the persistent K1 (one load round per tile): TPW, or 2 TPW
+static int k1p_tpw(const Geometry& g) {
     const int pt = g.prec == RSP_PREC_F64 ? 16 : 32;   // pulses per MFMA sub-tile
+    const int need = (g.NT * (g.P / pt) + (K1_THREADS / 64) - 1) / (K1_THREADS / 64);
+    return need <= k1_tpw(g) ? k1_tpw(g) : (need <= 2 * k1_tpw(g) ? 2 * k1_tpw(g) : 0);
+}
+
+bool k1_persistent_fits(const Geometry& g) {
     const int pts = g.prec == RSP_PREC_F64 ? 8 : 16;   // FFT points per thread (k1p_pts)
-    return g.pow2P && g.logP >= 6 && g.logP <= 8 && g.NT * (g.P / pt) <= (K1_THREADS / 64) * k1_tpw(g) &&
-           k1p_lds(g) <= 160 * 1024 && g.B * g.NT * g.P <= pts * K1_THREADS && g.ncu > 0 && !g.k1_tiled;
+    return g.pow2P && g.logP >= 6 && g.logP <= 8 && k1p_tpw(g) > 0 && k1p_lds(g) <= 160 * 1024 &&
+           g.B * g.NT * g.P <= pts * K1_THREADS && g.ncu > 0 && !g.k1_tiled;
 }
 
 template <class T, int BMAX, int CP>
@@ -1940,17 +1951,19 @@ static hipError_t launch_k1_t(const Geometry& g, const DevConsts& k, const Frame
         // one FFT size per instantiation keeps the prefetch registers + FFT under 256 VGPRs
         const size_t ldsp = k1p_lds(g);
         const int grid = std::min(g.ncu, nf * g.ntiles);
-#define K1P_LAUNCH(LGP)                                                                                        \
-    do {                                                                                                       \
-        hipError_t e = allow_lds(k1p_dbf_mtd<T, BMAX, CP, LGP>, ldsp);                                         \
-        if (e != hipSuccess) return e;                                                                         \
-        hipLaunchKernelGGL((k1p_dbf_mtd<T, BMAX, CP, LGP>), dim3(grid), dim3(K1_THREADS), ldsp, s, g, k, fp, nf); \
-        return hipGetLastError();                                                                              \
+        constexpr int NJ = CP / 4, MB = BMAX <= 8 ? 1 : 2, TPW = (16 / NJ) / MB > 0 ? (16 / NJ) / MB : 1;
+        const bool twice = k1p_tpw(g) == 2 * TPW;
+#define K1P_LAUNCH(LGP, TW)                                                                                      \
+    do {                                                                                                         \
+        hipError_t e = allow_lds(k1p_dbf_mtd<T, BMAX, CP, LGP, TW>, ldsp);                                       \
+        if (e != hipSuccess) return e;                                                                           \
+        hipLaunchKernelGGL((k1p_dbf_mtd<T, BMAX, CP, LGP, TW>), dim3(grid), dim3(K1_THREADS), ldsp, s, g, k, fp, nf); \
+        return hipGetLastError();                                                                                \
     } while (0)
         switch (g.logP) {
-            case 6: K1P_LAUNCH(6);
-            case 7: K1P_LAUNCH(7);
-            case 8: K1P_LAUNCH(8);
+            case 6: if (twice) K1P_LAUNCH(6, 2 * TPW); else K1P_LAUNCH(6, TPW);
+            case 7: if (twice) K1P_LAUNCH(7, 2 * TPW); else K1P_LAUNCH(7, TPW);
+            case 8: if (twice) K1P_LAUNCH(8, 2 * TPW); else K1P_LAUNCH(8, TPW);
             default: break;
         }
 #undef K1P_LAUNCH
