@@ -758,8 +758,8 @@ __global__ __launch_bounds__(MU_THREADS, 2) void k_music_cov64(int N, int K, con
 //     forms v_k (zlarfg) and keeps it; p = tau A v (lane = column, A Hermitian), w = p - tau/2
 //     (p^H v) v, A -= v w^H + w v^H -- three barriers per step.
 //  2. All eigenvalues of T by multisection, quad i -> the i-th smallest: the 4 lanes evaluate
-//     the Sturm count (LAPACK dstebz recurrence with pivmin) at 4 interior points, 24 rounds
-//     shrink the Gershgorin interval by 5^24 (below the rounding of the eigenvalue).
+//     the Sturm count (LAPACK dstebz recurrence with pivmin) at 4 interior points, 23 rounds
+//     shrink the Gershgorin interval by 5^23 > 2^53 (to the rounding of the eigenvalue).
 //  3. The M signal eigenvectors of T by inverse iteration (dlagtf / dlagts, lane j = vector j,
 //     3 solves with modified Gram-Schmidt) in wave 0, then q_j = H_0 ... H_{n-2} y_j, the
 //     reflectors applied by their own quads.
@@ -767,7 +767,7 @@ __global__ __launch_bounds__(MU_THREADS, 2) void k_music_cov64(int N, int K, con
 //  5. P = 1 ./ den, P_dB = 10 log10(P / max P), findpeaks + the M largest (MUSIC_1D.m:37-47).
 // ---------------------------------------------------------------------------------------
 #define ME_THREADS 256
-#define ME_SECT 24   // multisection rounds: 5^24 > 2^55
+#define ME_SECT 23   // multisection rounds: 5^23 > 2^53
 #ifndef ME_WPS
 #define ME_WPS 4     // waves per SIMD the register budget is sized for (4 instances per CU)
 #endif
@@ -780,7 +780,11 @@ template <int M>
 __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S, const double2* __restrict__ R,
                                                           const double2* __restrict__ S1T, int Spad,
                                                           double* __restrict__ spec_db, double* __restrict__ eig_out,
-                                                          int* __restrict__ peaks_out) {
+                                                          int* __restrict__ peaks_out, unsigned long long* __restrict__ trace) {
+    // trace (diagnostic builds, RSP_MUSIC_TRACE=1): s_memrealtime at the phase boundaries
+#define ME_STAMP(ix) \
+    if (trace && threadIdx.x == 0) trace[(size_t)blockIdx.x * 8 + (ix)] = wall_clock64()
+    ME_STAMP(0);
     extern __shared__ __attribute__((aligned(16))) double2 lds64[];
     double2* vb = lds64;                 // [2][64] v of the step (double-buffered by k parity)
     double2* wb = vb + 128;              // [2][64] w
@@ -855,13 +859,21 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
         __syncthreads();
         const double2 tau = taus[k];
         if (tau.x == 0.0 && tau.y == 0.0) continue;   // H_k = I (uniform)
+        // columns <= k are finished: their quads (whole waves, late in the reduction) skip the work
         const bool act = i > k && i < n;
         double2 p = z2;
+        if (act) {   // uniform per quad
+            double px = 0.0, py = 0.0;
 #pragma unroll
-        for (int u = 0; u < 16; ++u) p = zadd(p, zmc(a[u], vk[16 * q + u]));   // sum_j conj(A(j,i)) v_j
-        p.x = qsumd(p.x);
-        p.y = qsumd(p.y);
-        p = act ? zm(tau, p) : z2;
+            for (int u = 0; u < 16; ++u) {   // sum_j conj(A(j,i)) v_j
+                const double2 vj = vk[16 * q + u];
+                px = fma(a[u].x, vj.x, fma(a[u].y, vj.y, px));
+                py = fma(a[u].x, vj.y, fma(-a[u].y, vj.x, py));
+            }
+            px = qsumd(px);
+            py = qsumd(py);
+            p = zm(tau, make_double2(px, py));
+        }
         const double2 vi = vk[i];
         double2 pv = q == 0 ? zmc(p, vi) : z2;                                  // p^H v
         pv.x = wsumd(pv.x);
@@ -873,12 +885,21 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
         const double2 wi = act ? zadd(p, zm(alpha, vi)) : z2;
         if (q == 0) wk[i] = wi;
         __syncthreads();
-        if (act) {   // A(j, i) -= v_j conj(w_i) + w_j conj(v_i) (v_j = w_j = 0 for j <= k)
-            const double2 cw = zconj(wi), cv = zconj(vi);
+        if (act) {   // A(j, i) -= v_j conj(w_i) + w_j conj(v_i) (v_j = w_j = 0 for j <= k): 8 FMAs
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
                 const int j = 16 * q + u;
-                a[u] = zsub(a[u], zadd(zm(vk[j], cw), zm(wk[j], cv)));
+                const double2 vj = vk[j], wj = wk[j];
+                double ax = a[u].x, ay = a[u].y;
+                ax = fma(-vj.x, wi.x, ax);
+                ax = fma(-vj.y, wi.y, ax);
+                ax = fma(-wj.x, vi.x, ax);
+                ax = fma(-wj.y, vi.y, ax);
+                ay = fma(-vj.y, wi.x, ay);
+                ay = fma(vj.x, wi.y, ay);
+                ay = fma(-wj.y, vi.x, ay);
+                ay = fma(wj.x, vi.y, ay);
+                a[u] = make_double2(ax, ay);
             }
         }
     }
@@ -891,6 +912,7 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
         if (i == n - 1 && q == 0) dd[n - 1] = dl;
     }
     __syncthreads();
+    ME_STAMP(1);
     // ---- 2. eigenvalues by multisection (quad i -> the i-th smallest)
     {
         double glo = 1.0e300, ghi = -1.0e300, emax = 0.0;
@@ -909,8 +931,7 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
             int c = qv < 0.0;
             for (int r = 1; r < n; ++r) {
                 double rc = __builtin_amdgcn_rcp(qv);
-                rc = fma(fma(-qv, rc, 1.0), rc, rc);   // one Newton step: e2 / q to about an ulp
-                rc = fma(fma(-qv, rc, 1.0), rc, rc);
+                rc = fma(fma(-qv, rc, 1.0), rc, rc);   // one Newton step: 1 / q to about an ulp
                 qv = (dd[r] - x) - e2[r - 1] * rc;
                 if (fabs(qv) < pivmin) qv = -pivmin;
                 c += qv < 0.0;
@@ -933,6 +954,7 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
         }
     }
     __syncthreads();
+    ME_STAMP(2);
     // ---- 3. signal eigenvectors of T: inverse iteration in wave 0 (lane j = vector j, then
     //         lane = component)
     if (w == 0) {
@@ -1005,6 +1027,7 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
         for (int j = 0; j < M; ++j) Qs[j * 64 + lane] = make_double2(lane < n ? lu[(4 * 64 + lane) * M + j] : 0.0, 0.0);
     }
     __syncthreads();
+    ME_STAMP(3);
     // q_j = H_0 H_1 ... H_{n-2} y_j, k descending: the reflectors of wave wv's 16 columns are
     // applied by wave wv with lane = row and the M vectors in registers (a wave's turn starts and
     // ends with them in Qs); v_k passes from its quad to the wave through a 1 KB LDS buffer
@@ -1034,6 +1057,7 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
         }
         __syncthreads();
     }
+    ME_STAMP(4);
     // ---- 4. den(s) = |a(s) - Q_s (Q_s^H a(s))|^2, lane = angle
     for (int s = t; s < S; s += ME_THREADS) {
         double2 cf[M];
@@ -1054,6 +1078,7 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
         den[s] = r2;
     }
     __syncthreads();
+    ME_STAMP(5);
     // ---- 5. P = 1 ./ den, P_dB = 10 log10(P / max P) (MUSIC_1D.m:37-41)
     double pm = 0.0;
     for (int s = t; s < S; s += ME_THREADS) pm = fmax(pm, 1.0 / den[s]);
@@ -1120,6 +1145,8 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
     }
     if (t == 0)
         for (int rk = M; rk < MU_MMAX; ++rk) po[1 + rk] = 0;
+    ME_STAMP(6);
+#undef ME_STAMP
 }
 
 }  // namespace
@@ -1166,7 +1193,7 @@ hipError_t launch_eig64(rsp_music_plan* p, int n_inst) {
     }
     hipLaunchKernelGGL(k_music_eig64<MC>, dim3(n_inst), dim3(ME_THREADS), lds, p->stream, p->N, p->S,
                        (const double2*)p->d_R, (const double2*)p->d_S1T, p->Spad, (double*)p->d_spec,
-                       (double*)p->d_eig, p->d_peaks);
+                       (double*)p->d_eig, p->d_peaks, p->d_trace);
     return hipGetLastError();
 }
 
@@ -1449,7 +1476,8 @@ int32_t rsp_music_profile(rsp_music_plan* p, const void* d_X, int32_t n_inst, in
         double ph[6] = {0, 0, 0, 0, 0, 0};
         for (int i = 0; i < n_inst; ++i)
             for (int q = 0; q < 6; ++q) ph[q] += (double)(t[(size_t)i * 8 + q + 1] - t[(size_t)i * 8 + q]) * 0.01 / n_inst;
-        fprintf(stderr, "k_music_eig phases (us/instance): tridiag %.2f bisect %.2f inviter %.2f backxf %.2f spectrum %.2f peaks %.2f\n",
+        fprintf(stderr, "k_music_eig%s phases (us/instance): tridiag %.2f eigenvalues %.2f inviter %.2f backxf %.2f spectrum %.2f peaks %.2f\n",
+                p->f64 ? "64" : "",
                 ph[0], ph[1], ph[2], ph[3], ph[4], ph[5]);
     }
     return RSP_OK;

@@ -1,4 +1,4 @@
-"""Stage timing of the MUSIC path at BASELINE config #5 (usage: music_prof.py [n_inst] [iters]).
+"""Stage timing of the MUSIC path at BASELINE config #5 (usage: music_prof.py [n_inst] [iters] [c128|c64]).
 
 Synthesises n_inst instances of the MUSIC_1D.m scene (64 channels x 1024 snapshots) on the
 device, then times k_music_cov and k_music_eig with HIP events (rsp_music_profile) and prints
@@ -12,20 +12,24 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, 'radar-signal-simulation-and-target-detection_amd'))
 
+if os.environ.get('AB_LIB'):   # timing experiments only: an A/B variant of librsp.so
+    from rsp import _abi  # noqa: E402
+    _abi.LIB_PATH = os.environ['AB_LIB']
 from rsp.music import MusicPlan, music_1d_scene  # noqa: E402
 
 n_inst = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+prec = sys.argv[3] if len(sys.argv) > 3 else 'c128'
 N, K, M = 64, 1024, 3
 scene, scan, dl = music_1d_scene()
-plan = MusicPlan(N, K, M, scan, dl, max_batch=n_inst)
+plan = MusicPlan(N, K, M, scan, dl, max_batch=n_inst, precision=prec)
 d_X = plan.device_alloc(n_inst)
 plan.synthesize_device(d_X, scene, n_inst, inst0=0, seed=20250101)
 plan.process_device(d_X, n_inst, fetch=False)
 pr = plan.profile(d_X, n_inst, iters=iters)
 flops = 8.0 * N * (N + 1) / 2 * K * n_inst
-bytes_ = 8.0 * N * K * n_inst
-pr.update(n_inst=n_inst, cov_tflops=flops / (pr['cov_ms'] * 1e-3) / 1e12,
+bytes_ = (16.0 if prec == 'c128' else 8.0) * N * K * n_inst
+pr.update(n_inst=n_inst, precision=prec, cov_tflops=flops / (pr['cov_ms'] * 1e-3) / 1e12,
           cov_GBps=bytes_ / (pr['cov_ms'] * 1e-3) / 1e9, inst_per_s=n_inst / ((pr['cov_ms'] + pr['eig_ms']) * 1e-3))
 print(json.dumps(pr))
 plan.device_free(d_X)
