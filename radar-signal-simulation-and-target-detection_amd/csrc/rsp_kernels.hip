@@ -943,6 +943,52 @@ struct StoreRdm {   // last inverse pass: keep outputs i in [Lh-1, Lh-1+V) that 
         buf_st1(mag, ok ? (unsigned)(rho * Gp + gg) * (unsigned)sizeof(scal<V>) : RSP_OOB, cmag(x));
     }
 };
+// The same for a pass whose wave covers one row (nb >= 64, one butterfly per thread): the row's
+// kept gates [g0, gend) get their own buffer resources (scalar), so the output's offset
+// (o - Lh1) masks both ends by itself -- o < Lh1 wraps past num_records, o - Lh1 >= gend - g0
+// is past it -- and a row beyond rows_total has num_records 0.  One VALU add per store.
+// (Skipping |x| of the discarded outputs behind a branch measured +9 us per 8 x2 frames.)
+template <class V>
+struct StoreRdmW {
+    typedef scal<V> S;
+    V* rdm; S* mag; int G; int Gp; int row0; int rows_total; int Lh1; int g0; int gend;
+    __device__ __forceinline__ void put(int, int row, int o, int, V x) const {
+        const int rho = row0 + __builtin_amdgcn_readfirstlane(row);
+        const unsigned n = rho < rows_total ? (unsigned)(gend - g0) : 0u;
+        const __amdgpu_buffer_rsrc_t rr = buf_rsrc(rdm + (size_t)rho * G + g0, n * (unsigned)sizeof(V));
+        const __amdgpu_buffer_rsrc_t mr = buf_rsrc(mag + (size_t)rho * Gp + g0, n * (unsigned)sizeof(S));
+        // (o - Lh1) * size, written so that o's constant part folds into one add per store
+        buf_st<RSP_RDM_AUX>(rr, (unsigned)o * (unsigned)sizeof(V) - (unsigned)Lh1 * (unsigned)sizeof(V), x);
+        buf_st1(mr, (unsigned)o * (unsigned)sizeof(S) - (unsigned)Lh1 * (unsigned)sizeof(S), cmag(x));
+    }
+};
+
+// Samples [lo, hi] of row (b, v) of one segment as one buffer window: z's element index is
+// increasing in the compacted sample n' (tile-major, slot-minor), so a resource based at
+// n' = off (sample lo) that spans n' = off + hi - lo masks every sample outside [lo, hi] --
+// below wraps past num_records, above is past it.  rel(n') = the byte offset of n' in the
+// window (may wrap); zrow_window() returns the resource (num_records 0 for rows past
+// rows_total, which are uniform per wave here).
+struct ZWin {
+    __amdgpu_buffer_rsrc_t r;
+    int e_lo, PNT, lgNT, NT1;
+    __device__ __forceinline__ int rel(int np) const { return (np >> lgNT) * PNT + (np & NT1) - e_lo; }
+};
+template <class V>
+__device__ __forceinline__ ZWin zrow_window(const Geometry& g, const V* z, int rho, int rows_total, int off, int lo,
+                                            int hi) {
+    ZWin w;
+    const int b = rho / g.P, v = rho - b * g.P;
+    w.lgNT = ilog2(g.NT);
+    w.NT1 = g.NT - 1;
+    w.PNT = g.P * g.NT;
+    const int nph = off + hi - lo;
+    w.e_lo = (off >> w.lgNT) * w.PNT + (off & w.NT1);
+    const int e_hi = (nph >> w.lgNT) * w.PNT + (nph & w.NT1);
+    const V* base = z + ((size_t)b * g.ntiles * g.P + v) * g.NT + w.e_lo;
+    w.r = buf_rsrc(base, rho < rows_total ? (unsigned)(e_hi - w.e_lo + 1) * (unsigned)sizeof(V) : 0u);
+    return w;
+}
 
 // LDS pad of the overlap-save rows: one complex per 32.  For 16-B elements this keeps every
 // ds_read_b128 of a pass conflict-free (a pad per 16 would shift lanes 20-27 of a lane group
@@ -1003,9 +1049,26 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     // pass-0 butterflies and its 16 filter-spectrum values (for the fused middle pass)
     V v0[NB0][R0];
     const int lgNT = ilog2(g.NT);
+    // one row per wave (nb0 a multiple of 64, one butterfly per thread): the row's sample window
+    // is a scalar buffer resource, and a load's offset needs no mask
+    constexpr bool WROW = nb0 >= 64 && NB0 == 1;
+    if constexpr (WROW) {
+        const int rl = __builtin_amdgcn_readfirstlane(tid / nb0);
+        const ZWin zw = zrow_window(g, z, row0 + rl, rows_total, off, lo, hi);
+        const int j = tid & (nb0 - 1);
+        const int np0 = a + j - lo + off;
+        if ((nb0 & (g.NT - 1)) == 0) {   // uniform: element r sits r (nb0 P) past element 0
+            const unsigned e0 = (unsigned)zw.rel(np0) * (unsigned)sizeof(V), st = (unsigned)(nb0 * P) * (unsigned)sizeof(V);
+#pragma unroll
+            for (int r = 0; r < R0; ++r) v0[0][r] = buf_ld<V>(zw.r, e0 + r * st);
+        } else {
+#pragma unroll
+            for (int r = 0; r < R0; ++r) v0[0][r] = buf_ld<V>(zw.r, (unsigned)zw.rel(np0 + r * nb0) * (unsigned)sizeof(V));
+        }
+    }
     const __amdgpu_buffer_rsrc_t zr = buf_rsrc(z, (unsigned)(g.B * g.ntiles * P * g.NT * sizeof(V)));
 #pragma unroll
-    for (int t = 0; t < NB0; ++t) {
+    for (int t = 0; t < (WROW ? 0 : NB0); ++t) {
         const int beta = tid + t * K2_THREADS;
         const int rl = beta / nb0, j = beta & (nb0 - 1);
         const int rho = row0 + rl;
@@ -1035,11 +1098,12 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     // thread have the same j (different rows), so only the distinct ones are loaded
     constexpr int NHT = (M / RL) / K2_THREADS >= NBL ? NBL : ((M / RL) / K2_THREADS > 0 ? (M / RL) / K2_THREADS : 1);
     V hreg[NHT * RL];
+    const __amdgpu_buffer_rsrc_t hr = buf_rsrc(H + sd.H_off, (unsigned)(M * sizeof(V)));
 #pragma unroll
     for (int t = 0; t < NHT; ++t) {
         const int j = (tid + t * K2_THREADS) & (M / RL - 1);   // last pass: Ns = nb = M / RL, idxD = j
 #pragma unroll
-        for (int r = 0; r < RL; ++r) hreg[t * RL + r] = H[sd.H_off + j + r * (M / RL)];
+        for (int r = 0; r < RL; ++r) hreg[t * RL + r] = buf_ld<V>(hr, (unsigned)(j + r * (M / RL)) * (unsigned)sizeof(V));
     }
     constexpr int NTWF = tw_total(LGM, false, CMP, PAL);
     V* twL = L + K2_LDS_DATA(SH);
@@ -1072,11 +1136,16 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     // inverse passes 1 .. NP-1 (reversed radices); the last keeps the valid overlap-save
     // outputs = stitched gates
     const int gend = min(sd.gb, g0 + sd.V);
-    fft_range<LGM, 1, NP, RBL, 16, true, true, SH, K2_THREADS, CMP, PAL, XZ>(
-        L, rs, rows, twI, StoreLds<V>{L},
-        StoreRdm<V>{buf_rsrc(rdm, (unsigned)(rows_total * G * sizeof(V))),
-                    buf_rsrc(mag, (unsigned)(rows_total * g.Gp * sizeof(T))), G, g.Gp, row0, rows_total, Lh1, g0,
-                    gend});
+    // the inverse FFT's last pass runs the forward pass 0's radix (R0) over nb0 butterflies
+    if constexpr (WROW)
+        fft_range<LGM, 1, NP, RBL, 16, true, true, SH, K2_THREADS, CMP, PAL, XZ>(
+            L, rs, rows, twI, StoreLds<V>{L}, StoreRdmW<V>{rdm, mag, G, g.Gp, row0, rows_total, Lh1, g0, gend});
+    else
+        fft_range<LGM, 1, NP, RBL, 16, true, true, SH, K2_THREADS, CMP, PAL, XZ>(
+            L, rs, rows, twI, StoreLds<V>{L},
+            StoreRdm<V>{buf_rsrc(rdm, (unsigned)(rows_total * G * sizeof(V))),
+                        buf_rsrc(mag, (unsigned)(rows_total * g.Gp * sizeof(T))), G, g.Gp, row0, rows_total, Lh1, g0,
+                        gend});
 }
 
 
@@ -1113,28 +1182,27 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
     const int a = sd.seg_lo + g0 - Lh1;
     const V* twl = static_cast<const V*>(k.twM) + sd.tw_off;
     const V* __restrict__ H = static_cast<const V*>(k.H);
+    static_assert(rows == 1 && NB0 == 1, "one row per workgroup, one radix-16 butterfly per thread");
     V v0[NB0][R0];
     V hreg[NB0][R0];
-    const int lgNT = ilog2(g.NT);
-    const __amdgpu_buffer_rsrc_t zr = buf_rsrc(z, (unsigned)(g.B * g.ntiles * P * g.NT * sizeof(V)));
-#pragma unroll
-    for (int t = 0; t < NB0; ++t) {
-        const int beta = tid + t * K2_THREADS;
-        const int rl = beta / nb0, j = beta - rl * nb0;
-        const int rho = row0 + rl;
-        const bool live = beta < nb0 * rows && rho < rows_total;
-        const int b = rho / P, v = rho - b * P;
+    // threads nb0.. have no radix-16 butterfly (waves past nb0 skip the loads); the row's samples
+    // are one scalar buffer window (zrow_window), so the loads need no masks
+    if (tid < nb0) {
+        const ZWin zw = zrow_window(g, z, row0, rows_total, off, lo, hi);
+        const int j = tid;
         const int np0 = a + j - lo + off;
-        const int zb = ((b * g.ntiles + (np0 >> lgNT)) * P + v) * g.NT + (np0 & (g.NT - 1));
+        if ((nb0 & (g.NT - 1)) == 0) {   // uniform
+            const unsigned e0 = (unsigned)zw.rel(np0) * (unsigned)sizeof(V), st = (unsigned)(nb0 * P) * (unsigned)sizeof(V);
 #pragma unroll
-        for (int r = 0; r < R0; ++r) {
-            const int n = a + j + r * nb0;
-            const bool ok = live && n >= lo && n <= hi;
-            const unsigned e = ((nb0 & (g.NT - 1)) == 0) ? (unsigned)(zb + r * nb0 * P) : (unsigned)zaddr(g, b, v, n - lo + off);
-            v0[t][r] = buf_ld<V>(zr, ok ? e * (unsigned)sizeof(V) : RSP_OOB);
+            for (int r = 0; r < R0; ++r) v0[0][r] = buf_ld<V>(zw.r, e0 + r * st);
+        } else {
+#pragma unroll
+            for (int r = 0; r < R0; ++r) v0[0][r] = buf_ld<V>(zw.r, (unsigned)zw.rel(np0 + r * nb0) * (unsigned)sizeof(V));
         }
+        const __amdgpu_buffer_rsrc_t hr = buf_rsrc(H + sd.H_off, (unsigned)(M * sizeof(V)));
 #pragma unroll
-        for (int r = 0; r < R0; ++r) hreg[t][r] = H[sd.H_off + j + r * nb0];   // fused pass outputs j + r M/16
+        for (int r = 0; r < R0; ++r)   // fused pass outputs j + r M/16
+            hreg[0][r] = buf_ld<V>(hr, (unsigned)(j + r * nb0) * (unsigned)sizeof(V));
     }
     V* twL = L + K2_LDS_DATA(SH);
     for (int e = threadIdx.x; e < NTWF; e += K2_THREADS) twL[e] = twl[e];
@@ -1163,11 +1231,7 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
         V v[NB0][R0];
         shg_load<R0, true, NB0, SH, K2_THREADS, M, NS2, CMP>(L, rs, rows, twI + TW2, v, tid);
         shg_store<R0, true, NB0, SH, K2_THREADS, M, NS2>(
-            v, rs, rows,
-            StoreRdm<V>{buf_rsrc(rdm, (unsigned)(rows_total * G * sizeof(V))),
-                        buf_rsrc(mag, (unsigned)(rows_total * g.Gp * sizeof(T))), G, g.Gp, row0, rows_total, Lh1, g0,
-                        gend},
-            tid);
+            v, rs, rows, StoreRdmW<V>{rdm, mag, G, g.Gp, row0, rows_total, Lh1, g0, gend}, tid);
     }
 }
 
@@ -1190,6 +1254,10 @@ __global__ __launch_bounds__(K2_THREADS, 512 / K2_THREADS) void k2_pc(Geometry g
     const int lo = sd.lo, hi = sd.hi, off = sd.off;
     const int tid = threadIdx.x;
 
+#ifdef RSP_K2_CENSUS   // instruction-census builds (-S only): one job type per kernel
+    if (RSP_K2_CENSUS == 1) { k2_fft_job_mix<T, 2560, 10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); return; }
+    if (RSP_K2_CENSUS == 2) { k2_fft_job<T, 10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); return; }
+#endif
     if (sd.type == 1 && sd.logM == 0) {   // mixed-radix block
         k2_fft_job_mix<T, 2560, 10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L);
     } else if (sd.type == 1) {

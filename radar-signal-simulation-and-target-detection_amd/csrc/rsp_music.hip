@@ -817,20 +817,17 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
         double2* vk = vb + 64 * (k & 1);
         double2* wk = wb + 64 * (k & 1);
         if (w == (k >> 4)) {   // the wave holding column k (uniform)
-            const bool mine = i == k;
-            double xn = 0.0, dk = 0.0;
-            double2 al = z2;
+            // column k through LDS (wk of this step is free until its w is written): lane = row
+            double2* cb = wk;
+            if (i == k) {
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const int j = 16 * q + u;
-                if (mine && j >= k + 2 && j < n) xn += a[u].x * a[u].x + a[u].y * a[u].y;
-                if (mine && j == k + 1) al = a[u];
-                if (mine && j == k) dk = a[u].x;
+                for (int u = 0; u < 16; ++u) cb[16 * q + u] = a[u];
             }
-            xn = qsumd(xn);
-            al.x = qsumd(al.x);
-            al.y = qsumd(al.y);
-            dk = qsumd(dk);
+            wsync();
+            const double2 c = cb[lane];
+            const double xn = wsumd(lane >= k + 2 ? c.x * c.x + c.y * c.y : 0.0);   // rows >= n are 0
+            const double2 al = make_double2(rdld(c.x, k + 1), rdld(c.y, k + 1));
+            const double dk = rdld(c.x, k);
             double2 tau = z2, scale = z2;
             double beta = al.x;
             if (xn > 0.0 || al.y != 0.0) {   // zlarfg
@@ -840,23 +837,19 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
                 const double qd = 1.0 / (dn.x * dn.x + dn.y * dn.y);
                 scale = make_double2(dn.x * qd, -dn.y * qd);
             }
-            if (mine) {
-#pragma unroll
-                for (int u = 0; u < 16; ++u) {
-                    const int j = 16 * q + u;
-                    const double2 v = j == k + 1 ? make_double2(1.0, 0.0) : (j >= k + 2 && j < n ? zm(a[u], scale) : z2);
-                    a[u] = v;   // column k keeps v_k for the back-transformation
-                    vk[j] = v;
-                }
-                if (q == 0) {
-                    taus[k] = tau;
-                    dd[k] = dk;
-                    ee[k] = beta;
-                    e2[k] = beta * beta;
-                }
+            vk[lane] = lane == k + 1 ? make_double2(1.0, 0.0) : (lane >= k + 2 ? zm(c, scale) : z2);
+            if (lane == 0) {
+                taus[k] = tau;
+                dd[k] = dk;
+                ee[k] = beta;
+                e2[k] = beta * beta;
             }
         }
         __syncthreads();
+        if (w == (k >> 4) && i == k) {   // column k keeps v_k for the back-transformation
+#pragma unroll
+            for (int u = 0; u < 16; ++u) a[u] = vk[16 * q + u];
+        }
         const double2 tau = taus[k];
         if (tau.x == 0.0 && tau.y == 0.0) continue;   // H_k = I (uniform)
         // columns <= k are finished: their quads (whole waves, late in the reduction) skip the work
