@@ -81,6 +81,12 @@ __device__ __forceinline__ double cmag(d2 x) {
 
 // Raw buffer resources (SRSRC): 32-bit byte offsets and hardware range checking.  An offset at
 // or past num_records reads 0 / drops the store, so masked lanes need no branch or select.
+// The read/write barrier inside an LDS pass (RSP_K2_NOWAR: timing-only builds without it)
+#ifndef RSP_K2_NOWAR
+#define RSP_WAR_SYNC() __syncthreads()
+#else
+#define RSP_WAR_SYNC() ((void)0)
+#endif
 #define RSP_OOB 0x80000000u   // > any buffer this library makes (plans are validated < 2 GB/frame)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, unsigned bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
@@ -429,7 +435,7 @@ template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP
 __device__ __forceinline__ void sh_pass(V* buf, int rs, int nrows, const V* tw, const St& st) {
     V v[NB][R];
     sh_load<R, INV, NB, SH, NTHR, LGL, LGNS, CMP, XL>(buf, rs, nrows, tw, v);
-    __syncthreads();
+    RSP_WAR_SYNC();
     sh_store<R, INV, NB, SH, NTHR, LGL, LGNS>(v, rs, nrows, st);
     __syncthreads();
 }
@@ -516,7 +522,7 @@ template <int R, bool INV, int NB, int SH, int NTHR, int L, int NS, bool CMP, in
 __device__ __forceinline__ void shg_pass(V* buf, int rs, int nrows, const V* tw, const St& st) {
     V v[NB][R];
     shg_load<R, INV, NB, SH, NTHR, L, NS, CMP, XL>(buf, rs, nrows, tw, v);
-    __syncthreads();
+    RSP_WAR_SYNC();
     shg_store<R, INV, NB, SH, NTHR, L, NS>(v, rs, nrows, st);
     __syncthreads();
 }
@@ -1123,7 +1129,7 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
         V v[NBL][RL];
         sh_load<RL, false, NBL, SH, K2_THREADS, LGM, LGM - RBL, CMP>(L, rs, rows,
                                                                       twF + tw_pass_off(LGM, NP - 1, false, CMP, PAL), v);
-        __syncthreads();
+        RSP_WAR_SYNC();
 #pragma unroll
         for (int t = 0; t < NBL; ++t) {
             Dft<RL, false, V>::run(v[t]);
@@ -1215,7 +1221,7 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
     {
         V v[NB0][R0];
         shg_load<R0, false, NB0, SH, K2_THREADS, M, NS2, CMP>(L, rs, rows, twF + TW2, v, tid);
-        __syncthreads();
+        RSP_WAR_SYNC();
 #pragma unroll
         for (int t = 0; t < NB0; ++t) {
             Dft<R0, false, V>::run(v[t]);

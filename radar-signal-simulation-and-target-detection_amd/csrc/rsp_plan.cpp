@@ -1037,27 +1037,35 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
         (rc = p->upload(&dang, ang)) || (rc = p->upload(&dkl, kl)))
         return bail(rc);
     k.range_axis = dra; k.velocity_axis = dva; k.beam_angles = dang; k.klut = dkl;
-    {   // K2 dispatch order.  (1) Workgroups 2i and 2i+1 of a job (adjacent rows) form pair i, at
-        // key (i + 1/2) / npairs_j, so that the narrow FIR, medium and long jobs are interleaved in
-        // proportion through the launch.  (2) Workgroups go to the 8 XCDs round-robin by
-        // dispatch position, so the pairs are laid out 8 at a time: positions 16c + x and
-        // 16c + 8 + x hold pair 8c + x -- both rows of a pair on one XCD, whose L2 then serves
-        // the second half of every 128-B z line the first one fetched (a one-row overlap-save
-        // workgroup reads 64 B per line).  Unpaired workgroups go last.
-        struct Pr { double key; int a, b; };
-        std::vector<Pr> pr;
+    {   // K2 dispatch order.  (1) Workgroups of a job covering adjacent rows form groups of gs
+        // (below), at key (i + 1/2) / ngroups_j, so that the narrow FIR, medium and long jobs are
+        // interleaved in proportion through the launch.  (2) Workgroups go to the 8 XCDs
+        // round-robin by dispatch position, so the groups are laid out 8 at a time: positions
+        // 8 (gs c + m) + x hold member m of group 8c + x -- every row of a group on one XCD, whose
+        // L2 then serves the rest of every 128-B z line the first one fetched.  A z line holds
+        // 128 / (NT esz) adjacent rows, a workgroup rows_per_wg of them, so gs = the most
+        // workgroups one line spans over the jobs (x2: NT = 4, one-row long blocks -> 2; x4:
+        // NT = 1 -> 8).  Workgroups left over go last.
+        const int esz = 2 * p->rsz;
+        int gs = 1;
+        for (const K2Job& jb : p->jobs) {
+            const int rw = std::max(p->segs[jb.seg].rows_per_wg, 1);
+            gs = std::max(gs, std::min(8, 128 / std::max(rw * g.NT * esz, 1)));
+        }
+        struct Gr { double key; int first; };
+        std::vector<Gr> gr;
         std::vector<int> single;
         for (const K2Job& jb : p->jobs) {
-            const int np = jb.wg_count / 2;
-            for (int i = 0; i < np; ++i) pr.push_back({(i + 0.5) / np, jb.wg_begin + 2 * i, jb.wg_begin + 2 * i + 1});
-            if (jb.wg_count & 1) single.push_back(jb.wg_begin + jb.wg_count - 1);
+            const int ng = jb.wg_count / gs;
+            for (int i = 0; i < ng; ++i) gr.push_back({(i + 0.5) / ng, jb.wg_begin + gs * i});
+            for (int w = ng * gs; w < jb.wg_count; ++w) single.push_back(jb.wg_begin + w);
         }
-        std::stable_sort(pr.begin(), pr.end(), [](const Pr& x, const Pr& y) { return x.key < y.key; });
+        std::stable_sort(gr.begin(), gr.end(), [](const Gr& x, const Gr& y) { return x.key < y.key; });
         std::vector<int> order;
-        for (size_t c = 0; c < pr.size(); c += 8) {
-            const size_t e = std::min(pr.size(), c + 8);
-            for (size_t i = c; i < e; ++i) order.push_back(pr[i].a);
-            for (size_t i = c; i < e; ++i) order.push_back(pr[i].b);
+        for (size_t c = 0; c < gr.size(); c += 8) {
+            const size_t e = std::min(gr.size(), c + 8);
+            for (int m = 0; m < gs; ++m)
+                for (size_t i = c; i < e; ++i) order.push_back(gr[i].first + m);
         }
         for (int w : single) order.push_back(w);
         int* dord;
