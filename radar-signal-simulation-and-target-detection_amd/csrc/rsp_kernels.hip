@@ -283,6 +283,10 @@ struct StoreLds {
     V* buf;
     __device__ __forceinline__ void put(int, int, int, int loff, V x) const { buf[loff] = x; }
 };
+// A pass whose output goes back into the LDS rows it reads needs the read/write barrier; one
+// that stores to global memory (the FFT's last pass into z or the RDM) does not.
+template <class St> struct StoresLds { static constexpr bool value = false; };
+template <class V> struct StoresLds<StoreLds<V>> { static constexpr bool value = true; };
 
 // Twiddles w[r] = W_{Ns R}^{k r}, r = 1..R-1, of one butterfly (conjugated for the inverse)
 // from this pass's table: CMP = false: full rows [k][r-1] (R-1 loads, twk = row k); CMP = true:
@@ -431,20 +435,22 @@ __device__ __forceinline__ void sh_store(V (&v)[NB][R], int rs, int nrows, const
     }
 }
 
-template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP, int XL = 0, class V, class St>
+// TAIL = false: no barrier after the pass (the caller's next LDS writes go to other rows).
+template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP, int XL = 0, bool TAIL = true, class V,
+          class St>
 __device__ __forceinline__ void sh_pass(V* buf, int rs, int nrows, const V* tw, const St& st) {
     V v[NB][R];
     sh_load<R, INV, NB, SH, NTHR, LGL, LGNS, CMP, XL>(buf, rs, nrows, tw, v);
-    RSP_WAR_SYNC();
+    if constexpr (StoresLds<St>::value) RSP_WAR_SYNC();
     sh_store<R, INV, NB, SH, NTHR, LGL, LGNS>(v, rs, nrows, st);
-    __syncthreads();
+    if constexpr (TAIL) __syncthreads();
 }
 
 // Passes Q..QEND-1 of a 2^LG-point FFT (radix order reversed if REV) over `nrows` rows;
 // pass n_passes - 1 stores through `last`, the others through `mid`.  tw = this plan's
 // concatenated tables.  PTS = complex points per thread (nrows * L / NTHR).
 template <int LG, int Q, int QEND, int LGNS, int PTS, bool INV, bool REV, int SH, int NTHR, bool CMP, bool PAL = false,
-          int XIN = 0, class V, class StMid, class StLast>
+          int XIN = 0, bool TAIL = true, class V, class StMid, class StLast>
 __device__ __forceinline__ void fft_range(V* buf, int rs, int nrows, const V* tw, const StMid& mid, const StLast& last) {
     constexpr int NP = n_passes(LG);
     if constexpr (Q < QEND) {
@@ -453,18 +459,19 @@ __device__ __forceinline__ void fft_range(V* buf, int rs, int nrows, const V* tw
         constexpr int NB = (PTS + R - 1) / R;
         const V* twq = tw + tw_pass_off(LG, Q, REV, CMP, PAL);
         if constexpr (Q == NP - 1)
-            sh_pass<R, INV, NB, SH, NTHR, LG, LGNS, CMP, XIN>(buf, rs, nrows, twq, last);
+            sh_pass<R, INV, NB, SH, NTHR, LG, LGNS, CMP, XIN, TAIL>(buf, rs, nrows, twq, last);
         else
             sh_pass<R, INV, NB, SH, NTHR, LG, LGNS, CMP, XIN>(buf, rs, nrows, twq, mid);
-        fft_range<LG, Q + 1, QEND, LGNS + RB, PTS, INV, REV, SH, NTHR, CMP, PAL>(buf, rs, nrows, tw, mid, last);
+        fft_range<LG, Q + 1, QEND, LGNS + RB, PTS, INV, REV, SH, NTHR, CMP, PAL, 0, TAIL>(buf, rs, nrows, tw, mid, last);
     }
 }
 
-// All passes of a 2^LG-point FFT over `nrows` rows; the last pass stores through `last`.
-template <int LG, int PTS, int SH, int NTHR, class V, class StMid, class StLast>
+// All passes of a 2^LG-point FFT over `nrows` rows; the last pass stores through `last`
+// (TAIL: followed by a barrier).
+template <int LG, int PTS, int SH, int NTHR, bool TAIL = true, class V, class StMid, class StLast>
 __device__ __forceinline__ void fft_passes(V* buf, int rs, int nrows, const V* tw, const StMid& mid,
                                            const StLast& last) {
-    fft_range<LG, 0, n_passes(LG), 0, PTS, false, false, SH, NTHR, false>(buf, rs, nrows, tw, mid, last);
+    fft_range<LG, 0, n_passes(LG), 0, PTS, false, false, SH, NTHR, false, false, 0, TAIL>(buf, rs, nrows, tw, mid, last);
 }
 
 // ---- Stockham passes of any length L and radix R (mixed-radix overlap-save blocks) ----------
@@ -924,8 +931,10 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
         }
         __syncthreads();
 #else
-        fft_passes<LGP, k1p_pts<T>(), K1_SH, K1_THREADS>(Y + cur * bufsz, Ppad, B * NT, twl,
-                                                          StoreLds<V>{Y + cur * bufsz}, sz);   // ends with a barrier
+        // no barrier after the last pass: its reads of buffer cur are ordered before the next
+        // writes of cur (the next tile's dbf) by the barrier below; dbf now writes cur ^ 1
+        fft_passes<LGP, k1p_pts<T>(), K1_SH, K1_THREADS, false>(Y + cur * bufsz, Ppad, B * NT, twl,
+                                                                 StoreLds<V>{Y + cur * bufsz}, sz);
 #endif
         if (Tn < total) dbf(Y + (cur ^ 1) * bufsz);
         __syncthreads();
@@ -1144,10 +1153,10 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     const int gend = min(sd.gb, g0 + sd.V);
     // the inverse FFT's last pass runs the forward pass 0's radix (R0) over nb0 butterflies
     if constexpr (WROW)
-        fft_range<LGM, 1, NP, RBL, 16, true, true, SH, K2_THREADS, CMP, PAL, XZ>(
+        fft_range<LGM, 1, NP, RBL, 16, true, true, SH, K2_THREADS, CMP, PAL, XZ, false>(
             L, rs, rows, twI, StoreLds<V>{L}, StoreRdmW<V>{rdm, mag, G, g.Gp, row0, rows_total, Lh1, g0, gend});
     else
-        fft_range<LGM, 1, NP, RBL, 16, true, true, SH, K2_THREADS, CMP, PAL, XZ>(
+        fft_range<LGM, 1, NP, RBL, 16, true, true, SH, K2_THREADS, CMP, PAL, XZ, false>(
             L, rs, rows, twI, StoreLds<V>{L},
             StoreRdm<V>{buf_rsrc(rdm, (unsigned)(rows_total * G * sizeof(V))),
                         buf_rsrc(mag, (unsigned)(rows_total * g.Gp * sizeof(T))), G, g.Gp, row0, rows_total, Lh1, g0,
