@@ -949,12 +949,12 @@ template <class V>
 struct StoreRdm {   // last inverse pass: keep outputs i in [Lh-1, Lh-1+V) that map to gates < gend;
                     // also writes |x| (the CFAR input, fsf:184-185) into the magnitude map.
                     // Branch-free: rejected outputs get an out-of-range buffer offset.
-    __amdgpu_buffer_rsrc_t rdm, mag; int G; int Gp; int row0; int rows_total; int Lh1; int g0; int gend;
+    __amdgpu_buffer_rsrc_t rdm, mag; int G; int Gp; int row0; int rows_total; int Lh1; int g0; int gend; bool has_rdm;
     __device__ __forceinline__ void put(int, int row, int o, int, V x) const {
         const int gg = g0 + o - Lh1;
         const int rho = row0 + row;
         const bool ok = o >= Lh1 && gg < gend && rho < rows_total;
-        buf_st<RSP_RDM_AUX>(rdm, ok ? (unsigned)(rho * G + gg) * (unsigned)sizeof(V) : RSP_OOB, x);
+        if (has_rdm) buf_st<RSP_RDM_AUX>(rdm, ok ? (unsigned)(rho * G + gg) * (unsigned)sizeof(V) : RSP_OOB, x);
         buf_st1(mag, ok ? (unsigned)(rho * Gp + gg) * (unsigned)sizeof(scal<V>) : RSP_OOB, cmag(x));
     }
 };
@@ -973,7 +973,8 @@ struct StoreRdmW {
         const __amdgpu_buffer_rsrc_t rr = buf_rsrc(rdm + (size_t)rho * G + g0, n * (unsigned)sizeof(V));
         const __amdgpu_buffer_rsrc_t mr = buf_rsrc(mag + (size_t)rho * Gp + g0, n * (unsigned)sizeof(S));
         // (o - Lh1) * size, written so that o's constant part folds into one add per store
-        buf_st<RSP_RDM_AUX>(rr, (unsigned)o * (unsigned)sizeof(V) - (unsigned)Lh1 * (unsigned)sizeof(V), x);
+        if (rdm)   // uniform: null when the launch keeps the RDM on chip (lane_ptrs)
+            buf_st<RSP_RDM_AUX>(rr, (unsigned)o * (unsigned)sizeof(V) - (unsigned)Lh1 * (unsigned)sizeof(V), x);
         buf_st1(mr, (unsigned)o * (unsigned)sizeof(S) - (unsigned)Lh1 * (unsigned)sizeof(S), cmag(x));
     }
 };
@@ -1160,7 +1161,7 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
             L, rs, rows, twI, StoreLds<V>{L},
             StoreRdm<V>{buf_rsrc(rdm, (unsigned)(rows_total * G * sizeof(V))),
                         buf_rsrc(mag, (unsigned)(rows_total * g.Gp * sizeof(T))), G, g.Gp, row0, rows_total, Lh1, g0,
-                        gend});
+                        gend, rdm != nullptr});
 }
 
 
@@ -1341,9 +1342,11 @@ __global__ __launch_bounds__(K2_THREADS, 512 / K2_THREADS) void k2_pc(Geometry g
                     t = tp[j];
                     a0 += t * w0; a1 += t * w1; a2 += t * w2; a3 += t * w3;
                 }
-                V* ro = rdm + (size_t)rho * G + gg0;
+                if (rdm) {
+                    V* ro = rdm + (size_t)rho * G + gg0;
+                    ro[0] = a0; ro[1] = a1; ro[2] = a2; ro[3] = a3;
+                }
                 T* mo = mag + (size_t)rho * g.Gp + gg0;
-                ro[0] = a0; ro[1] = a1; ro[2] = a2; ro[3] = a3;
                 mo[0] = cmag(a0); mo[1] = cmag(a1); mo[2] = cmag(a2); mo[3] = cmag(a3);
             } else {
                 for (int q = 0; q < 4 && q0 + q < nout; ++q) {
@@ -1353,7 +1356,7 @@ __global__ __launch_bounds__(K2_THREADS, 512 / K2_THREADS) void k2_pc(Geometry g
                     const V* xr = row + kk;
                     V acc = V{};
                     for (int j = 0; j < sd.ntaps; ++j) acc += tp[j] * xr[-j];
-                    rdm[(size_t)rho * G + gg] = acc;
+                    if (rdm) rdm[(size_t)rho * G + gg] = acc;
                     mag[(size_t)rho * g.Gp + gg] = cmag(acc);
                 }
             }

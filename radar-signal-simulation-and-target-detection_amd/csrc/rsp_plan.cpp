@@ -461,12 +461,16 @@ int setup_lane(rsp_plan* p, Lane& L) {
     return lane_host_alloc(p, L, std::min(p->det_bound, 1024));
 }
 
-FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const void* const* in, int nf) {
+// rdm = false: K2 keeps the complex RD map on chip and stores only its magnitudes, the one
+// input of K3 and S9.  fun_process_single_frame returns final_targets (fsf:13); its rdm_13beam
+// is an intermediate, so the throughput queue does not write it to HBM (-10% k2_pc); frames
+// whose RDM is asked for (rsp_process_frame with out->rdm, process_stage2) write it.
+FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const void* const* in, int nf, bool rdm = true) {
     FramePtrs fp{};
     for (int f = 0; f < nf; ++f) {
         fp.in[f] = in[f];
         fp.z[f] = (char*)L.z + p->z_elems * p->esz * f;
-        fp.rdm[f] = (char*)L.rdm + p->rdm_elems * p->esz * f;
+        fp.rdm[f] = rdm ? (char*)L.rdm + p->rdm_elems * p->esz * f : nullptr;
         fp.mag[f] = (char*)L.mag + p->mag_elems * p->rsz * f;
         DevDet* rec = L.dets + (size_t)(L.dcap + 1) * f;
         fp.count[f] = reinterpret_cast<int*>(rec);   // zeroed by K1, bumped by K3
@@ -487,8 +491,8 @@ FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const void* const* in, int
 #define RSP_K12_SUB 0
 #endif
 int launch_batch(rsp_plan* p, Lane& L, const void* const* in, const int* ids, int nf, void* smap = nullptr,
-                 const int* slots = nullptr) {
-    FramePtrs fp = lane_ptrs(p, L, in, nf);
+                 const int* slots = nullptr, bool want_rdm = false) {
+    FramePtrs fp = lane_ptrs(p, L, in, nf, want_rdm);
     fp.smap[0] = smap;
     if (slots)   // producer-ring frames: K1 after their upload / synthesis
         for (int f = 0; f < nf; ++f)
@@ -755,7 +759,7 @@ int run_sync_frame(rsp_plan* p, const void* d_in, int frame_idx, rsp_frame_out* 
         if (!p->d_smap && (rc = p->dalloc_bytes(&p->d_smap, (size_t)(p->g.B - 1) * p->g.P * p->g.G * p->rsz))) return rc;
         smap = p->d_smap;
     }
-    if ((rc = launch_batch(p, L, in, ids, 1, smap))) return rc;
+    if ((rc = launch_batch(p, L, in, ids, 1, smap, nullptr, out && out->rdm))) return rc;
     if ((rc = harvest(p, L, &dets))) return rc;
     FrameResult fr = p->results.back();
     p->results.resize(nres);   // synchronous frames do not enter the queue's result list
@@ -1425,7 +1429,7 @@ int32_t rsp_profile_stages(rsp_plan* p, const void* const* d_cubes, int32_t n_cu
     for (int j = 0; j < nsets; ++j) {
         const void* in[RSP_MAX_F];
         for (int f = 0; f < nf; ++f) in[f] = d_cubes[(j * nf + f) % n_cubes];
-        fps[j] = lane_ptrs(p, L, in, nf);
+        fps[j] = lane_ptrs(p, L, in, nf, false);   // as the queue: no complex RDM stores
     }
     const Geometry& g = p->g;
     hipEvent_t e0, e1;
@@ -1459,10 +1463,9 @@ int32_t rsp_profile_stages(rsp_plan* p, const void* const* d_cubes, int32_t n_cu
         const int64_t es = (int64_t)p->esz, rs = (int64_t)p->rsz;   // complex / real element bytes
         const int64_t cube = (int64_t)g.C * g.nU * g.P * es;       // used fast-time samples
         const int64_t z = (int64_t)g.B * g.nU * g.P * es;          // Doppler-domain rows
-        const int64_t rdm = (int64_t)g.B * g.P * g.G * es;         // complex RD map
-        const int64_t mag = (int64_t)g.B * g.P * g.G * rs;         // |RD| map
+        const int64_t mag = (int64_t)g.B * g.P * g.G * rs;         // |RD| map (the RDM stays on chip)
         if (cap > 0) bytes_out[0] = nf * (cube + z);
-        if (cap > 1) bytes_out[1] = nf * (z + rdm + mag);
+        if (cap > 1) bytes_out[1] = nf * (z + mag);
         if (cap > 2) bytes_out[2] = nf * mag;
     }
     return RSP_OK;
