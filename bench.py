@@ -391,6 +391,13 @@ def main():
         for lv, pr in zip(live, prof):
             st = {'stage': pr['stage'], 'ms_per_launch': pr['ms'], 'frames_per_launch': pr['frames'],
                   'alg_bytes_per_launch': pr['bytes'], 'achieved_GBps': pr['bytes'] / (pr['ms'] * 1e-3) / 1e9}
+            if pr['stage'] == 'k1_dbf_mtd':   # the DBF on the matrix cores: B x C complex MACs per cell
+                fl = pr['frames'] * sz.B * sz.C * sz.used_samples * sz.P * 8.0
+                mpk = F64_PEAK_TFLOPS if a.precision == 'c128' else 157.3
+                st['alg_mfma_flops_per_launch'] = fl
+                st['achieved_mfma_TFLOPs'] = fl / (pr['ms'] * 1e-3) / 1e12
+                st['mfma_frac'] = st['achieved_mfma_TFLOPs'] / mpk
+                st['mfma_peak_TFLOPs'] = mpk
             if lv['launches']:
                 st['live_overlapped_ms_per_launch'] = lv['ms_total'] / lv['launches']
                 st['live_frames_per_launch'] = lv['frames'] / lv['launches']

@@ -1270,6 +1270,12 @@ __global__ __launch_bounds__(K2_THREADS, 512 / K2_THREADS) void k2_pc(Geometry g
     const int lo = sd.lo, hi = sd.hi, off = sd.off;
     const int tid = threadIdx.x;
 
+#ifdef RSP_K2_ONLY   // timing-only builds: 1 = narrow FIR jobs only, 2 = power-of-two blocks only, 3 = 2560 blocks only
+    {
+        const int jt = sd.type != 1 ? 1 : (sd.logM == 0 ? 3 : 2);
+        if (jt != RSP_K2_ONLY) return;
+    }
+#endif
 #ifdef RSP_K2_CENSUS   // instruction-census builds (-S only): one job type per kernel
     if (RSP_K2_CENSUS == 1) { k2_fft_job_mix<T, 2560, 10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); return; }
     if (RSP_K2_CENSUS == 2) { k2_fft_job<T, 10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); return; }
