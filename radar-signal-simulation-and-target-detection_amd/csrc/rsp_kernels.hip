@@ -994,6 +994,9 @@ template <class V>
 __device__ __forceinline__ ZWin zrow_window(const Geometry& g, const V* z, int rho, int rows_total, int off, int lo,
                                             int hi) {
     ZWin w;
+#ifdef RSP_K2_HOTZ   // timing-only builds: every row reads row (rho mod 16)'s samples (cache-resident)
+    rho = rho & 15;
+#endif
     const int b = rho / g.P, v = rho - b * g.P;
     w.lgNT = ilog2(g.NT);
     w.NT1 = g.NT - 1;
