@@ -151,6 +151,7 @@ struct DevConsts {
     const void* win;         // MTD window [P], real
     const void* twP;         // W_P^i table (direct DFT path), complex
     const void* twPp;        // per-pass Stockham twiddles of the P-point FFT, complex
+    const void* twD;         // persistent K1's in-place FFT: [i][n2] = W_P^(n2 2^i), i < 4, n2 < P/16, complex
     const void* taps;        // narrow FIR taps, real
     const void* H;           // overlap-save spectra, 1/M scaled, complex
     const void* twM;         // per-pass Stockham twiddles of each overlap-save block size, complex

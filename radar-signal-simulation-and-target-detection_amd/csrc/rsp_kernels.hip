@@ -638,6 +638,71 @@ struct StoreZ {
     }
 };
 
+// In-place decimation-in-frequency FFT of length P = 16 R1 over nrows LDS rows (stride rs, pads
+// per 2^SH), two passes:
+//   A: radix 16 over x[n1 R1 + n2] (n1 < 16), output k1 times W_P^(n2 k1), written back to the
+//      slots it was read from (n1 -> k1): no thread writes a slot another reads, so the pass
+//      needs no read/write barrier (a Stockham pass does);
+//   B: radix R1 over the R1 contiguous y[k1 R1 + n2] -> X[k1 + 16 k2], stored through st with
+//      the natural bin o = k1 + 16 k2 (the z store applies fftshift).
+// twd = the compact pass-A table in LDS, [i][n2] = W_P^(n2 2^i) (load_tw).  Same arithmetic per
+// output as the radix-16 x radix-R1 Stockham plan, with the twiddles on the other side.
+// PTS = points per thread (nrows P <= PTS NTHR, k1_persistent_fits).
+template <int LGP, int PTS, int NTHR, int SH, class V, class St>
+__device__ __forceinline__ void k1_fft_dif(V* buf, int rs, int nrows, const V* twd, const St& st) {
+    constexpr int P = 1 << LGP, R1 = P / 16, LGR1 = LGP - 4;
+    static_assert(R1 >= 4 && R1 <= 16, "P in 64..256");
+    {
+        const int total = R1 * nrows;
+        constexpr int NB = (PTS + 15) / 16;
+#pragma unroll
+        for (int t = 0; t < NB; ++t) {
+            const int beta = threadIdx.x + t * NTHR;
+            if (beta < total) {
+                const int row = beta >> LGR1, n2 = beta & (R1 - 1);
+                V* src = buf + row * rs;
+                V x[16];
+#pragma unroll
+                for (int n1 = 0; n1 < 16; ++n1) x[n1] = src[lidx<SH>(n1 * R1 + n2)];
+                V b[4];   // W^(n2 2^i)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) b[i] = twd[i * R1 + n2];
+                Dft<16, false, V>::run(x);
+                // W^(n2 k1) for k1 = 1..15 as in load_tw (w[r] = w[2^hb] w[r - 2^hb]), each applied
+                // as soon as it exists so that only w[1..8] stay live
+                V w[16];
+#pragma unroll
+                for (int k1 = 1; k1 < 16; ++k1) {
+                    const int hb = 1 << clog2(k1);
+                    w[k1] = (hb == k1) ? b[clog2(k1)] : vmul(w[hb], w[k1 - hb]);
+                    x[k1] = vmul(x[k1], w[k1]);
+                }
+#pragma unroll
+                for (int k1 = 0; k1 < 16; ++k1) src[lidx<SH>(k1 * R1 + n2)] = x[k1];
+            }
+        }
+    }
+    __syncthreads();
+    {
+        const int total = 16 * nrows;
+        constexpr int NB = (16 * PTS + P - 1) / P;
+#pragma unroll
+        for (int t = 0; t < NB; ++t) {
+            const int beta = threadIdx.x + t * NTHR;
+            if (beta < total) {
+                const int row = beta >> 4, k1 = beta & 15;
+                const V* src = buf + row * rs;
+                V y[R1];
+#pragma unroll
+                for (int n2 = 0; n2 < R1; ++n2) y[n2] = src[lidx<SH>(k1 * R1 + n2)];
+                Dft<R1, false, V>::run(y);
+#pragma unroll
+                for (int k2 = 0; k2 < R1; ++k2) st.put(k2, row, k1 + 16 * k2, 0, y[k2]);
+            }
+        }
+    }
+}
+
 // Slow-time FFT of every (beam, sample) column in LDS for the runtime log2(P); the last pass
 // stores through `last`.
 template <class V, class StLast>
@@ -646,8 +711,8 @@ __device__ __forceinline__ void k1_fft(int lgp, V* Y, int Ppad, int ncols, const
     switch (lgp) {
         case 4: fft_passes<4, 16, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
         case 5: fft_passes<5, 16, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
-        case 6: fft_passes<6, 16, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
-        case 7: fft_passes<7, 16, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
+        case 6: k1_fft_dif<6, 16, K1_THREADS, K1_SH>(Y, Ppad, ncols, twl, last); break;   // twl = twD
+        case 7: k1_fft_dif<7, 16, K1_THREADS, K1_SH>(Y, Ppad, ncols, twl, last); break;
         case 8: fft_passes<8, 16, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
         default: fft_passes<9, 16, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
     }
@@ -668,7 +733,11 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
     V* twl = Y + B * NT * Ppad;
     const bool fft = (mode & 2) && g.pow2P;
     const int sh = fft ? K1_SH : 0;
-    const V* __restrict__ twPp = static_cast<const V*>(k.twPp);
+    // P = 64, 128 run the in-place k1_fft_dif (as the persistent K1: the same bits), the other
+    // powers of two the Stockham passes
+    const bool dif = fft && g.logP >= 6 && g.logP <= 7;
+    const V* __restrict__ twPp = static_cast<const V*>(dif ? k.twD : k.twPp);
+    const int ntw = dif ? (P >> 2) : g.twPp_elems;
     const T* __restrict__ win = static_cast<const T*>(k.win);
     // twiddles: global loads issued first, LDS stores after the cube loads are in flight (the
     // barrier before the FFT orders them), so no load waits behind a barrier at kernel start
@@ -677,7 +746,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
 #pragma unroll
     for (int u = 0; u < TWPRE; ++u) {
         const int i = threadIdx.x + u * K1_THREADS;
-        if (fft && i < g.twPp_elems) twv[u] = twPp[i];
+        if (fft && i < ntw) twv[u] = twPp[i];
     }
     const V* __restrict__ x = static_cast<const V*>(fp.in[f]);
     const size_t NP = (size_t)g.cpitch;   // channel stride
@@ -761,9 +830,9 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
 #pragma unroll
         for (int u = 0; u < TWPRE; ++u) {
             const int i = threadIdx.x + u * K1_THREADS;
-            if (i < g.twPp_elems) twl[i] = twv[u];
+            if (i < ntw) twl[i] = twv[u];
         }
-        for (int i = threadIdx.x + TWPRE * K1_THREADS; i < g.twPp_elems; i += K1_THREADS) twl[i] = twPp[i];
+        for (int i = threadIdx.x + TWPRE * K1_THREADS; i < ntw; i += K1_THREADS) twl[i] = twPp[i];
     }
     __syncthreads();
     V* __restrict__ z = static_cast<V*>(fp.z[f]);
@@ -808,6 +877,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
 // the plan halves NT for double so that two tile buffers still fit the 160 KB of LDS.
 template <class T> constexpr int k1p_pts() { return sizeof(T) == 4 ? 16 : 8; }
 
+
 // K1, persistent and software-pipelined (the default for power-of-two P when one load round
 // covers a tile): one workgroup per CU walks the (frame, tile) list with two LDS tile buffers.
 // While tile TT's slow-time FFT runs out of one buffer and its last pass streams z to HBM, the
@@ -828,8 +898,13 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
     const int total = nf * g.ntiles;
     int TT = blockIdx.x;
     if (TT >= total) return;
-    const V* __restrict__ twPp = static_cast<const V*>(k.twPp);
-    for (int i = threadIdx.x; i < g.twPp_elems; i += K1_THREADS) twl[i] = twPp[i];
+    if constexpr (LGP <= 7) {   // k1_fft_dif's table, 4 x P/16
+        const V* __restrict__ twD = static_cast<const V*>(k.twD);
+        for (int i = threadIdx.x; i < (P >> 2); i += K1_THREADS) twl[i] = twD[i];
+    } else {
+        const V* __restrict__ twPp = static_cast<const V*>(k.twPp);
+        for (int i = threadIdx.x; i < g.twPp_elems; i += K1_THREADS) twl[i] = twPp[i];
+    }
     constexpr int NJ = CP / 4, MB = BMAX <= 8 ? 1 : 2, TPW = TPWX;
     constexpr int PT = 16 * D::PPL;
     const int lane = threadIdx.x & 63, grp = lane >> 4, col = lane & 15;
@@ -931,10 +1006,15 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
         }
         __syncthreads();
 #else
-        // no barrier after the last pass: its reads of buffer cur are ordered before the next
-        // writes of cur (the next tile's dbf) by the barrier below; dbf now writes cur ^ 1
-        fft_passes<LGP, k1p_pts<T>(), K1_SH, K1_THREADS, false>(Y + cur * bufsz, Ppad, B * NT, twl,
-                                                                 StoreLds<V>{Y + cur * bufsz}, sz);
+        // P <= 128: in place, one barrier (between its passes); P = 256 (x4): the Stockham passes
+        // (the in-place pass A's 16 twiddles spill there, +7 % K1).  No barrier after the last
+        // pass: its reads of buffer cur are ordered before the next writes of cur (the next
+        // tile's dbf) by the barrier below, and dbf now writes cur ^ 1
+        if constexpr (LGP <= 7)
+            k1_fft_dif<LGP, k1p_pts<T>(), K1_THREADS, K1_SH>(Y + cur * bufsz, Ppad, B * NT, twl, sz);
+        else
+            fft_passes<LGP, k1p_pts<T>(), K1_SH, K1_THREADS, false>(Y + cur * bufsz, Ppad, B * NT, twl,
+                                                                     StoreLds<V>{Y + cur * bufsz}, sz);
 #endif
         if (Tn < total) dbf(Y + (cur ^ 1) * bufsz);
         __syncthreads();

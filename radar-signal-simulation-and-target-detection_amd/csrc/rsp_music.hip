@@ -758,7 +758,7 @@ __global__ __launch_bounds__(MU_THREADS, 2) void k_music_cov64(int N, int K, con
 //     forms v_k (zlarfg) and keeps it; p = tau A v (lane = column, A Hermitian), w = p - tau/2
 //     (p^H v) v, A -= v w^H + w v^H -- three barriers per step.
 //  2. All eigenvalues of T by multisection, quad i -> the i-th smallest: the 4 lanes evaluate
-//     the Sturm count (LAPACK dstebz recurrence with pivmin) at 4 interior points, 23 rounds
+//     the Sturm count (the leading minors' sign changes, division-free) at 4 interior points, 23 rounds
 //     shrink the Gershgorin interval by 5^23 > 2^53 (to the rounding of the eigenvalue).
 //  3. The M signal eigenvectors of T by inverse iteration (dlagtf / dlagts, lane j = vector j,
 //     3 solves with modified Gram-Schmidt) in wave 0, then q_j = H_0 ... H_{n-2} y_j, the
@@ -772,7 +772,7 @@ __global__ __launch_bounds__(MU_THREADS, 2) void k_music_cov64(int N, int K, con
 #define ME_WPS 4     // waves per SIMD the register budget is sized for (4 instances per CU)
 #endif
 __host__ __device__ constexpr size_t me_lds_bytes(int M, int S) {
-    return (size_t)4 * 64 * 16 + 64 * 16 + 8 * 16 + 4 * 64 * 8 + (size_t)5 * 64 * M * 8 + (size_t)M * 64 * 16 +
+    return (size_t)4 * 64 * 16 + 64 * 16 + 8 * 16 + 3 * 68 * 8 + 64 * 8 + (size_t)5 * 64 * M * 8 + (size_t)M * 64 * 16 +
            ((size_t)S + 8) * 8 + 8 * 16;
 }
 
@@ -790,10 +790,10 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
     double2* wb = vb + 128;              // [2][64] w
     double2* taus = wb + 128;            // [64]
     double2* red = taus + 64;            // [8] per-wave partial sums
-    double* dd = reinterpret_cast<double*>(red + 8);   // T diagonal
-    double* ee = dd + 64;                // T off-diagonal (beta_k, signed)
-    double* e2 = ee + 64;                // beta_k^2
-    double* lam = e2 + 64;               // ascending eigenvalues
+    double* dd = reinterpret_cast<double*>(red + 8);   // T diagonal (+ 4 pad rows for the Sturm count)
+    double* ee = dd + 68;                // T off-diagonal (beta_k, signed)
+    double* e2 = ee + 68;                // beta_k^2 (+ pad)
+    double* lam = e2 + 68;               // ascending eigenvalues
     double* lu = lam + 64;               // [5][64][M]: U diag, U super 1, U super 2, mult, y
     double2* Qs = reinterpret_cast<double2*>(lu + 5 * 64 * M);   // [M][64]
     double* den = reinterpret_cast<double*>(Qs + M * 64);        // [S]
@@ -918,16 +918,41 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
         const double tn = fmax(fabs(glo), fabs(ghi));
         const double pivmin = 2.2250738585072014e-308 * fmax(1.0, emax);   // dstebz PIVMIN
         double lo = glo - 4.4e-16 * tn - 2.0 * pivmin, hi = ghi + 4.4e-16 * tn + 2.0 * pivmin;
-        auto sturm = [&](double x) -> int {   // # eigenvalues of T below x
-            double qv = dd[0] - x;
-            if (fabs(qv) < pivmin) qv = -pivmin;
-            int c = qv < 0.0;
-            for (int r = 1; r < n; ++r) {
-                double rc = __builtin_amdgcn_rcp(qv);
-                rc = fma(fma(-qv, rc, 1.0), rc, rc);   // one Newton step: 1 / q to about an ulp
-                qv = (dd[r] - x) - e2[r - 1] * rc;
-                if (fabs(qv) < pivmin) qv = -pivmin;
-                c += qv < 0.0;
+        // # eigenvalues of T below x: sign changes of the leading minors p_r = det(T_r - x I),
+        // p_r = (d_r - x) p_{r-1} - e_{r-1}^2 p_{r-2} -- the division-free form of dstebz's
+        // q_r = p_r / p_{r-1} (its dependent chain is one FMA per row instead of a reciprocal).
+        // A zero minor counts as a sign change, as q_r = 0 -> -pivmin does there; both minors
+        // are rescaled by a power of two every 4 rows (no overflow or underflow).
+        // rows n .. n + 3 pad the count to whole blocks of 4: d = ghi + 1 > every x of the
+        // search and e^2 = 0 keep the minors' signs (p_r = (d - x) p_{r-1}, d - x > 0)
+        __syncthreads();   // every lane has read dd / e2 (Gershgorin) before the pad rows land
+        if (t < 4) {
+            dd[n + t] = ghi + 1.0;
+            e2[n - 1 + t] = 0.0;
+        }
+        __syncthreads();
+        auto sturm = [&](double x) -> int {
+            double pm = 1.0, pc = dd[0] - x;
+            bool sc = !(pc > 0.0);   // effective sign of p_0 (zero -> negative, as -pivmin)
+            int c = sc;
+            double dn = dd[1], en = e2[0];   // row r's (d_r, e_{r-1}^2), loaded a row ahead
+            for (int r0 = 1; r0 < n; r0 += 4) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int r = r0 + j;
+                    const double d = dn, e = en;
+                    dn = dd[r + 1];   // r + 1 <= n + 3 (padded)
+                    en = e2[r];
+                    const double pn = fma(d - x, pc, -e * pm);
+                    const bool sn = (pn < 0.0) | ((pn == 0.0) & !sc);
+                    c += sn ^ sc;
+                    sc = sn;
+                    pm = pc;
+                    pc = pn;
+                }
+                const int ex = __builtin_amdgcn_frexp_exp(pc);   // rescale both by 2^-ex
+                pc = __builtin_amdgcn_ldexp(pc, -ex);
+                pm = __builtin_amdgcn_ldexp(pm, -ex);
             }
             return c;
         };

@@ -1024,9 +1024,12 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
                 atab[((mb * nj + j) * 2 + 0) * 64 + lane] = im ? wi : wr;    // coefficient of Re(x_c)
                 atab[((mb * nj + j) * 2 + 1) * 64 + lane] = im ? wr : -wi;   // coefficient of Im(x_c)
             }
-    std::vector<cd> twPp, twP(P);
+    std::vector<cd> twPp, twP(P), twD;
     if (g.pow2P) build_pass_twiddles(g.logP, twPp);
     g.twPp_elems = (int)twPp.size();
+    if (g.pow2P && P >= 64 && P <= 128)   // k1_fft_dif: compact pass-A twiddles, column-major [i][n2]
+        for (int i = 0; i < 4; ++i)
+            for (int n2 = 0; n2 < P / 16; ++n2) twD.push_back(root_of_unity((long long)n2 << i, P));
     for (int i = 0; i < P; ++i) twP[i] = root_of_unity(i, P);
     std::vector<double> win(pre->MTD_win, pre->MTD_win + P);
     std::vector<double> ra(pre->range_axis, pre->range_axis + G), va(pre->velocity_axis, pre->velocity_axis + P);
@@ -1035,7 +1038,7 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
     for (int i = 0; i + 1 < B; ++i) kl[i] = pre->k_slopes_LUT[i];
     DevConsts& k = p->k;
     double *dra, *dva, *dang, *dkl;
-    if ((rc = p->upload_r(&k.Atab, atab)) || (rc = p->upload_c(&k.twP, twP)) || (rc = p->upload_c(&k.twPp, twPp)) ||
+    if ((rc = p->upload_r(&k.Atab, atab)) || (rc = p->upload_c(&k.twP, twP)) || (rc = p->upload_c(&k.twPp, twPp)) || (rc = p->upload_c(&k.twD, twD)) ||
         (rc = p->upload_r(&k.win, win)) || (rc = p->upload_r(&k.taps, taps)) || (rc = p->upload_c(&k.H, H)) ||
         (rc = p->upload_c(&k.twM, twM)) || (rc = p->upload(&dra, ra)) || (rc = p->upload(&dva, va)) ||
         (rc = p->upload(&dang, ang)) || (rc = p->upload(&dkl, kl)))
