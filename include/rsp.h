@@ -271,6 +271,11 @@ int32_t rsp_profile_stages(rsp_plan* plan, const void* const* d_cubes, int32_t n
                            float* ms_out, int64_t* bytes_out, int32_t cap, int32_t* frames_out);
 const char* rsp_stage_name(int32_t stage);
 
+/* The box's streaming-copy bandwidth (SURVEY 8(d) "measured stream-copy peak"): a 16-B-per-lane
+ * non-temporal copy kernel over two device buffers of `bytes` each, `iters` timed launches;
+ * *gbps = 2 * bytes / average launch time (read + write).  Measurement only; no plan needed. */
+int32_t rsp_hbm_copy_probe(int32_t device, int64_t bytes, int32_t iters, double* gbps);
+
 /* Live stage timing of the throughput queue (rsp_enqueue_device): with timing on, every batch
  * records HIP events around K1, K2 and K3 on the stream the kernels run on, and harvest adds the
  * elapsed times.  rsp_set_stage_timing resets the sums.  rsp_stage_times: ms_sum[i] = total ms

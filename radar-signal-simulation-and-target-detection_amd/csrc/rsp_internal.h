@@ -172,6 +172,7 @@ struct SynthTarget {          // per-target constants of S4 (fsf:51-73), host-co
 
 // Launchers (rsp_kernels.hip).  `mode` bits for K1: 1 = apply DBF, 2 = apply MTD.
 hipError_t launch_k1(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int mode, hipStream_t s);
+hipError_t launch_stream_copy(const void* in, void* out, size_t n16, int ncu, hipStream_t s);
 hipError_t launch_k2(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int rows, hipStream_t s);
 hipError_t launch_k3(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, hipStream_t s);
 hipError_t launch_mtd_cols(const Geometry& g, const DevConsts& k, const void* pc, void* rdm, hipStream_t s);

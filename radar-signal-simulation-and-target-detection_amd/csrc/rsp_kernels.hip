@@ -2181,6 +2181,34 @@ static hipError_t launch_k2_p(const Geometry& g, const DevConsts& k, const Frame
     return hipGetLastError();
 }
 
+// Streaming copy (rsp_hbm_copy_probe): CU16 x 16 B per lane, all loads in flight before the
+// stores, one chunk per workgroup.
+#ifndef RSP_COPY_U
+#define RSP_COPY_U 4
+#endif
+#ifndef RSP_COPY_NT
+#define RSP_COPY_NT 0
+#endif
+__global__ __launch_bounds__(256) void k_stream_copy(const u32x4* __restrict__ in, u32x4* __restrict__ out, size_t n16) {
+    const size_t base = (size_t)blockIdx.x * (256 * RSP_COPY_U) + threadIdx.x;
+    u32x4 v[RSP_COPY_U];
+#pragma unroll
+    for (int u = 0; u < RSP_COPY_U; ++u)
+        if (base + u * 256 < n16) v[u] = RSP_COPY_NT ? __builtin_nontemporal_load(in + base + u * 256) : in[base + u * 256];
+#pragma unroll
+    for (int u = 0; u < RSP_COPY_U; ++u)
+        if (base + u * 256 < n16) {
+            if (RSP_COPY_NT) __builtin_nontemporal_store(v[u], out + base + u * 256);
+            else out[base + u * 256] = v[u];
+        }
+}
+
+hipError_t launch_stream_copy(const void* in, void* out, size_t n16, int, hipStream_t s) {
+    hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)((n16 + 256 * RSP_COPY_U - 1) / (256 * RSP_COPY_U))), dim3(256), 0, s,
+                       static_cast<const u32x4*>(in), static_cast<u32x4*>(out), n16);
+    return hipGetLastError();
+}
+
 hipError_t launch_k2(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int rows, hipStream_t s) {
     return g.prec == RSP_PREC_F64 ? launch_k2_p<double>(g, k, fp, nf, rows, s)
                                   : launch_k2_p<float>(g, k, fp, nf, rows, s);

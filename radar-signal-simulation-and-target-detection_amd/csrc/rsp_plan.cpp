@@ -1474,6 +1474,40 @@ int32_t rsp_profile_stages(rsp_plan* p, const void* const* d_cubes, int32_t n_cu
     return RSP_OK;
 }
 
+int32_t rsp_hbm_copy_probe(int32_t device, int64_t bytes, int32_t iters, double* gbps) {
+    if (!gbps || bytes < (1 << 20) || iters < 1) return fail(RSP_ERR_INVALID, "bad argument");
+    HIPCHK(hipSetDevice(device));
+    int ncu = 0;
+    HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
+    const size_t n16 = (size_t)bytes / 16;
+    void *a = nullptr, *b = nullptr;
+    if (hipMalloc(&a, n16 * 16) != hipSuccess) return fail(RSP_ERR_NOMEM, "hipMalloc(%lld) failed", (long long)bytes);
+    if (hipMalloc(&b, n16 * 16) != hipSuccess) {
+        (void)hipFree(a);
+        return fail(RSP_ERR_NOMEM, "hipMalloc(%lld) failed", (long long)bytes);
+    }
+    hipEvent_t e0, e1;
+    hipError_t e = hipMemset(a, 0, n16 * 16);
+    if (e == hipSuccess) e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    float ms = 0.f;
+    if (e == hipSuccess) {
+        for (int i = 0; i < 3 && e == hipSuccess; ++i) e = launch_stream_copy(a, b, n16, ncu, nullptr);
+        if (e == hipSuccess) e = hipEventRecord(e0, nullptr);
+        for (int i = 0; i < iters && e == hipSuccess; ++i) e = launch_stream_copy(a, b, n16, ncu, nullptr);
+        if (e == hipSuccess) e = hipEventRecord(e1, nullptr);
+        if (e == hipSuccess) e = hipEventSynchronize(e1);
+        if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    }
+    (void)hipFree(a);
+    (void)hipFree(b);
+    if (e != hipSuccess) return fail(RSP_ERR_DEVICE, "copy probe: %s", hipGetErrorString(e));
+    *gbps = 2.0 * (double)(n16 * 16) / (ms * 1e-3 / iters) / 1e9;
+    return RSP_OK;
+}
+
 int32_t rsp_device_alloc(rsp_plan* p, int64_t bytes, void** d) {
     if (!p || !d || bytes <= 0) return fail(RSP_ERR_INVALID, "bad argument");
     HIPCHK(hipSetDevice(p->device));

@@ -163,6 +163,7 @@ PROTOTYPES = {
     'rsp_profile_stages': (ct.c_int32, [_P, ct.POINTER(_P), ct.c_int32, ct.c_int32, ct.POINTER(ct.c_float),
                                         ct.POINTER(ct.c_int64), ct.c_int32, ct.POINTER(ct.c_int32)]),
     'rsp_stage_name': (ct.c_char_p, [ct.c_int32]),
+    'rsp_hbm_copy_probe': (ct.c_int32, [ct.c_int32, ct.c_int64, ct.c_int32, ct.POINTER(ct.c_double)]),
     'rsp_set_stage_timing': (ct.c_int32, [_P, ct.c_int32]),
     'rsp_stage_times': (ct.c_int32, [_P, ct.POINTER(ct.c_double), ct.c_int32, ct.POINTER(ct.c_int64),
                                      ct.POINTER(ct.c_int64)]),
