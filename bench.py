@@ -452,10 +452,14 @@ def main():
         # the box's measured stream-copy rate beside the datasheet peak
         import ctypes as ct
         from rsp import _abi
-        gbps = ct.c_double()
-        if _abi.lib().rsp_hbm_copy_probe(dev, 1 << 30, 20, ct.byref(gbps)) == 0:
-            out['roofline']['stream_copy_GBps'] = gbps.value
-            out['roofline']['frac_of_stream_copy'] = achieved / gbps.value
+        best = 0.0
+        for _ in range(3):   # the best of 3 probes of 20 copies of 1 GiB (> the 256 MiB Infinity Cache)
+            gbps = ct.c_double()
+            if _abi.lib().rsp_hbm_copy_probe(dev, 1 << 30, 20, ct.byref(gbps)) == 0:
+                best = max(best, gbps.value)
+        if best > 0:
+            out['roofline']['stream_copy_GBps'] = best
+            out['roofline']['frac_of_stream_copy'] = achieved / best
         if a.e2e:
             out['e2e_h2d_bytes_per_frame'] = sz.C * sz.used_samples * sz.P * esz
             out['e2e_h2d_GBps'] = fps * out['e2e_h2d_bytes_per_frame'] / 1e9
