@@ -2114,6 +2114,9 @@ static int k1p_tpw(const Geometry& g) {
 }
 
 bool k1_persistent_fits(const Geometry& g) {
+#ifdef RSP_AB_K1_TILED   // timing-only builds: the tiled K1 everywhere
+    return false;
+#endif
     const int pts = g.prec == RSP_PREC_F64 ? 8 : 16;   // FFT points per thread (k1p_pts)
     return g.pow2P && g.logP >= 6 && g.logP <= 8 && k1p_tpw(g) > 0 && k1p_lds(g) <= 160 * 1024 &&
            g.B * g.NT * g.P <= pts * K1_THREADS && g.ncu > 0 && !g.k1_tiled;
@@ -2125,7 +2128,10 @@ static hipError_t launch_k1_t(const Geometry& g, const DevConsts& k, const Frame
     if (mode == 3 && k1_persistent_fits(g)) {
         // one FFT size per instantiation keeps the prefetch registers + FFT under 256 VGPRs
         const size_t ldsp = k1p_lds(g);
-        const int grid = std::min(g.ncu, nf * g.ntiles);
+#ifndef RSP_AB_K1P_GRID4   // timing-only builds: the persistent grid on GRID4/4 of the CUs
+#define RSP_AB_K1P_GRID4 4
+#endif
+        const int grid = std::min(g.ncu * RSP_AB_K1P_GRID4 / 4, nf * g.ntiles);
         constexpr int NJ = CP / 4, MB = BMAX <= 8 ? 1 : 2, TPW = (16 / NJ) / MB > 0 ? (16 / NJ) / MB : 1;
         const bool twice = k1p_tpw(g) == 2 * TPW;
 #define K1P_LAUNCH(LGP, TW)                                                                                      \
