@@ -10,7 +10,9 @@
 #ifndef RSP_NLANES
 #define RSP_NLANES 3         // streams the throughput queue uses (<= RSP_LANES)
 #endif
+#ifndef RSP_K2_POINTS
 #define RSP_K2_POINTS 4096   // complex points per pulse-compression workgroup
+#endif
 #define K2_THREADS 256       // threads per pulse-compression workgroup (16 points each)
 #define RSP_THREADS 256
 // Compile-time kernel choices (defaults = the shipped library; other values only for A/B

@@ -1153,7 +1153,8 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     constexpr bool WROW = nb0 >= 64 && NB0 == 1;
     if constexpr (WROW) {
         const int rl = __builtin_amdgcn_readfirstlane(tid / nb0);
-        const ZWin zw = zrow_window(g, z, row0 + rl, rows_total, off, lo, hi);
+        // waves past the block's rows (fewer rows than 256 / nb0) load nothing
+        const ZWin zw = zrow_window(g, z, row0 + rl, rl < rows ? rows_total : 0, off, lo, hi);
         const int j = tid & (nb0 - 1);
         const int np0 = a + j - lo + off;
         if ((nb0 & (g.NT - 1)) == 0) {   // uniform: element r sits r (nb0 P) past element 0
@@ -1334,8 +1335,11 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
     }
 }
 
+#ifndef RSP_K2_MINB
+#define RSP_K2_MINB (512 / K2_THREADS)   // workgroups per CU the compiler sizes k2_pc for
+#endif
 template <class T>
-__global__ __launch_bounds__(K2_THREADS, 512 / K2_THREADS) void k2_pc(Geometry g, DevConsts k, FramePtrs fp, int rows_total) {
+__global__ __launch_bounds__(K2_THREADS, RSP_K2_MINB) void k2_pc(Geometry g, DevConsts k, FramePtrs fp, int rows_total) {
     typedef cx<T> V;
     V* L = reinterpret_cast<V*>(rsp_lds);   // overlap-save rows | narrow: staged rows + taps
     const int f = blockIdx.y;
