@@ -10,6 +10,9 @@
 #ifndef RSP_NLANES
 #define RSP_NLANES 3         // streams the throughput queue uses (<= RSP_LANES)
 #endif
+#ifndef RSP_Z_LINE
+#define RSP_Z_LINE 0   // bytes of one row's z chunk (0: NT samples, the K1 tile width)
+#endif
 #ifndef RSP_K2_POINTS
 #define RSP_K2_POINTS 4096   // complex points per pulse-compression workgroup
 #endif
@@ -101,6 +104,7 @@ struct Geometry {
     int cpitch;      // device cube channel pitch in complex samples (= N*P)
     int Gp;          // row stride of the magnitude maps (G rounded up to 4)
     int NT, nU, ntiles, Ppad;
+    int NZ, nzc;     // z layout: NZ compacted samples per (row, chunk) slab, nzc chunks per row
     int twPp_elems;  // per-pass twiddles of the P-point FFT
     int pow2P, logP;
     int nseg, njobs, nwg_k2;

@@ -555,8 +555,8 @@ __device__ __forceinline__ int used_sample(const Geometry& g, int np) {
 
 // z (compacted Doppler-domain rows) addressing: row (b, v), compacted sample n'.
 __device__ __forceinline__ size_t zaddr(const Geometry& g, int b, int v, int np) {
-    const int lgNT = ilog2(g.NT);
-    return (((size_t)b * g.ntiles + (np >> lgNT)) * g.P + v) * g.NT + (np & (g.NT - 1));
+    const int lgNZ = ilog2(g.NZ);
+    return (((size_t)b * g.nzc + (np >> lgNZ)) * g.P + v) * g.NZ + (np & (g.NZ - 1));
 }
 
 // ======================================================================================
@@ -627,14 +627,15 @@ __device__ __forceinline__ void dbf_store(T* Yf, const typename Dbf<T>::Acc (&ac
 // column, so the lines fill within the workgroup.
 template <class V>
 struct StoreZ {
-    __amdgpu_buffer_rsrc_t z; int lgNT, ntiles, tile, P, half;
+    __amdgpu_buffer_rsrc_t z; int lgNT, nzc, tile, P, half, lgNZ;
     __device__ __forceinline__ void put(int, int row, int o, int, V x) const {
         const int b = row >> lgNT, nl = row & ((1 << lgNT) - 1);
         const int v = (o + half) & (P - 1);
+        const int np = (tile << lgNT) + nl;   // compacted sample
 #if RSP_K1_ABLATE & 4   // timing ablation only: no z stores
         if (x.x == (scal<V>)1234.5678)
 #endif
-        buf_st<RSP_Z_AUX>(z, (unsigned)(((((b * ntiles + tile) * P + v) << lgNT) + nl)) * (unsigned)sizeof(V), x);
+        buf_st<RSP_Z_AUX>(z, (unsigned)(((((b * nzc + (np >> lgNZ)) * P + v) << lgNZ) + (np & ((1 << lgNZ) - 1)))) * (unsigned)sizeof(V), x);
     }
 };
 
@@ -842,7 +843,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
         for (int e = threadIdx.x; e < B * zslab; e += K1_THREADS) {
             const int b = e / zslab, rem = e - b * zslab;
             const int v = rem >> lgNT, nl = rem & (NT - 1);
-            z[((size_t)b * g.ntiles + tile) * zslab + rem] = Y[(b * NT + nl) * Ppad + v];
+            z[zaddr(g, b, v, tile * NT + nl)] = Y[(b * NT + nl) * Ppad + v];
         }
         return;
     }
@@ -850,7 +851,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
     if (fft) {
         // ---- P-point FFT of every (b, nl) column (fsf:135); the last pass applies fftshift
         // and stores the [P][NT] slabs from registers
-        const StoreZ<V> sz{buf_rsrc(z, (unsigned)(B * g.ntiles * zslab * sizeof(V))), lgNT, g.ntiles, tile, P, half};
+        const StoreZ<V> sz{buf_rsrc(z, (unsigned)(B * g.nzc * P * g.NZ * sizeof(V))), lgNT, g.nzc, tile, P, half, ilog2(g.NZ)};
         k1_fft(g.logP, Y, Ppad, B * NT, twl, sz);
     } else {
         // non power-of-two P: direct DFT straight to global (O(P^2) per column)
@@ -868,7 +869,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
                 idx += kk;
                 if (idx >= P) idx -= P;
             }
-            z[((size_t)b * g.ntiles + tile) * zslab + rem] = acc;
+            z[zaddr(g, b, v, tile * NT + nl)] = acc;
         }
     }
 }
@@ -987,7 +988,7 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
             dbf_store<T, MB>(Yf, acc, grp, B, NT, Ppad, nlv[u], pv[u], wv_[u], K1_SH);
         }
     };
-    const int zslab = P * NT, lgNT = ilog2(NT), half = P >> 1;
+    const int lgNT = ilog2(NT), half = P >> 1;
     issue(TT);
     dbf(Y);
     __syncthreads();
@@ -998,7 +999,7 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
         const int f = __builtin_amdgcn_readfirstlane(TT / g.ntiles), tile = TT - f * g.ntiles;
         if (tile == 0 && threadIdx.x == 0 && fp.count[f]) *fp.count[f] = 0;   // K3's detection counter
         V* __restrict__ z = static_cast<V*>(fp.z[f]);
-        const StoreZ<V> sz{buf_rsrc(z, (unsigned)(B * g.ntiles * zslab * sizeof(V))), lgNT, g.ntiles, tile, P, half};
+        const StoreZ<V> sz{buf_rsrc(z, (unsigned)(B * g.nzc * P * g.NZ * sizeof(V))), lgNT, g.nzc, tile, P, half, ilog2(g.NZ)};
 #if RSP_K1_ABLATE & 1   // timing ablation only: no FFT, the tile goes to z as is
         for (int e = threadIdx.x; e < B * NT * P; e += K1_THREADS) {
             const int row = e >> LGP, o = e & (P - 1);
@@ -1078,13 +1079,13 @@ __device__ __forceinline__ ZWin zrow_window(const Geometry& g, const V* z, int r
     rho = rho & 15;
 #endif
     const int b = rho / g.P, v = rho - b * g.P;
-    w.lgNT = ilog2(g.NT);
-    w.NT1 = g.NT - 1;
-    w.PNT = g.P * g.NT;
+    w.lgNT = ilog2(g.NZ);
+    w.NT1 = g.NZ - 1;
+    w.PNT = g.P * g.NZ;
     const int nph = off + hi - lo;
     w.e_lo = (off >> w.lgNT) * w.PNT + (off & w.NT1);
     const int e_hi = (nph >> w.lgNT) * w.PNT + (nph & w.NT1);
-    const V* base = z + ((size_t)b * g.ntiles * g.P + v) * g.NT + w.e_lo;
+    const V* base = z + ((size_t)b * g.nzc * g.P + v) * g.NZ + w.e_lo;
     w.r = buf_rsrc(base, rho < rows_total ? (unsigned)(e_hi - w.e_lo + 1) * (unsigned)sizeof(V) : 0u);
     return w;
 }
@@ -1147,7 +1148,7 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     // every global load of the workgroup in flight together: the 16 samples of this thread's
     // pass-0 butterflies and its 16 filter-spectrum values (for the fused middle pass)
     V v0[NB0][R0];
-    const int lgNT = ilog2(g.NT);
+    const int lgNT = ilog2(g.NZ);
     // one row per wave (nb0 a multiple of 64, one butterfly per thread): the row's sample window
     // is a scalar buffer resource, and a load's offset needs no mask
     constexpr bool WROW = nb0 >= 64 && NB0 == 1;
@@ -1157,7 +1158,7 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
         const ZWin zw = zrow_window(g, z, row0 + rl, rl < rows ? rows_total : 0, off, lo, hi);
         const int j = tid & (nb0 - 1);
         const int np0 = a + j - lo + off;
-        if ((nb0 & (g.NT - 1)) == 0) {   // uniform: element r sits r (nb0 P) past element 0
+        if ((nb0 & (g.NZ - 1)) == 0) {   // uniform: element r sits r (nb0 P) past element 0
             const unsigned e0 = (unsigned)zw.rel(np0) * (unsigned)sizeof(V), st = (unsigned)(nb0 * P) * (unsigned)sizeof(V);
 #pragma unroll
             for (int r = 0; r < R0; ++r) v0[0][r] = buf_ld<V>(zw.r, e0 + r * st);
@@ -1166,7 +1167,7 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
             for (int r = 0; r < R0; ++r) v0[0][r] = buf_ld<V>(zw.r, (unsigned)zw.rel(np0 + r * nb0) * (unsigned)sizeof(V));
         }
     }
-    const __amdgpu_buffer_rsrc_t zr = buf_rsrc(z, (unsigned)(g.B * g.ntiles * P * g.NT * sizeof(V)));
+    const __amdgpu_buffer_rsrc_t zr = buf_rsrc(z, (unsigned)(g.B * g.nzc * P * g.NZ * sizeof(V)));
 #pragma unroll
     for (int t = 0; t < (WROW ? 0 : NB0); ++t) {
         const int beta = tid + t * K2_THREADS;
@@ -1176,9 +1177,9 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
         // z index of sample n0 + r nb0: when NT | nb0 the tile advances by nb0/NT per r and the
         // in-tile slot is fixed, so element r sits at zb + r (nb0 P) (one multiply per thread)
         const int np0 = a + j - lo + off;
-        const int zb = ((b * g.ntiles + (np0 >> lgNT)) * P + v) * g.NT + (np0 & (g.NT - 1));
+        const int zb = ((b * g.nzc + (np0 >> lgNT)) * P + v) * g.NZ + (np0 & (g.NZ - 1));
         // branch-free: every lane loads (an out-of-range offset when masked)
-        if ((nb0 & (g.NT - 1)) == 0) {   // uniform
+        if ((nb0 & (g.NZ - 1)) == 0) {   // uniform
 #pragma unroll
             for (int r = 0; r < R0; ++r) {
                 const int n = a + j + r * nb0;
@@ -1291,7 +1292,7 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
         const ZWin zw = zrow_window(g, z, row0, rows_total, off, lo, hi);
         const int j = tid;
         const int np0 = a + j - lo + off;
-        if ((nb0 & (g.NT - 1)) == 0) {   // uniform
+        if ((nb0 & (g.NZ - 1)) == 0) {   // uniform
             const unsigned e0 = (unsigned)zw.rel(np0) * (unsigned)sizeof(V), st = (unsigned)(nb0 * P) * (unsigned)sizeof(V);
 #pragma unroll
             for (int r = 0; r < R0; ++r) v0[0][r] = buf_ld<V>(zw.r, e0 + r * st);

@@ -945,6 +945,9 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
     if ((size_t)B * g.NT * g.Ppad * esz > 160 * 1024 || (g.pow2P && B * g.NT * P > 8192))
         return bail(fail(RSP_ERR_UNSUPPORTED, "B*P too large for the slow-time FFT tile"));
     g.ntiles = (g.nU + g.NT - 1) / g.NT;
+    // z chunks: NT samples (one K1 tile) per row slab, or RSP_Z_LINE bytes (A/B builds)
+    g.NZ = std::max(g.NT, RSP_Z_LINE / (int)esz);
+    g.nzc = (g.nU + g.NZ - 1) / g.NZ;
     if ((int)U.size() > RSP_MAX_IVL) return bail(fail(RSP_ERR_UNSUPPORTED, "too many sample intervals"));
     g.nivl = (int)U.size();
     for (int q = 0, st = 0; q < g.nivl; ++q) {
@@ -1057,7 +1060,7 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
         int gs = 1;
         for (const K2Job& jb : p->jobs) {
             const int rw = std::max(p->segs[jb.seg].rows_per_wg, 1);
-            gs = std::max(gs, std::min(8, 128 / std::max(rw * g.NT * esz, 1)));
+            gs = std::max(gs, std::min(8, 128 / std::max(rw * g.NZ * esz, 1)));
         }
         struct Gr { double key; int first; };
         std::vector<Gr> gr;
@@ -1085,7 +1088,7 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
         if ((rc = p->upload(&p->d_tx, tx))) return bail(rc);
     }
     if ((rc = p->dalloc(&p->d_tg, 64))) return bail(rc);
-    p->z_elems = (size_t)B * g.ntiles * g.NT * P;
+    p->z_elems = (size_t)B * g.nzc * g.NZ * P;
     p->rdm_elems = (size_t)B * P * G;
     g.Gp = (G + 3) & ~3;
     p->mag_elems = (size_t)B * P * g.Gp;
