@@ -64,9 +64,11 @@ def host_cpu():
     return {'model': model, 'nproc': os.cpu_count(), 'affinity': aff, 'cgroup_quota': quota, 'usable': usable}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--gpus', type=int, default=1,
+                    help='GPUs (ranks) of the run: under torchrun it must equal WORLD_SIZE; without it, N > 1 '
+                         'spawns N ranks through torch.distributed.run and relays rank 0\'s line')
     ap.add_argument('--steps', type=int, default=500)
     ap.add_argument('--warmup', type=int, default=20)
     ap.add_argument('--config', default='x2')
@@ -88,9 +90,56 @@ def parse():
                     help='collective backend for N > 1 (nccl = RCCL over xGMI; gloo: CPU tensors, for rehearsing '
                          'several ranks on one GPU together with --same-device)')
     ap.add_argument('--same-device', action='store_true', help='every rank uses GPU 0 (rehearsal only)')
+    ap.add_argument('--want-rdm', action='store_true',
+                    help='every frame also writes its complex range-Doppler map (rdm_13beam, fsf:131-136) to a '
+                         'device buffer of the caller (rsp_enqueue_device_rdm): the rsp_mex(\'cube\') contract; '
+                         'a secondary line, not the headline')
     ap.add_argument('--stage-timing', action='store_true',
                     help='HIP events around every kernel in the timed region (diagnostic: overlapped durations)')
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def launch_mode(gpus, env_world, visible, same_device, backend):
+    """What `bench.py --gpus N` does: ('run', None) in this process (N = 1, or a torchrun rank whose
+    WORLD_SIZE is N), ('spawn', None) to start N ranks, or ('error', message).  Pure: no GPU call;
+    `visible` = torch.cuda.device_count() (which does not initialise the GPU on this image)."""
+    if gpus < 1:
+        return 'error', '--gpus must be >= 1, got %d' % gpus
+    if env_world is not None:   # a rank started by torchrun / torch.distributed.run
+        if env_world != gpus:
+            return 'error', '--gpus %d but WORLD_SIZE=%d: launch one rank per GPU with --nproc-per-node %d' % (
+                gpus, env_world, gpus)
+        return 'run', None
+    if gpus == 1:
+        return 'run', None
+    if same_device:
+        if backend == 'nccl':
+            return 'error', ('--same-device puts every rank on GPU 0, which RCCL refuses; '
+                             'rehearse with --dist-backend gloo')
+    elif visible < gpus:
+        return 'error', '--gpus %d but only %d GPU(s) visible (rehearse on one GPU with --same-device ' \
+                        '--dist-backend gloo)' % (gpus, visible)
+    return 'spawn', None
+
+
+def spawn_ranks(gpus, argv):
+    """Start `gpus` ranks of this script with torch.distributed.run (rendezvous on 127.0.0.1) as a
+    child process -- this process never touches the GPU -- and relay rank 0's JSON line."""
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(('127.0.0.1', 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', str(gpus),
+           '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.abspath(__file__)] + list(argv)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+    if r.returncode != 0 or not lines:
+        sys.stderr.write(r.stdout)
+        return r.returncode or 1
+    print(lines[-1])
+    return 0
 
 
 def scene(cfg):
@@ -188,15 +237,19 @@ def main_music(a):
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', 0))
     dist = None
+    dev = 0 if (world == 1 or a.same_device) else local
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if a.dist_backend == 'nccl':
+            torch.cuda.set_device(dev)
+            dist.init_process_group('nccl', device_id=torch.device('cuda', dev))
+        else:
+            dist.init_process_group('gloo')
     from rsp.music import MusicPlan, music_1d_scene
     N, K, M, I = 64, 1024, 3, a.batch
     scene, scan, dl = music_1d_scene()
-    plan = MusicPlan(N, K, M, scan, dl, max_batch=I, device=local if world > 1 else 0, precision=a.precision)
+    plan = MusicPlan(N, K, M, scan, dl, max_batch=I, device=dev, precision=a.precision)
     f64 = a.precision == 'c128'
     mfma_peak = F64_PEAK_TFLOPS if f64 else MFMA_F32_PEAK_TFLOPS
     valu_peak = F64_PEAK_TFLOPS if f64 else MFMA_F32_PEAK_TFLOPS
@@ -217,7 +270,7 @@ def main_music(a):
     el = time.perf_counter() - t0
     if dist is not None:
         import torch
-        t = torch.tensor([el], dtype=torch.float64, device='cuda')
+        t = torch.tensor([el], dtype=torch.float64, device='cuda' if a.dist_backend == 'nccl' else 'cpu')
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     out = None
@@ -275,6 +328,17 @@ def main_music(a):
 
 def main():
     a = parse()
+    env_world = int(os.environ['WORLD_SIZE']) if 'WORLD_SIZE' in os.environ else None
+    visible = 0
+    if env_world is None and a.gpus > 1 and not a.same_device:
+        import torch
+        visible = torch.cuda.device_count()   # does not initialise the GPU (no HIP context)
+    mode, msg = launch_mode(a.gpus, env_world, visible, a.same_device, a.dist_backend)
+    if mode == 'error':
+        sys.stderr.write('bench.py: %s\n' % msg)
+        return 2
+    if mode == 'spawn':
+        return spawn_ranks(a.gpus, sys.argv[1:])
     if a.config == 'music5':
         return main_music(a)
     rank = int(os.environ.get('RANK', 0))
@@ -325,6 +389,11 @@ def main():
 
     nfr = max(a.warmup, 2 * NLANES, WARM_MIN, a.steps) * a.fpl   # the queue's argument lists, built before timing
     seq_cubes = [ring[i % len(ring)] for i in range(nfr)]
+    # --want-rdm: a ring of (lanes + 1) x fpl device RD maps; frame i writes map i mod len.  A map
+    # comes round again only after the batch that wrote it has been harvested (rsp_enqueue_device_rdm)
+    rdm_ring = [plan.device_alloc(sz.rdm_elems * sz.elem_bytes) for _ in range((NLANES + 1) * a.fpl)] \
+        if a.want_rdm else []
+    seq_rdms = [rdm_ring[i % len(rdm_ring)] for i in range(nfr)] if a.want_rdm else None
 
     def run(nbatches, base):   # nbatches full batches of fpl frames
         n = nbatches * a.fpl
@@ -332,11 +401,12 @@ def main():
             for i in range(n):
                 plan.enqueue_host(hring[i % len(hring)], base + i)
         else:
-            plan.enqueue_many(seq_cubes[:n], range(base, base + n))
+            plan.enqueue_many(seq_cubes[:n], range(base, base + n), rdms=seq_rdms[:n] if a.want_rdm else None)
         plan.drain()
 
     def run_all():   # config #3: each of this rank's frames once
-        plan.enqueue_many(ring, range(1 + f0, 1 + f0 + len(ring)))
+        plan.enqueue_many(ring, range(1 + f0, 1 + f0 + len(ring)),
+                          rdms=[rdm_ring[i % len(rdm_ring)] for i in range(len(ring))] if a.want_rdm else None)
         plan.drain()
 
     # warm-up: every lane (stream) with full batches, and >= WARM_MIN batches so that the clocks
@@ -386,7 +456,7 @@ def main():
         # the same F-frame batch with HIP events on the kernel's stream, chip otherwise idle.  In the
         # timed region consecutive batches overlap on the device (lanes), so a kernel's span there
         # is shared with the neighbouring batch's kernels; --stage-timing records those spans too.
-        prof = plan.profile_stages(ring, iters=a.profile_iters)
+        prof = plan.profile_stages(ring, iters=a.profile_iters, d_rdms=rdm_ring[:a.fpl] if a.want_rdm else None)
         stages = []
         for lv, pr in zip(live, prof):
             st = {'stage': pr['stage'], 'ms_per_launch': pr['ms'], 'frames_per_launch': pr['frames'],
@@ -423,6 +493,8 @@ def main():
             cfg_no = '3'
         if a.e2e:
             metric += ', end to end (host cubes in pinned memory -> H2D of the used samples -> chain)'
+        if a.want_rdm:
+            metric += ', complex range-Doppler map of every frame written to HBM (rsp_enqueue_device_rdm)'
         steps = (a.frames_total + a.fpl - 1) // a.fpl if a.frames_total else a.steps
         out = {
             'metric': metric,
@@ -434,7 +506,11 @@ def main():
             'dtype': 'fp64 (complex128)' if a.precision == 'c128' else 'fp32 (complex64)',
             'data': 'synthetic (device Philox noise + v8_2 targets)',
             'cells_per_s': fps * cells,
-            'achieved_GBps_frame': fps * frame_alg_bytes / 1e9,
+            'achieved_GBps_frame': fps * frame_alg_bytes / 1e9,   # SURVEY 8(d) bytes: cube read + RD map write
+            # the algorithmic bytes this run's kernels actually move per frame (K1 + K2 + K3 stage
+            # bytes; without --want-rdm the complex RD map is not written, only |RDM|)
+            'alg_bytes_moved_per_frame': sum(st['alg_bytes_per_launch'] for st in stages) / dom['frames_per_launch'],
+            'rdm_written': bool(a.want_rdm),
             'config': {'workload': 'BASELINE config #%s: %s C=%d B=%d N=%d P=%d G=%d' % (
                 cfg_no, a.config, sz.C, sz.B, sz.N, sz.P, sz.G), 'frames_per_launch': a.fpl, 'frames_per_step': a.fpl,
                 'ring': len(hring) if a.e2e else len(ring),
@@ -467,7 +543,7 @@ def main():
             out['cpu_baseline'] = cpu_baseline(cfg, cfar, clus, W, ang, k, targets, nframes=a.cpu_frames, name=a.config)
         else:
             out['cpu_baseline'] = None
-    for p in ring:
+    for p in ring + rdm_ring:
         plan.device_free(p)
     for h in hring:
         plan.host_free(h)
@@ -479,4 +555,4 @@ def main():
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main())

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RSP_ABI_VERSION 3
+#define RSP_ABI_VERSION 4
 
 typedef enum rsp_status {
     RSP_OK = 0,
@@ -216,6 +216,15 @@ int32_t rsp_synthesize_device(rsp_plan* plan, const rsp_target_in* targets, int3
 int32_t rsp_enqueue_device(rsp_plan* plan, const void* d_cube, int32_t frame_idx);
 /* rsp_enqueue_device for n frames in one call (d_cubes[i], frame_idx[i]). */
 int32_t rsp_enqueue_device_n(rsp_plan* plan, const void* const* d_cubes, const int32_t* frame_idx, int32_t n);
+/* rsp_enqueue_device that also produces the frame's complex range-Doppler map rdm_13beam
+ * (fsf:131-136, the rsp_mex('cube') output): K2 writes it straight into the caller's device buffer
+ * d_rdm (rsp_sizes.rdm_elems complex elements in the plan's precision, device layout [B][P][G],
+ * range fastest).  d_rdm must stay allocated, and must not be handed to another frame, until
+ * rsp_drain returns; the map is complete then.  Without it (rsp_enqueue_device) the map stays
+ * on chip and only |RDM| reaches HBM. */
+int32_t rsp_enqueue_device_rdm(rsp_plan* plan, const void* d_cube, int32_t frame_idx, void* d_rdm);
+int32_t rsp_enqueue_device_rdm_n(rsp_plan* plan, const void* const* d_cubes, const int32_t* frame_idx,
+                                 void* const* d_rdms, int32_t n);
 /* End-to-end form of rsp_enqueue_device: a host PNC cube in the plan's precision (no conversion;
  * rsp_process_cube converts).  Only the fast-time samples the chain reads (rsp_sizes.used_samples)
  * are copied, asynchronously on the plan's upload stream into a plan-owned device ring, so
@@ -269,6 +278,10 @@ int32_t rsp_process_stage2_gated(rsp_plan* plan, const void* iq_gated, int32_t d
  * Stage names via rsp_stage_name. */
 int32_t rsp_profile_stages(rsp_plan* plan, const void* const* d_cubes, int32_t n_cubes, int32_t iters,
                            float* ms_out, int64_t* bytes_out, int32_t cap, int32_t* frames_out);
+/* rsp_profile_stages with K2 writing every frame's complex RD map (d_rdms[f], f < nf, as
+ * rsp_enqueue_device_rdm); bytes_out[1] then includes the map.  d_rdms = NULL: rsp_profile_stages. */
+int32_t rsp_profile_stages_rdm(rsp_plan* plan, const void* const* d_cubes, int32_t n_cubes, void* const* d_rdms,
+                               int32_t iters, float* ms_out, int64_t* bytes_out, int32_t cap, int32_t* frames_out);
 const char* rsp_stage_name(int32_t stage);
 
 /* The box's streaming-copy bandwidth (SURVEY 8(d) "measured stream-copy peak"): a 16-B-per-lane

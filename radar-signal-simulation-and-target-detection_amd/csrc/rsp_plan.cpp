@@ -148,7 +148,7 @@ struct Lane {
     bool timed = false;
     hipEvent_t done = nullptr;
     void* z = nullptr;          // F frames
-    void* rdm = nullptr;        // F frames
+    void* rdm = nullptr;        // ONE frame: the synchronous paths' RDM (queue frames write the caller's maps)
     void* mag = nullptr;        // F frames
     DevDet* dets = nullptr;     // F x (1 + dcap): record 0 of each frame holds its count
     int dcap = 0;               // device detection-list capacity per frame (grows on demand)
@@ -255,6 +255,7 @@ struct rsp_plan {
     int64_t stage_launches = 0, stage_frames = 0;
     // pending batch of the queue
     const void* pend_in[RSP_MAX_F];
+    void* pend_rdm[RSP_MAX_F];  // caller's device RD map of each pending frame (nullptr: kept on chip)
     int pend_ids[RSP_MAX_F];
     int pend_slot[RSP_MAX_F];   // producer-ring slot of each pending frame, -1 = caller's device cube
     int npend = 0;
@@ -421,12 +422,16 @@ int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga,
 }
 
 // Device detection lists of a lane: F x (1 + cap) records (record 0 of a frame = its count).
+// The new lists are allocated first and swapped in only on success: a failed growth leaves the
+// lane with its old lists and capacity (still consistent for the next launch).
 int lane_dets_alloc(rsp_plan* p, Lane& L, int cap) {
+    const int ncap = std::max(cap, 1);
+    DevDet* nd = nullptr;
+    if (hipMalloc((void**)&nd, sizeof(DevDet) * (size_t)(ncap + 1) * p->F) != hipSuccess)
+        return fail(RSP_ERR_NOMEM, "hipMalloc of %d-detection lists failed", ncap);
     if (L.dets) HIPCHK(hipFree(L.dets));
-    L.dets = nullptr;
-    L.dcap = std::max(cap, 1);
-    if (hipMalloc((void**)&L.dets, sizeof(DevDet) * (size_t)(L.dcap + 1) * p->F) != hipSuccess)
-        return fail(RSP_ERR_NOMEM, "hipMalloc of %d-detection lists failed", L.dcap);
+    L.dets = nd;
+    L.dcap = ncap;
     return RSP_OK;
 }
 
@@ -455,22 +460,24 @@ int setup_lane(rsp_plan* p, Lane& L) {
     for (auto& e : L.tev) HIPCHK(hipEventCreate(&e));
     int rc;
     if ((rc = p->dalloc_bytes(&L.z, p->z_elems * p->F * p->esz))) return rc;
-    if ((rc = p->dalloc_bytes(&L.rdm, p->rdm_elems * p->F * p->esz))) return rc;
+    if ((rc = p->dalloc_bytes(&L.rdm, p->rdm_elems * p->esz))) return rc;   // one frame (sync paths)
     if ((rc = p->dalloc_bytes(&L.mag, p->mag_elems * p->F * p->rsz))) return rc;
     if ((rc = lane_dets_alloc(p, L, std::min(p->det_bound, 4096)))) return rc;
     return lane_host_alloc(p, L, std::min(p->det_bound, 1024));
 }
 
-// rdm = false: K2 keeps the complex RD map on chip and stores only its magnitudes, the one
-// input of K3 and S9.  fun_process_single_frame returns final_targets (fsf:13); its rdm_13beam
-// is an intermediate, so the throughput queue does not write it to HBM (-10% k2_pc); frames
-// whose RDM is asked for (rsp_process_frame with out->rdm, process_stage2) write it.
-FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const void* const* in, int nf, bool rdm = true) {
+// rdm[f] = nullptr: K2 keeps frame f's complex RD map on chip and stores only its magnitudes,
+// the one input of K3 and S9.  fun_process_single_frame returns final_targets (fsf:13); its
+// rdm_13beam is an intermediate, so the throughput queue does not write it to HBM (-10% k2_pc)
+// unless the caller hands a map for the frame (rsp_enqueue_device_rdm).  rdm == nullptr: no
+// frame writes its map.  The synchronous paths (rsp_process_* with out->rdm, process_stage2)
+// run one frame into the lane's own map L.rdm.
+FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const void* const* in, int nf, void* const* rdm) {
     FramePtrs fp{};
     for (int f = 0; f < nf; ++f) {
         fp.in[f] = in[f];
         fp.z[f] = (char*)L.z + p->z_elems * p->esz * f;
-        fp.rdm[f] = rdm ? (char*)L.rdm + p->rdm_elems * p->esz * f : nullptr;
+        fp.rdm[f] = rdm ? rdm[f] : nullptr;
         fp.mag[f] = (char*)L.mag + p->mag_elems * p->rsz * f;
         DevDet* rec = L.dets + (size_t)(L.dcap + 1) * f;
         fp.count[f] = reinterpret_cast<int*>(rec);   // zeroed by K1, bumped by K3
@@ -491,8 +498,8 @@ FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const void* const* in, int
 #define RSP_K12_SUB 0
 #endif
 int launch_batch(rsp_plan* p, Lane& L, const void* const* in, const int* ids, int nf, void* smap = nullptr,
-                 const int* slots = nullptr, bool want_rdm = false) {
-    FramePtrs fp = lane_ptrs(p, L, in, nf, want_rdm);
+                 const int* slots = nullptr, void* const* rdm = nullptr) {
+    FramePtrs fp = lane_ptrs(p, L, in, nf, rdm);
     fp.smap[0] = smap;
     if (slots)   // producer-ring frames: K1 after their upload / synthesis
         for (int f = 0; f < nf; ++f)
@@ -614,7 +621,7 @@ int flush_pending(rsp_plan* p) {
     Lane& L = p->lanes[p->next_lane];
     int rc = harvest(p, L);
     if (rc) return rc;
-    rc = launch_batch(p, L, p->pend_in, p->pend_ids, p->npend, nullptr, p->pend_slot);
+    rc = launch_batch(p, L, p->pend_in, p->pend_ids, p->npend, nullptr, p->pend_slot, p->pend_rdm);
     p->npend = 0;
     p->next_lane = (p->next_lane + 1) % p->nlanes;
     return rc;
@@ -656,12 +663,13 @@ int ring_acquire(rsp_plan* p, int* slot) {
     return RSP_OK;
 }
 
-int enqueue_frame(rsp_plan* p, const void* d_cube, int slot, int frame_idx) {
+int enqueue_frame(rsp_plan* p, const void* d_cube, int slot, int frame_idx, void* d_rdm = nullptr) {
     if (slot >= 0) {
         HIPCHK(hipEventRecord(p->slot_ready[slot], p->up_stream));
         p->slot_used[slot] = 1;
     }
     p->pend_in[p->npend] = d_cube;
+    p->pend_rdm[p->npend] = d_rdm;
     p->pend_ids[p->npend] = frame_idx;
     p->pend_slot[p->npend] = slot;
     if (++p->npend == p->F) return flush_pending(p);
@@ -759,7 +767,8 @@ int run_sync_frame(rsp_plan* p, const void* d_in, int frame_idx, rsp_frame_out* 
         if (!p->d_smap && (rc = p->dalloc_bytes(&p->d_smap, (size_t)(p->g.B - 1) * p->g.P * p->g.G * p->rsz))) return rc;
         smap = p->d_smap;
     }
-    if ((rc = launch_batch(p, L, in, ids, 1, smap, nullptr, out && out->rdm))) return rc;
+    void* rdm[1] = {L.rdm};
+    if ((rc = launch_batch(p, L, in, ids, 1, smap, nullptr, out && out->rdm ? rdm : nullptr))) return rc;
     if ((rc = harvest(p, L, &dets))) return rc;
     FrameResult fr = p->results.back();
     p->results.resize(nres);   // synchronous frames do not enter the queue's result list
@@ -1198,6 +1207,24 @@ int32_t rsp_enqueue_device_n(rsp_plan* p, const void* const* d_cubes, const int3
     return RSP_OK;
 }
 
+int32_t rsp_enqueue_device_rdm(rsp_plan* p, const void* d_cube, int32_t frame_idx, void* d_rdm) {
+    if (!p || !d_cube || !d_rdm) return fail(RSP_ERR_INVALID, "null argument");
+    HIPCHK(hipSetDevice(p->device));
+    return enqueue_frame(p, d_cube, -1, frame_idx, d_rdm);
+}
+
+int32_t rsp_enqueue_device_rdm_n(rsp_plan* p, const void* const* d_cubes, const int32_t* frame_idx, void* const* d_rdms,
+                                 int32_t n) {
+    if (!p || (n > 0 && (!d_cubes || !frame_idx || !d_rdms)) || n < 0) return fail(RSP_ERR_INVALID, "bad argument");
+    HIPCHK(hipSetDevice(p->device));
+    for (int i = 0; i < n; ++i) {
+        if (!d_cubes[i] || !d_rdms[i]) return fail(RSP_ERR_INVALID, "cube or map %d is null", i);
+        int rc = enqueue_frame(p, d_cubes[i], -1, frame_idx[i], d_rdms[i]);
+        if (rc) return rc;
+    }
+    return RSP_OK;
+}
+
 int32_t rsp_enqueue_host(rsp_plan* p, const void* h_cube, int32_t dtype, int32_t frame_idx) {
     if (!p || !h_cube) return fail(RSP_ERR_INVALID, "null argument");
     if (dtype != (p->g.prec == RSP_PREC_F64 ? RSP_C128 : RSP_C64))
@@ -1379,7 +1406,8 @@ int32_t rsp_process_stage2(rsp_plan* p, const void* iq, int32_t dtype, double* m
     if ((rc = upload_cube(p, iq, dtype, gs.B, p->d_cube, L.stream))) return rc;
     if (!p->d_aux && (rc = p->dalloc_bytes(&p->d_aux, p->rdm_elems * p->esz))) return rc;
     const void* in[1] = {p->d_cube};
-    const FramePtrs fp = lane_ptrs(p, L, in, 1);
+    void* rdm[1] = {L.rdm};
+    const FramePtrs fp = lane_ptrs(p, L, in, 1, rdm);
     HIPCHK(launch_k1(gs, p->k, fp, 1, 0, L.stream));
     HIPCHK(launch_k2(gs, p->k, fp, 1, gs.B * gs.P, L.stream));      // PC rows (b, m) -> L.rdm
     HIPCHK(launch_mtd_cols(gs, p->k, L.rdm, p->d_aux, L.stream));  // S7 over pulses
@@ -1422,6 +1450,11 @@ int32_t rsp_process_stage2_gated(rsp_plan* p, const void* iq, int32_t dtype, int
 
 int32_t rsp_profile_stages(rsp_plan* p, const void* const* d_cubes, int32_t n_cubes, int32_t iters, float* ms_out,
                            int64_t* bytes_out, int32_t cap, int32_t* frames_out) {
+    return rsp_profile_stages_rdm(p, d_cubes, n_cubes, nullptr, iters, ms_out, bytes_out, cap, frames_out);
+}
+
+int32_t rsp_profile_stages_rdm(rsp_plan* p, const void* const* d_cubes, int32_t n_cubes, void* const* d_rdms,
+                               int32_t iters, float* ms_out, int64_t* bytes_out, int32_t cap, int32_t* frames_out) {
     if (!p || !d_cubes || n_cubes < 1 || iters < 1) return fail(RSP_ERR_INVALID, "bad argument");
     HIPCHK(hipSetDevice(p->device));
     int rc = drain_all(p);
@@ -1435,7 +1468,7 @@ int32_t rsp_profile_stages(rsp_plan* p, const void* const* d_cubes, int32_t n_cu
     for (int j = 0; j < nsets; ++j) {
         const void* in[RSP_MAX_F];
         for (int f = 0; f < nf; ++f) in[f] = d_cubes[(j * nf + f) % n_cubes];
-        fps[j] = lane_ptrs(p, L, in, nf, false);   // as the queue: no complex RDM stores
+        fps[j] = lane_ptrs(p, L, in, nf, d_rdms);   // as the queue: complex RDM stores only into d_rdms
     }
     const Geometry& g = p->g;
     hipEvent_t e0, e1;
@@ -1471,7 +1504,8 @@ int32_t rsp_profile_stages(rsp_plan* p, const void* const* d_cubes, int32_t n_cu
         const int64_t z = (int64_t)g.B * g.nU * g.P * es;          // Doppler-domain rows
         const int64_t mag = (int64_t)g.B * g.P * g.G * rs;         // |RD| map (the RDM stays on chip)
         if (cap > 0) bytes_out[0] = nf * (cube + z);
-        if (cap > 1) bytes_out[1] = nf * (z + mag);
+        const int64_t rdm = d_rdms ? (int64_t)g.B * g.P * g.G * es : 0;   // the RD map, when written
+        if (cap > 1) bytes_out[1] = nf * (z + mag + rdm);
         if (cap > 2) bytes_out[2] = nf * mag;
     }
     return RSP_OK;

@@ -15,7 +15,9 @@
  *   [MTD_results, PC_results] = rsp_mex('stage2', iq_data, config, precomputed_data [, opts])
  *       process_stage2_mtd.m:1 on beamformed iq_data [P x N x B] (full PRT) or [P x Ng x B]
  *       gated like the v2 .mat frames (opts.gate_cols 3 x 2, default 83:310, 311:1033, 1034:3486).
- *   rsp_mex('clear')      -- destroys the cached plan.
+ *   [phi_e, P_MUSIC_dB, EVA, R] = rsp_mex('music', X1, M, phi_list, d_over_lambda [, opts])
+ *       MUSIC_1D.m:26-48 on snapshots X1 [N x K] (or a batch [N x K x I]); see music_cmd.
+ *   rsp_mex('clear')      -- destroys the cached plans.
  *
  * opts (optional struct): seed (20250101), device (0), precision ('double' (default) | 'single'),
  * frames_per_launch (1), gate_cols.
@@ -43,6 +45,8 @@ static void cleanup(void) {
     g_key = NULL;
     g_key_len = 0;
 }
+
+static void exit_all(void);   /* mexAtExit keeps one function: both cached plans */
 
 static void check(int32_t rc) {
     if (rc != RSP_OK) mexErrMsgIdAndTxt("radar:rsp", "librsp: %s", rsp_last_error());
@@ -241,7 +245,7 @@ static void ensure_plan(Inputs* in) {
     memcpy(g_key, b.p, b.n);
     g_key_len = b.n;
     mxFree(b.p);
-    mexAtExit(cleanup);
+    mexAtExit(exit_all);
 }
 
 /* ---- outputs ------------------------------------------------------------------------------- */
@@ -294,16 +298,128 @@ static void frame_inputs(int nrhs, const mxArray* prhs[], Inputs* in, uint64_t* 
     read_opts(nrhs > 7 ? prhs[7] : NULL, &in->opt, seed, cols, &hc);
 }
 
+/* ---- MUSIC (MUSIC_1D.m:26-48) ----------------------------------------------------------------
+ * [phi_e, P_MUSIC_dB, EVA, R] = rsp_mex('music', X1, M, phi_list, d_over_lambda [, opts])
+ * X1 [N x K] or [N x K x I] complex (double or single) snapshots; phi_list the scan grid in rad
+ * (MUSIC_1D.m:35); d_over_lambda = d / lambda (MUSIC_1D.m:11).  phi_e [M x I] in degrees
+ * (MUSIC_1D.m:47; NaN where findpeaks found fewer than M peaks), P_MUSIC_dB [n_scan x I] (:41),
+ * EVA [N x I] descending (:30-31), R [N x N x I] (:28).  opts: device, precision.  The MUSIC plan
+ * is cached apart from the frame plan and rebuilt when N, K, M, I, the grid or opts change. */
+static rsp_music_plan* g_music = NULL;
+static unsigned char* g_music_key = NULL;
+static size_t g_music_key_len = 0;
+
+static void music_cleanup(void) {
+    if (g_music) rsp_music_destroy(g_music);
+    g_music = NULL;
+    free(g_music_key);
+    g_music_key = NULL;
+    g_music_key_len = 0;
+}
+
+static void music_cmd(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    const mxArray* x;
+    const mwSize* dims;
+    mwSize nscan, nd, i, m;
+    rsp_music_config cfg;
+    rsp_music_out out;
+    int32_t dtype, device = 0, I;
+    const void* data;
+    const double* scan;
+    int32_t* pk;
+    int32_t* npk;
+    Buf b = {NULL, 0, 0};
+    if (nrhs < 5) mexErrMsgIdAndTxt("radar:rsp", "usage: rsp_mex('music', X1, M, phi_list, d_over_lambda [, opts])");
+    x = prhs[1];
+    nd = mxGetNumberOfDimensions(x);
+    dims = mxGetDimensions(x);
+    if (nd > 3) mexErrMsgIdAndTxt("radar:rsp", "X1 must be N x K or N x K x I");
+    if (mxIsDouble(x) && mxIsComplex(x)) { dtype = RSP_C128; data = mxGetComplexDoubles(x); }
+    else if (mxIsSingle(x) && mxIsComplex(x)) { dtype = RSP_C64; data = mxGetComplexSingles(x); }
+    else mexErrMsgIdAndTxt("radar:rsp", "X1 must be complex double or single");
+    scan = real_arr(prhs[3], &nscan);
+    memset(&cfg, 0, sizeof cfg);
+    cfg.channel_num = (int32_t)dims[0];
+    cfg.num_snapshots = (int32_t)dims[1];
+    I = nd == 3 ? (int32_t)dims[2] : 1;
+    cfg.num_sources = (int32_t)mxGetScalar(prhs[2]);
+    cfg.n_scan = (int32_t)nscan;
+    cfg.d_over_lambda = mxGetScalar(prhs[4]);
+    cfg.scan_rad = scan;
+    cfg.max_batch = I;
+    cfg.precision = RSP_C128;
+    if (nrhs > 5 && mxIsStruct(prhs[5])) {
+        const mxArray* o = prhs[5];
+        if (mxGetField(o, 0, "device")) device = (int32_t)mxGetScalar(mxGetField(o, 0, "device"));
+        if (mxGetField(o, 0, "precision")) {
+            char s[16];
+            mxGetString(mxGetField(o, 0, "precision"), s, sizeof s);
+            if (!strcmp(s, "single")) cfg.precision = RSP_C64;
+            else if (strcmp(s, "double")) mexErrMsgIdAndTxt("radar:rsp", "opts.precision must be 'double' or 'single'");
+        }
+    }
+    {   /* cache key: the config without its borrowed pointer, the device and the grid */
+        rsp_music_config k = cfg;
+        k.scan_rad = NULL;
+        put(&b, &k, sizeof k);
+        put(&b, &device, sizeof device);
+        key_arr(&b, scan, nscan);
+    }
+    if (!(g_music && g_music_key_len == b.n && !memcmp(g_music_key, b.p, b.n))) {
+        music_cleanup();
+        check(rsp_music_create(&cfg, device, &g_music));
+        g_music_key = (unsigned char*)malloc(b.n);
+        memcpy(g_music_key, b.p, b.n);
+        g_music_key_len = b.n;
+        mexAtExit(exit_all);
+    }
+    mxFree(b.p);
+    memset(&out, 0, sizeof out);
+    pk = (int32_t*)mxCalloc((size_t)cfg.num_sources * I, sizeof(int32_t));
+    npk = (int32_t*)mxCalloc((size_t)I, sizeof(int32_t));
+    out.peak_idx = pk;
+    out.n_peaks = npk;
+    plhs[0] = mxCreateDoubleMatrix((mwSize)cfg.num_sources, (mwSize)I, mxREAL);
+    if (nlhs > 1) {
+        plhs[1] = mxCreateDoubleMatrix(nscan, (mwSize)I, mxREAL);
+        out.spectrum_db = mxGetDoubles(plhs[1]);
+    }
+    if (nlhs > 2) {
+        plhs[2] = mxCreateDoubleMatrix(dims[0], (mwSize)I, mxREAL);
+        out.eigenvalues = mxGetDoubles(plhs[2]);
+    }
+    if (nlhs > 3) {
+        mwSize d[3];
+        d[0] = dims[0]; d[1] = dims[0]; d[2] = (mwSize)I;
+        plhs[3] = mxCreateNumericArray(3, d, mxDOUBLE_CLASS, mxCOMPLEX);
+        out.covariance = (double*)mxGetComplexDoubles(plhs[3]);
+    }
+    check(rsp_music_process(g_music, data, dtype, I, &out));
+    {   /* phi_e = phi_list(P_peaks_idx) * 180 / pi (MUSIC_1D.m:47), 1-based indices */
+        double* phi = mxGetDoubles(plhs[0]);
+        for (i = 0; i < (mwSize)I; ++i)
+            for (m = 0; m < (mwSize)cfg.num_sources; ++m) {
+                const int32_t p = pk[i * cfg.num_sources + m];
+                phi[i * cfg.num_sources + m] = p > 0 ? scan[p - 1] * 180.0 / 3.14159265358979323846 : mxGetNaN();
+            }
+    }
+}
+
+static void exit_all(void) {
+    cleanup();
+    music_cleanup();
+}
+
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     char cmd[16];
     Inputs in;
     uint64_t seed;
     rsp_sizes sz;
     memset(&in, 0, sizeof in);
-    if (nrhs < 1 || !mxIsChar(prhs[0])) mexErrMsgIdAndTxt("radar:rsp", "first argument: 'frame', 'cube', 'stage2' or 'clear'");
+    if (nrhs < 1 || !mxIsChar(prhs[0])) mexErrMsgIdAndTxt("radar:rsp", "first argument: 'frame', 'cube', 'stage2', 'music' or 'clear'");
     mxGetString(prhs[0], cmd, sizeof cmd);
     if (!strcmp(cmd, "clear")) {
-        cleanup();
+        exit_all();
         return;
     }
     if (!strcmp(cmd, "frame")) {   /* fun_process_single_frame(targets, config, ..., frame_idx) */
@@ -397,6 +513,10 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         else
             check(rsp_process_stage2_gated(g_plan, data, dtype, (int32_t)dims[1], hc ? cols : NULL,
                                            (double*)mxGetComplexDoubles(plhs[0]), (double*)mxGetComplexDoubles(plhs[1])));
+        return;
+    }
+    if (!strcmp(cmd, "music")) {   /* MUSIC_1D.m:26-48 */
+        music_cmd(nlhs, plhs, nrhs, prhs);
         return;
     }
     mexErrMsgIdAndTxt("radar:rsp", "unknown command '%s'", cmd);

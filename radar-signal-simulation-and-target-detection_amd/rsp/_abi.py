@@ -144,6 +144,8 @@ PROTOTYPES = {
                                            ct.c_double, _P]),
     'rsp_enqueue_device': (ct.c_int32, [_P, _P, ct.c_int32]),
     'rsp_enqueue_device_n': (ct.c_int32, [_P, ct.POINTER(_P), ct.POINTER(ct.c_int32), ct.c_int32]),
+    'rsp_enqueue_device_rdm': (ct.c_int32, [_P, _P, ct.c_int32, _P]),
+    'rsp_enqueue_device_rdm_n': (ct.c_int32, [_P, ct.POINTER(_P), ct.POINTER(ct.c_int32), ct.POINTER(_P), ct.c_int32]),
     'rsp_enqueue_host': (ct.c_int32, [_P, _P, ct.c_int32, ct.c_int32]),
     'rsp_host_alloc': (ct.c_int32, [_P, ct.c_int64, ct.POINTER(_P)]),
     'rsp_host_free': (ct.c_int32, [_P, _P]),
@@ -162,6 +164,9 @@ PROTOTYPES = {
     'rsp_process_stage2_gated': (ct.c_int32, [_P, _P, ct.c_int32, ct.c_int32, ct.POINTER(ct.c_int32), _dp, _dp]),
     'rsp_profile_stages': (ct.c_int32, [_P, ct.POINTER(_P), ct.c_int32, ct.c_int32, ct.POINTER(ct.c_float),
                                         ct.POINTER(ct.c_int64), ct.c_int32, ct.POINTER(ct.c_int32)]),
+    'rsp_profile_stages_rdm': (ct.c_int32, [_P, ct.POINTER(_P), ct.c_int32, ct.POINTER(_P), ct.c_int32,
+                                            ct.POINTER(ct.c_float), ct.POINTER(ct.c_int64), ct.c_int32,
+                                            ct.POINTER(ct.c_int32)]),
     'rsp_stage_name': (ct.c_char_p, [ct.c_int32]),
     'rsp_hbm_copy_probe': (ct.c_int32, [ct.c_int32, ct.c_int64, ct.c_int32, ct.POINTER(ct.c_double)]),
     'rsp_set_stage_timing': (ct.c_int32, [_P, ct.c_int32]),

@@ -88,9 +88,14 @@ def stage2_config(config):
         raise KeyError('config.Sig_Config needs point_prt_segments or point_prt = [total narrow medium long]')
     B = int(config.get('mtd', {}).get('beam_num', sc['beam_num']))
     d = config.get('Array', {}).get('element_spacing', 0.0138)
-    return make_config(prtNum=int(sc['prtNum']), prt=prt, channel_num=int(sc.get('channel_num', B)), beam_num=B,
-                       tao=tuple(sc['tao']), gap_duration=tuple(sc.get('gap_duration', (11.4e-6, 31.8e-6, 153.4e-6))),
-                       point_prt_segments=segs, fs=fs, fc=float(sc['fc']), B=float(sc['B']), element_spacing=d)
+    out = make_config(prtNum=int(sc['prtNum']), prt=prt, channel_num=int(sc.get('channel_num', B)), beam_num=B,
+                      tao=tuple(sc['tao']), gap_duration=tuple(sc.get('gap_duration', (11.4e-6, 31.8e-6, 153.4e-6))),
+                      point_prt_segments=segs, fs=fs, fc=float(sc['fc']), B=float(sc['B']), element_spacing=d)
+    if 'c' in sc:   # the caller's c, as matlab/process_stage2_mtd.m (s.c = sc.c; s.wavelength = s.c / s.fc)
+        o = out['Sig_Config']
+        o['c'] = float(sc['c'])
+        o['wavelength'] = o['c'] / o['fc']
+    return out
 
 
 def default_cfar_params():

@@ -227,12 +227,27 @@ class Plan:
     def enqueue(self, ptr, frame_idx):
         check(lib().rsp_enqueue_device(self.h, ct.c_void_p(ptr), int(frame_idx)))
 
-    def enqueue_many(self, ptrs, frame_ids):
-        """rsp_enqueue_device_n: device cubes ptrs[i] as frames frame_ids[i], one C call."""
+    def enqueue_many(self, ptrs, frame_ids, rdms=None):
+        """rsp_enqueue_device_n: device cubes ptrs[i] as frames frame_ids[i], one C call.  With
+        ``rdms`` (device pointers, one per frame, rdm_elems complex elements each) every frame's
+        complex RD map is written there (rsp_enqueue_device_rdm_n), complete after drain()."""
         n = len(ptrs)
         arr = (ct.c_void_p * max(n, 1))(*ptrs)
         ids = (ct.c_int32 * max(n, 1))(*[int(f) for f in frame_ids])
-        check(lib().rsp_enqueue_device_n(self.h, arr, ids, n))
+        if rdms is None:
+            check(lib().rsp_enqueue_device_n(self.h, arr, ids, n))
+        else:
+            if len(rdms) != n:
+                raise ValueError('one RD map per frame')
+            ra = (ct.c_void_p * max(n, 1))(*rdms)
+            check(lib().rsp_enqueue_device_rdm_n(self.h, arr, ids, ra, n))
+
+    def rdm_from_device(self, ptr):
+        """A device RD map ([B][P][G], plan precision, as rsp_enqueue_device_rdm writes it) as the
+        MATLAB-shaped [P, G, B] complex array of rdm_13beam (fsf:135)."""
+        sz = self.sizes
+        m = self.device_download(ptr, sz.rdm_elems, self.cdtype).reshape(sz.B, sz.P, sz.G)
+        return np.transpose(m, (1, 2, 0))
 
     def host_alloc(self, nbytes):
         """Pinned host memory (rsp_host_alloc); returns the address."""
@@ -311,8 +326,9 @@ class Plan:
         return [{'stage': lib().rsp_stage_name(i).decode(), 'ms_total': ms[i], 'launches': nl.value,
                  'frames': nf.value} for i in range(n)]
 
-    def profile_stages(self, d_cubes, iters=20):
-        """Per-stage HIP-event timing; d_cubes = device pointer or list of pointers (batched)."""
+    def profile_stages(self, d_cubes, iters=20, d_rdms=None):
+        """Per-stage HIP-event timing; d_cubes = device pointer or list of pointers (batched).
+        d_rdms: K2 also writes each frame's complex RD map there (rsp_profile_stages_rdm)."""
         if not isinstance(d_cubes, (list, tuple)):
             d_cubes = [d_cubes]
         n = self.sizes.n_stages
@@ -320,7 +336,8 @@ class Plan:
         by = (ct.c_int64 * n)()
         arr = (ct.c_void_p * len(d_cubes))(*d_cubes)
         nf = ct.c_int32()
-        check(lib().rsp_profile_stages(self.h, arr, len(d_cubes), int(iters), ms, by, n, ct.byref(nf)))
+        ra = (ct.c_void_p * len(d_rdms))(*d_rdms) if d_rdms else None
+        check(lib().rsp_profile_stages_rdm(self.h, arr, len(d_cubes), ra, int(iters), ms, by, n, ct.byref(nf)))
         return [{'stage': lib().rsp_stage_name(i).decode(), 'ms': ms[i], 'bytes': by[i], 'frames': nf.value}
                 for i in range(n)]
 

@@ -35,6 +35,7 @@ mxArray* mxCreateNumericArray(mwSize ndim, const mwSize* dims, mxClassID classid
 void* mxCalloc(mwSize n, mwSize size);
 void* mxRealloc(void* ptr, mwSize size);
 void mxFree(void* ptr);
+double mxGetNaN(void);
 void mexErrMsgIdAndTxt(const char* errorid, const char* errormsg, ...);
 int mexAtExit(void (*exit_fcn)(void));
 #endif

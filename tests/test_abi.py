@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert _abi.lib().rsp_abi_version() == 3
+    assert _abi.lib().rsp_abi_version() == 4
 
 
 STRUCTS = {'rsp_sig_config': _abi.SigConfig, 'rsp_cfar_params': _abi.CfarParams,

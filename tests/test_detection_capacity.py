@@ -101,3 +101,33 @@ def test_dense_hits_complex_single_queue_equals_sync():
             assert r['final_targets'] == sync['final_targets']
     finally:
         plan.close()
+
+
+def test_between_readback_and_device_capacity():
+    """A frame with more detections than the pinned read-back holds (1024) but fewer than the
+    device list (4096): harvest takes the first 1024 from the read-back and the rest by a direct
+    copy, without regrowing the device list.  On a fresh plan the queue must give the synchronous
+    path's lists (counts and final targets) for every frame."""
+    s = scenario('small')
+    cube = noisy_cube(s, targets_for('small'), dtype=np.complex128)
+    cfar = dict(s['cfar'], T_CFAR=2.0)
+    qplan = Plan(s['cfg'], cfar, s['clus'], s['pre_p'], frames_per_launch=2)   # fresh: initial capacities
+    splan = Plan(s['cfg'], cfar, s['clus'], s['pre_p'])
+    try:
+        d = qplan.device_alloc(qplan.cube_bytes)
+        try:
+            qplan.upload_cube(d, cube)
+            qplan.enqueue_many([d] * 4, range(20, 24))
+            qplan.drain()
+            res = qplan.results()
+        finally:
+            qplan.device_free(d)
+        sync = splan.process_cube(cube, frame_idx=1)
+        n = len(sync['detections'])
+        assert 1024 < n <= 4096, n
+        for r in res:
+            assert r['n_dets'] == n
+            assert r['final_targets'] == sync['final_targets']
+    finally:
+        qplan.close()
+        splan.close()

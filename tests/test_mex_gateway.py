@@ -71,3 +71,169 @@ def test_integration_matlab_wrappers_match_committed_files():
     code = [ln for ln in committed.splitlines() if ln.strip() and not ln.lstrip().startswith('%')]
     assert [ln for ln in block[0].splitlines() if ln.strip()] == code
     assert 'persistent inited' not in doc and "rsp_mex('init'" not in doc
+    for name in ('music_1d_gpu.m', 'music_1d_calllib.m'):   # shown verbatim (comments included)
+        committed = open(os.path.join(d, name)).read()
+        first = committed.splitlines()[0]
+        block = [b for b in re.findall(r'```matlab\n(.*?)```', doc, re.S) if b.splitlines()[0] == first]
+        assert block == [committed], name
+
+
+# ---- MATLAB loadlibrary/calllib bindings: libstruct fields and libpointer classes vs rsp.h ----
+HEADER = os.path.join(ROOT, 'include', 'rsp.h')
+MATLAB_DIR = os.path.dirname(MEX)
+
+
+def _c_structs():
+    """{struct name: {field: C type}} of every typedef struct in include/rsp.h."""
+    src = re.sub(r'/\*.*?\*/', '', open(HEADER).read(), flags=re.S)
+    out = {}
+    for name, body in re.findall(r'typedef struct (\w+) \{(.*?)\}\s*\w+;', src, re.S):
+        fields = {}
+        for decl in body.split(';'):
+            decl = decl.strip()
+            if not decl:
+                continue
+            m = re.match(r'((?:const\s+)?\w+\s*\**)\s*(.*)$', decl)
+            base = m.group(1).replace('const', '').replace(' ', '')
+            for f in m.group(2).split(','):
+                f = f.strip()
+                arr = re.match(r'(\w+)\[(\d+)\]', f)
+                stars = base.count('*') + len(re.match(r'\**', f).group(0))
+                fname = arr.group(1) if arr else f.lstrip('*')
+                fields[fname] = base.rstrip('*') + '*' * stars + ('[]' if arr else '')
+        out[name] = fields
+    return out
+
+
+def _c_prototypes():
+    """{function: [argument C types]} of include/rsp.h."""
+    src = re.sub(r'/\*.*?\*/', '', open(HEADER).read(), flags=re.S)
+    protos = {}
+    for name, args in re.findall(r'\b\w+\**\s+\**(rsp_\w+)\(([^)]*)\);', src):
+        types = []
+        for a in args.split(','):
+            a = a.strip()
+            if not a or a == 'void':
+                continue
+            types.append(re.sub(r'\s*\b\w+$', '', a.replace('const ', '')).replace(' ', ''))
+        protos[name] = types
+    return protos
+
+
+# C type -> the class a MATLAB value for it must have ('numeric' literals are converted by MATLAB)
+_PTR_CLASS = {'double*': 'doublePtr', 'float*': 'singlePtr', 'int32_t*': 'int32Ptr', 'void*': 'doublePtr'}
+_SCALAR = {'double': ('double', 'numeric'), 'int32_t': ('int32',), 'uint64_t': ('uint64',)}
+
+
+def _matlab_sources():
+    srcs = [(f, open(os.path.join(MATLAB_DIR, f)).read()) for f in sorted(os.listdir(MATLAB_DIR)) if f.endswith('.m')]
+    for i, b in enumerate(re.findall(r'```matlab\n(.*?)```', open(INTEGRATION).read(), re.S)):
+        srcs.append(('INTEGRATION.md block %d' % i, b))
+    return srcs
+
+
+def _split_args(s):
+    """Top-level comma split of a MATLAB argument list."""
+    out, depth, cur = [], 0, ''
+    for ch in s:
+        if ch in '([{':
+            depth += 1
+        elif ch in ')]}':
+            depth -= 1
+        if ch == ',' and depth == 0:
+            out.append(cur.strip())
+            cur = ''
+        else:
+            cur += ch
+    if cur.strip():
+        out.append(cur.strip())
+    return out
+
+
+def _call_args(src, fn):
+    """Argument lists of every call fn(...) in src (MATLAB ... continuations joined)."""
+    src = re.sub(r'\.\.\.\s*\n\s*', ' ', src)
+    calls = []
+    for m in re.finditer(r'\b%s\(' % fn, src):
+        depth, i = 1, m.end()
+        while depth:
+            depth += {'(': 1, ')': -1}.get(src[i], 0)
+            i += 1
+        calls.append(_split_args(src[m.end():i - 1]))
+    return calls
+
+
+def _value_class(v, ptrs):
+    v = v.strip()
+    if v in ptrs:
+        return ptrs[v]
+    m = re.match(r'(int32|uint64|double|single)\(', v)
+    if m:
+        return m.group(1)
+    if re.fullmatch(r'[A-Za-z_]\w*', v):
+        return 'unknown'   # a variable this source does not define
+    return 'numeric'
+
+
+def test_matlab_calllib_types_match_the_header():
+    """Every libstruct in the committed MATLAB wrappers and INTEGRATION.md sets exactly the fields of
+    its C struct (none missing, e.g. rsp_music_config.precision), each with a value of the field's
+    C type (pointer fields: a libpointer of the matching class), and every calllib passes as many
+    arguments as the prototype has, with libpointers of the matching class for pointer arguments."""
+    structs, protos = _c_structs(), _c_prototypes()
+    assert structs['rsp_music_config']['precision'] == 'int32_t'
+    assert structs['rsp_music_out']['spectrum_db'] == 'double*'
+    checked = 0
+    for where, src in _matlab_sources():
+        code = re.sub(r'%.*', '', src)
+        partial = re.search(r'%\s*\.\.\.', src) is not None   # a documented fragment ('% ... likewise')
+        ptrs = {}
+        for var, cls in re.findall(r'(\w+)\s*=\s*libpointer\(\'(\w+)\'', code):
+            ptrs[var] = cls
+        for var, sname in re.findall(r'(\w+)\s*=\s*libstruct\(\'(\w+)\'', code):
+            ptrs[var] = sname
+        for args in _call_args(code, 'libstruct'):
+            sname = args[0].strip("'")
+            assert sname in structs, (where, sname)
+            full = [a for a in args[1:] if a.startswith('struct(')]
+            if not full:
+                continue
+            kv = _split_args(full[0][len('struct('):-1])
+            given = {kv[i].strip("'"): kv[i + 1] for i in range(0, len(kv), 2)}
+            cfields = structs[sname]
+            assert set(given) <= set(cfields), (where, sname, set(given) - set(cfields))
+            if not partial:
+                assert set(given) == set(cfields), (where, sname, 'missing', set(cfields) - set(given))
+            for f, v in given.items():
+                ct, cls = cfields[f], _value_class(v, ptrs)
+                if cls == 'unknown':   # e.g. numel(...) arguments: only pointer fields need a variable
+                    assert not ct.endswith('*'), (where, sname, f, v)
+                    continue
+                if ct.endswith('*'):
+                    assert cls == _PTR_CLASS[ct], (where, sname, f, ct, v)
+                else:
+                    assert cls in _SCALAR[ct], (where, sname, f, ct, v)
+                checked += 1
+        for args in _call_args(code, 'calllib'):
+            fn = args[1].strip("'")
+            assert fn in protos, (where, fn)
+            cargs = args[2:]
+            assert len(cargs) == len(protos[fn]), (where, fn, cargs, protos[fn])
+            for v, ct in zip(cargs, protos[fn]):
+                cls = _value_class(v, ptrs)
+                assert cls != 'unknown' or partial, (where, fn, v)
+                if cls == 'unknown':
+                    continue
+                opaque = ct.endswith('*') and ct.rstrip('*') not in structs and ct.rstrip('*') + '*' not in _PTR_CLASS
+                if ct.endswith('**') or (opaque and ct != 'char*'):
+                    # opaque handles (rsp_plan*, rsp_music_plan*) are voidPtr; a ** output receives the
+                    # address of a voidPtr libpointer (MATLAB passes its address for a PtrPtr argument)
+                    assert cls == 'voidPtr', (where, fn, v, ct)
+                elif ct.rstrip('*') in structs:
+                    assert cls == ct.rstrip('*'), (where, fn, v, ct)
+                elif ct.endswith('*') and ct != 'char*':
+                    assert cls == _PTR_CLASS[ct] or (ct == 'void*' and cls == 'voidPtr'), (where, fn, v, ct)
+                elif ct in _SCALAR:
+                    assert cls in _SCALAR[ct], (where, fn, v, ct)
+                checked += 1
+    assert checked >= 30

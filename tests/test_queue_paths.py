@@ -111,3 +111,47 @@ def test_results_rows_equal_results():
         plan.device_free(d)
         plan.device_free(e)
         plan.close()
+
+
+@pytest.mark.parametrize('prec', ['c128', 'c64'])
+def test_queue_rdm_equals_sync_rdm(prec):
+    """rsp_enqueue_device_rdm: the queue writes each requested frame's complex RD map (rdm_13beam,
+    fsf:131-136) into the caller's device buffer.  It must equal the synchronous rsp_process_cube
+    map of the same cube exactly, frames that request no map must leave their buffers untouched,
+    and the final targets must be the queue's without maps."""
+    s = scenario('x2')
+    t = targets_for('x2')
+    plan = Plan(s['cfg'], s['cfar'], s['clus'], s['pre_p'], frames_per_launch=2, precision=prec)
+    sz = plan.sizes
+    esz = np.dtype(plan.cdtype).itemsize
+    cubes = [plan.device_alloc(plan.cube_bytes) for _ in range(2)]
+    maps = [plan.device_alloc(sz.rdm_elems * esz) for _ in range(3)]
+    try:
+        for i, c in enumerate(cubes):
+            plan.synthesize_device(c, t, frame_idx=i + 1)
+            t = C.evolve_targets(t, s['cfg'])
+        sentinel = np.full(sz.rdm_elems, 7.0 + 3.0j, plan.cdtype)
+        plan.device_upload(maps[2], sentinel)
+        plan.sync()
+        seq = [0, 1, 0, 1, 0]
+        plan.enqueue_many([cubes[k] for k in seq], range(30, 35))
+        plan.drain()
+        ref = plan.results()
+        # frames 30 and 31 with maps, then three without (map 2 must stay the sentinel)
+        plan.enqueue_many([cubes[0], cubes[1]], [30, 31], rdms=[maps[0], maps[1]])
+        plan.enqueue_many([cubes[k] for k in seq[2:]], range(32, 35))
+        plan.drain()
+        got = plan.results()
+        _same(got, ref)
+        for k in range(2):
+            host = plan.device_download(cubes[k], plan.cube_bytes // esz, plan.cdtype)
+            host = host.reshape(plan.P, plan.N, sz.C, order='F')
+            want = plan.process_cube(host, frame_idx=30 + k, want_rdm=True)['rdm']
+            q = plan.rdm_from_device(maps[k])
+            assert q.shape == want.shape
+            np.testing.assert_array_equal(q.astype(np.complex128), want)
+        np.testing.assert_array_equal(plan.device_download(maps[2], sz.rdm_elems, plan.cdtype), sentinel)
+    finally:
+        for p in cubes + maps:
+            plan.device_free(p)
+        plan.close()

@@ -29,3 +29,13 @@ def test_stage2_config_keeps_v8_configs():
         for k in ('prtNum', 'point_PRT', 'channel_num', 'beam_num', 'point_prt_segments', 'gap_duration', 'tao'):
             assert out['Sig_Config'][k] == cfg['Sig_Config'][k], (name, k)
         assert out['Array'] == cfg['Array']
+
+
+def test_stage2_config_keeps_the_callers_c():
+    """A caller-supplied Sig_Config.c is honoured and the wavelength follows it, as in
+    matlab/process_stage2_mtd.m (s.c = sc.c; s.wavelength = s.c / s.fc)."""
+    cfg = C.debug_v3_config()
+    cfg['Sig_Config']['c'] = 3e8
+    sc = C.stage2_config(cfg)['Sig_Config']
+    assert sc['c'] == 3e8 and sc['wavelength'] == 3e8 / sc['fc']
+    assert C.stage2_config(C.debug_v3_config())['Sig_Config']['c'] == C.C_LIGHT
