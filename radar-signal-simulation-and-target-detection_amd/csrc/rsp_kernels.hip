@@ -65,9 +65,6 @@ __device__ __forceinline__ V vtw(double c, double s) {   // exp(-+ i theta)
 // magnitudes of a radar map; 0 stays 0.
 __device__ __forceinline__ float cmag(f2 x) { return __builtin_amdgcn_sqrtf(x.x * x.x + x.y * x.y); }
 __device__ __forceinline__ double cmag(d2 x) {
-#if defined(RSP_CMAG_EXACT)
-    return __builtin_sqrt(x.x * x.x + x.y * x.y);
-#endif
     const double q = x.x * x.x + x.y * x.y;
     const double r = __builtin_amdgcn_rsq(q);           // v_rsq_f64
     double g = q * r, h = 0.5 * r;
@@ -81,11 +78,19 @@ __device__ __forceinline__ double cmag(d2 x) {
 
 // Raw buffer resources (SRSRC): 32-bit byte offsets and hardware range checking.  An offset at
 // or past num_records reads 0 / drops the store, so masked lanes need no branch or select.
-// The read/write barrier inside an LDS pass (RSP_K2_NOWAR: timing-only builds without it)
-#ifndef RSP_K2_NOWAR
+// The read/write barrier inside an in-place LDS pass (every read of the pass before any write)
 #define RSP_WAR_SYNC() __syncthreads()
-#else
-#define RSP_WAR_SYNC() ((void)0)
+// Synchronisation between the passes of an LDS FFT: the workgroup barrier, or (WL) only a
+// compiler fence when every row of the pass belongs to one wave (rows never shared between
+// waves): a wave's LDS instructions execute in order, so its reads of a pass complete before its
+// writes, and its writes before the next pass's reads.
+template <bool WL>
+__device__ __forceinline__ void pass_sync() {
+    if constexpr (WL) __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    else __syncthreads();
+}
+#ifndef RSP_K2_WLOCAL
+#define RSP_K2_WLOCAL 1   // one-row-per-wave overlap-save blocks sync their passes per wave (-1 % k2_pc)
 #endif
 #define RSP_OOB 0x80000000u   // > any buffer this library makes (plans are validated < 2 GB/frame)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, unsigned bytes) {
@@ -271,7 +276,7 @@ template <bool INV, class V> struct Dft<12, INV, V> {
 constexpr int clog2(int x) { return x <= 1 ? 0 : 1 + clog2(x >> 1); }
 
 // LDS index inside a row: SH > 0 inserts one complex every 2^SH to break power-of-two
-// strides (tools/lds_conflicts.py models the gfx950 bank rules for each pass).
+// strides (tools/ab/lds_conflicts.py models the gfx950 bank rules for each pass).
 template <int SH>
 __device__ __forceinline__ int lidx(int i) { return SH ? i + (i >> SH) : i; }
 
@@ -293,7 +298,7 @@ template <class V> struct StoresLds<StoreLds<V>> { static constexpr bool value =
 // compact columns [i][k] = W^(k 2^i) (lgR loads, twk = table + k, column stride NS), the other
 // powers formed as products of at most lgR - 1 of them.  Column-major so that the lanes of a
 // pass (consecutive k) read consecutive 16-B entries: conflict-free, where [k][i] rows of 4
-// entries put every 4th lane on the same banks (tools/lds_conflicts_k2v2.py).
+// entries put every 4th lane on the same banks (tools/ab/lds_conflicts_k2v2.py).
 template <int R, bool INV, bool CMP, int NS, class V>
 __device__ __forceinline__ void load_tw(const V* twk, V (&w)[R]) {
     if constexpr (!CMP) {
@@ -339,7 +344,7 @@ constexpr int n_passes(int m) {
 // (2048 = 16 x 8 x 16, 1024 = 16 x 4 x 16): a palindrome, so the inverse FFT runs the same
 // radices, and both Ns = 1 passes -- the forward first pass and the inverse first pass fused
 // into the forward last one -- are radix 16, whose stride-16 stores are at most 2-way
-// conflicted (tools/lds_conflicts64.py).  Must match radix_plan() in rsp_plan.cpp.
+// conflicted (tools/ab/lds_conflicts64.py).  Must match radix_plan() in rsp_plan.cpp.
 constexpr int rad_bits_pal(int m, int q) {
     return n_passes(m) == 3 && q >= 1 ? rad_bits(m, 3 - q) : rad_bits(m, q);
 }
@@ -373,7 +378,15 @@ constexpr int tw_total(int LG, bool rev = false, bool cmp = false, bool pal = fa
 // With power-of-two nb, Ns and pads every 2^SH, lidx(j + r nb) = lidx(j) + r nb + ((r nb) >> SH)
 // and lidx(idxD + r Ns) = lidx(idxD) + r Ns + ((r Ns) >> SH): every LDS address of a butterfly
 // is a per-thread base plus a compile-time offset (ds_read/ds_write immediate offsets).
-template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP = false, int XL = 0, class V>
+// WM: row r belongs to wave r (nrows = NTHR / 64): thread (wave w, lane l) takes butterflies
+// l + 64 t of row w, so that a pass's LDS traffic stays inside the wave (WL passes).
+template <int NTHR, int LGNB, bool WM>
+__device__ __forceinline__ int sh_beta(int t) {
+    if constexpr (WM) return ((threadIdx.x >> 6) << LGNB) + (threadIdx.x & 63) + 64 * t;
+    else return threadIdx.x + t * NTHR;
+}
+template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP = false, int XL = 0, bool WM = false,
+          class V>
 __device__ __forceinline__ void sh_load(const V* buf, int rs, int nrows, const V* tw, V (&v)[NB][R]) {
     constexpr int lgR = clog2(R);
     constexpr int lgnb = LGL - lgR;
@@ -383,7 +396,7 @@ __device__ __forceinline__ void sh_load(const V* buf, int rs, int nrows, const V
     const int total = nb * nrows;
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
-        const int beta = threadIdx.x + t * NTHR;
+        const int beta = sh_beta<NTHR, lgnb, WM>(t);
         if (beta < total) {
             const int row = beta >> lgnb, j = beta & (nb - 1);
             const int k = j & (Ns - 1);
@@ -405,7 +418,7 @@ __device__ __forceinline__ void sh_load(const V* buf, int rs, int nrows, const V
 // (Ns = 1 radix-16 passes only).  Their stores write 16 j + r for lane j, which the pad layout
 // puts 2-way on the banks of every group of 8 lanes; swizzled, the 8 lanes hit 8 distinct
 // 16-B banks, and the next pass's reads (j + r nb, nb a multiple of 128) stay conflict-free.
-template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, int XL = 0, class V, class St>
+template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, int XL = 0, bool WM = false, class V, class St>
 __device__ __forceinline__ void sh_store(V (&v)[NB][R], int rs, int nrows, const St& st) {
     constexpr int lgR = clog2(R);
     constexpr int lgnb = LGL - lgR;
@@ -415,7 +428,7 @@ __device__ __forceinline__ void sh_store(V (&v)[NB][R], int rs, int nrows, const
     const int total = nb * nrows;
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
-        const int beta = threadIdx.x + t * NTHR;
+        const int beta = sh_beta<NTHR, lgnb, WM>(t);
         if (beta < total) {
             const int row = beta >> lgnb, j = beta & (nb - 1);
             const int k = j & (Ns - 1);
@@ -436,21 +449,24 @@ __device__ __forceinline__ void sh_store(V (&v)[NB][R], int rs, int nrows, const
 }
 
 // TAIL = false: no barrier after the pass (the caller's next LDS writes go to other rows).
-template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP, int XL = 0, bool TAIL = true, class V,
-          class St>
+template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP, int XL = 0, bool TAIL = true,
+          bool WL = false, class V, class St>
 __device__ __forceinline__ void sh_pass(V* buf, int rs, int nrows, const V* tw, const St& st) {
     V v[NB][R];
-    sh_load<R, INV, NB, SH, NTHR, LGL, LGNS, CMP, XL>(buf, rs, nrows, tw, v);
-    if constexpr (StoresLds<St>::value) RSP_WAR_SYNC();
-    sh_store<R, INV, NB, SH, NTHR, LGL, LGNS>(v, rs, nrows, st);
-    if constexpr (TAIL) __syncthreads();
+    sh_load<R, INV, NB, SH, NTHR, LGL, LGNS, CMP, XL, WL>(buf, rs, nrows, tw, v);
+    if constexpr (StoresLds<St>::value) {
+        if constexpr (WL) pass_sync<true>();
+        else RSP_WAR_SYNC();
+    }
+    sh_store<R, INV, NB, SH, NTHR, LGL, LGNS, 0, WL>(v, rs, nrows, st);
+    if constexpr (TAIL) pass_sync<WL>();
 }
 
 // Passes Q..QEND-1 of a 2^LG-point FFT (radix order reversed if REV) over `nrows` rows;
 // pass n_passes - 1 stores through `last`, the others through `mid`.  tw = this plan's
 // concatenated tables.  PTS = complex points per thread (nrows * L / NTHR).
 template <int LG, int Q, int QEND, int LGNS, int PTS, bool INV, bool REV, int SH, int NTHR, bool CMP, bool PAL = false,
-          int XIN = 0, bool TAIL = true, class V, class StMid, class StLast>
+          int XIN = 0, bool TAIL = true, bool WL = false, class V, class StMid, class StLast>
 __device__ __forceinline__ void fft_range(V* buf, int rs, int nrows, const V* tw, const StMid& mid, const StLast& last) {
     constexpr int NP = n_passes(LG);
     if constexpr (Q < QEND) {
@@ -459,10 +475,11 @@ __device__ __forceinline__ void fft_range(V* buf, int rs, int nrows, const V* tw
         constexpr int NB = (PTS + R - 1) / R;
         const V* twq = tw + tw_pass_off(LG, Q, REV, CMP, PAL);
         if constexpr (Q == NP - 1)
-            sh_pass<R, INV, NB, SH, NTHR, LG, LGNS, CMP, XIN, TAIL>(buf, rs, nrows, twq, last);
+            sh_pass<R, INV, NB, SH, NTHR, LG, LGNS, CMP, XIN, TAIL, WL>(buf, rs, nrows, twq, last);
         else
-            sh_pass<R, INV, NB, SH, NTHR, LG, LGNS, CMP, XIN>(buf, rs, nrows, twq, mid);
-        fft_range<LG, Q + 1, QEND, LGNS + RB, PTS, INV, REV, SH, NTHR, CMP, PAL, 0, TAIL>(buf, rs, nrows, tw, mid, last);
+            sh_pass<R, INV, NB, SH, NTHR, LG, LGNS, CMP, XIN, true, WL>(buf, rs, nrows, twq, mid);
+        fft_range<LG, Q + 1, QEND, LGNS + RB, PTS, INV, REV, SH, NTHR, CMP, PAL, 0, TAIL, WL>(buf, rs, nrows, tw, mid,
+                                                                                             last);
     }
 }
 
@@ -478,23 +495,38 @@ __device__ __forceinline__ void fft_passes(V* buf, int rs, int nrows, const V* t
 // Same formulation as sh_load / sh_store with L, R, Ns compile-time constants that need not be
 // powers of two: divisions by them become multiply-shifts, and every LDS index is padded per
 // element (lidx of the full position).
+// Padded LDS offset of element j + r D of a row when it splits into a per-thread base lidx(j) plus
+// a compile-time offset: always when D is a multiple of the pad period 2^SH ((j + r D) >> SH =
+// (j >> SH) + r D / 2^SH); with DIVP also when D divides 2^SH and the thread's j mod 2^SH < D
+// (shg_store: idxD = (j / NS) NS R + j mod NS with NS R a multiple of 2^SH), where the carry of
+// j mod 2^SH + r D past 2^SH is that of r D alone.
+template <int SH, int D, bool DIVP = false>
+constexpr bool lidx_sep() {
+    return SH == 0 || D % (1 << SH) == 0 || (DIVP && (1 << SH) % D == 0);
+}
+template <int SH, int D>
+constexpr int lidx_off(int r) {
+    return r * D + (SH ? (r * D) >> SH : 0);
+}
+
 template <int R, bool INV, int NB, int SH, int NTHR, int L, int NS, bool CMP, int XL = 0, class V>
 __device__ __forceinline__ void shg_load(const V* buf, int rs, int nrows, const V* tw, V (&v)[NB][R],
                                          int tix = threadIdx.x) {
     constexpr int nb = L / R;
     static_assert(!XL || nb % 128 == 0, "XOR-swizzled input needs r nb to keep the swizzle bits");
+    constexpr bool SEP = lidx_sep<SH, nb>();
     const int total = nb * nrows;
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
         const int beta = tix + t * NTHR;
         if (beta < total) {
             const int row = beta / nb, j = beta - row * nb;
-            const V* src = XL ? buf + row * L + (j ^ ((j >> 4) & 7)) : buf + row * rs;
+            const V* src = XL ? buf + row * L + (j ^ ((j >> 4) & 7)) : buf + row * rs + (SEP ? lidx<SH>(j) : 0);
             V w[R];
             if (NS > 1) load_tw<R, INV, CMP, NS>(tw + (CMP ? j % NS : (j % NS) * tw_row(R, CMP)), w);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                V x = XL ? src[r * nb] : src[lidx<SH>(j + r * nb)];
+                V x = XL ? src[r * nb] : (SEP ? src[lidx_off<SH, nb>(r)] : src[lidx<SH>(j + r * nb)]);
                 if (r > 0 && NS > 1) x = vmul(x, w[r]);
                 v[t][r] = x;
             }
@@ -517,6 +549,10 @@ __device__ __forceinline__ void shg_store(V (&v)[NB][R], int rs, int nrows, cons
                 const int wbase = row * L + idxD, c = j & 7;
 #pragma unroll
                 for (int r = 0; r < R; ++r) st.put(t * R + r, row, idxD + r, wbase + (r & 8) + ((r & 7) ^ c), v[t][r]);
+            } else if constexpr (lidx_sep<SH, NS, (NS * R) % (1 << SH) == 0>()) {
+                const int wbase = row * rs + lidx<SH>(idxD);
+#pragma unroll
+                for (int r = 0; r < R; ++r) st.put(t * R + r, row, idxD + r * NS, wbase + lidx_off<SH, NS>(r), v[t][r]);
             } else {
 #pragma unroll
                 for (int r = 0; r < R; ++r)
@@ -563,9 +599,6 @@ __device__ __forceinline__ size_t zaddr(const Geometry& g, int b, int v, int np)
 // K1: DBF + MTD window + slow-time FFT + fftshift -> compacted rows
 // ======================================================================================
 #define K1_THREADS 512
-#ifndef RSP_K1_ABLATE
-#define RSP_K1_ABLATE 0   // timing ablations (A/B builds only): 1 = no FFT, 2 = no DBF MFMA, 4 = no z stores
-#endif
 #define K1_SH 4   // LDS pad shift of the slow-time FFT rows (row stride P + P/16)
 
 // DBF (fsf:93-97) on the matrix cores as a real GEMM: D[16 rows x 16 pulses] += A[16 x 4
@@ -632,9 +665,6 @@ struct StoreZ {
         const int b = row >> lgNT, nl = row & ((1 << lgNT) - 1);
         const int v = (o + half) & (P - 1);
         const int np = (tile << lgNT) + nl;   // compacted sample
-#if RSP_K1_ABLATE & 4   // timing ablation only: no z stores
-        if (x.x == (scal<V>)1234.5678)
-#endif
         buf_st<RSP_Z_AUX>(z, (unsigned)(((((b * nzc + (np >> lgNZ)) * P + v) << lgNZ) + (np & ((1 << lgNZ) - 1)))) * (unsigned)sizeof(V), x);
     }
 };
@@ -973,17 +1003,10 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
 #pragma unroll
                 for (int a = 0; a < D::NACC; ++a) acc[mb][a] = typename D::Acc{};
             if (vld[u]) {   // samples past the used ones: zero columns, like k1_dbf_mtd's n = -1
-#if RSP_K1_ABLATE & 2   // timing ablation only: no DBF arithmetic (the loads still feed the store)
-#pragma unroll
-                for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-                    for (int j = 0; j < NJ; ++j) acc[mb][0][j & 3] += xv[u][j][0];
-#else
 #pragma unroll
                 for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
                     for (int j = 0; j < NJ; ++j) D::mma(acc[mb], are[mb][j], aim[mb][j], xv[u][j]);
-#endif
             }
             dbf_store<T, MB>(Yf, acc, grp, B, NT, Ppad, nlv[u], pv[u], wv_[u], K1_SH);
         }
@@ -1000,13 +1023,6 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
         if (tile == 0 && threadIdx.x == 0 && fp.count[f]) *fp.count[f] = 0;   // K3's detection counter
         V* __restrict__ z = static_cast<V*>(fp.z[f]);
         const StoreZ<V> sz{buf_rsrc(z, (unsigned)(B * g.nzc * P * g.NZ * sizeof(V))), lgNT, g.nzc, tile, P, half, ilog2(g.NZ)};
-#if RSP_K1_ABLATE & 1   // timing ablation only: no FFT, the tile goes to z as is
-        for (int e = threadIdx.x; e < B * NT * P; e += K1_THREADS) {
-            const int row = e >> LGP, o = e & (P - 1);
-            sz.put(0, row, o, 0, (Y + cur * bufsz)[row * Ppad + o + (o >> K1_SH)]);
-        }
-        __syncthreads();
-#else
         // P <= 128: in place, one barrier (between its passes); P = 256 (x4): the Stockham passes
         // (the in-place pass A's 16 twiddles spill there, +7 % K1).  No barrier after the last
         // pass: its reads of buffer cur are ordered before the next writes of cur (the next
@@ -1016,7 +1032,6 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
         else
             fft_passes<LGP, k1p_pts<T>(), K1_SH, K1_THREADS, false>(Y + cur * bufsz, Ppad, B * NT, twl,
                                                                      StoreLds<V>{Y + cur * bufsz}, sz);
-#endif
         if (Tn < total) dbf(Y + (cur ^ 1) * bufsz);
         __syncthreads();
         cur ^= 1;
@@ -1059,6 +1074,34 @@ struct StoreRdmW {
         buf_st1(mr, (unsigned)o * (unsigned)sizeof(S) - (unsigned)Lh1 * (unsigned)sizeof(S), cmag(x));
     }
 };
+// The same for a pass whose output rows are uniform per wave (or per workgroup): the row's
+// resources are built once, before the pass, by the caller; RDM (compile-time) says whether the
+// complex map is stored.  The pass is the overlap-save block's last inverse pass with nb = NS
+// butterflies per row: thread j's output r is o = j + r NS, so the outputs r < rskip =
+// floor(Lh1 / NS) lie below Lh1 -- discarded overlap-save outputs -- for every thread, and their
+// |x| and stores are skipped (a uniform branch; only checked for r < R / 2, where they can be).
+template <class V, bool RDM, int NS, int R>
+struct StoreRowK {
+    typedef scal<V> S;
+    __amdgpu_buffer_rsrc_t rr, mr;
+    unsigned lh1v, lh1s;   // Lh1 in bytes of V / of S
+    int rskip;
+    __device__ __forceinline__ StoreRowK(V* rdm, S* mag, int G, int Gp, int rho, int rows_total, int Lh1, int g0,
+                                         int gend) {
+        const unsigned n = rho < rows_total ? (unsigned)(gend - g0) : 0u;
+        if (RDM) rr = buf_rsrc(rdm + (size_t)rho * G + g0, n * (unsigned)sizeof(V));
+        mr = buf_rsrc(mag + (size_t)rho * Gp + g0, n * (unsigned)sizeof(S));
+        lh1v = (unsigned)Lh1 * (unsigned)sizeof(V);
+        lh1s = (unsigned)Lh1 * (unsigned)sizeof(S);
+        rskip = Lh1 / NS;
+    }
+    __device__ __forceinline__ void put(int idx, int, int o, int, V x) const {
+        const int r = idx % R;
+        if (r < R / 2 && r < rskip) return;
+        if (RDM) buf_st<RSP_RDM_AUX>(rr, (unsigned)o * (unsigned)sizeof(V) - lh1v, x);
+        buf_st1(mr, (unsigned)o * (unsigned)sizeof(S) - lh1s, cmag(x));
+    }
+};
 
 // Samples [lo, hi] of row (b, v) of one segment as one buffer window: z's element index is
 // increasing in the compacted sample n' (tile-major, slot-minor), so a resource based at
@@ -1075,9 +1118,6 @@ template <class V>
 __device__ __forceinline__ ZWin zrow_window(const Geometry& g, const V* z, int rho, int rows_total, int off, int lo,
                                             int hi) {
     ZWin w;
-#ifdef RSP_K2_HOTZ   // timing-only builds: every row reads row (rho mod 16)'s samples (cache-resident)
-    rho = rho & 15;
-#endif
     const int b = rho / g.P, v = rho - b * g.P;
     w.lgNT = ilog2(g.NZ);
     w.NT1 = g.NZ - 1;
@@ -1093,7 +1133,7 @@ __device__ __forceinline__ ZWin zrow_window(const Geometry& g, const V* z, int r
 // LDS pad of the overlap-save rows: one complex per 32.  For 16-B elements this keeps every
 // ds_read_b128 of a pass conflict-free (a pad per 16 would shift lanes 20-27 of a lane group
 // onto lane 12's bank), and the stride-16 stores of the two radix-16 Ns = 1 passes 2-way
-// (tools/lds_conflicts64.py)
+// (tools/ab/lds_conflicts64.py)
 template <class T> constexpr int k2_sh() { return sizeof(T) == 4 ? 5 : RSP_K2_SH64; }
 #define K2_LDS_DATA(SH) (RSP_K2_POINTS + (RSP_K2_POINTS >> (SH)))
 
@@ -1152,6 +1192,8 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     // one row per wave (nb0 a multiple of 64, one butterfly per thread): the row's sample window
     // is a scalar buffer resource, and a load's offset needs no mask
     constexpr bool WROW = nb0 >= 64 && NB0 == 1;
+    // RSP_K2_WLOCAL: one row per wave in every pass too (rows == 4), so passes sync the wave only
+    constexpr bool WLc = RSP_K2_WLOCAL && WROW && rows == K2_THREADS / 64;
     if constexpr (WROW) {
         const int rl = __builtin_amdgcn_readfirstlane(tid / nb0);
         // waves past the block's rows (fewer rows than 256 / nb0) load nothing
@@ -1217,31 +1259,44 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     sh_store<R0, false, NB0, SH, K2_THREADS, LGM, 0, XZ>(v0, rs, rows, StoreLds<V>{L});
     __syncthreads();
     // forward passes 1 .. NP-2
-    fft_range<LGM, 1, NP - 1, RB0, 16, false, false, SH, K2_THREADS, CMP, PAL, XZ>(L, rs, rows, twF, StoreLds<V>{L},
-                                                                               StoreLds<V>{L});
+    fft_range<LGM, 1, NP - 1, RB0, 16, false, false, SH, K2_THREADS, CMP, PAL, XZ, true, WLc>(L, rs, rows, twF,
+                                                                                          StoreLds<V>{L}, StoreLds<V>{L});
     // fused: forward last pass, x H (1/M folded in), inverse pass 0 of the reversed plan
     {
         V v[NBL][RL];
-        sh_load<RL, false, NBL, SH, K2_THREADS, LGM, LGM - RBL, CMP>(L, rs, rows,
-                                                                      twF + tw_pass_off(LGM, NP - 1, false, CMP, PAL), v);
-        RSP_WAR_SYNC();
+        sh_load<RL, false, NBL, SH, K2_THREADS, LGM, LGM - RBL, CMP, 0, WLc>(
+            L, rs, rows, twF + tw_pass_off(LGM, NP - 1, false, CMP, PAL), v);
+        if constexpr (WLc) pass_sync<true>();
+        else RSP_WAR_SYNC();
 #pragma unroll
         for (int t = 0; t < NBL; ++t) {
             Dft<RL, false, V>::run(v[t]);
 #pragma unroll
             for (int r = 0; r < RL; ++r) v[t][r] = vmul(v[t][r], hreg[(t % NHT) * RL + r]);
         }
-        sh_store<RL, true, NBL, SH, K2_THREADS, LGM, 0, XZ>(v, rs, rows, StoreLds<V>{L});
-        __syncthreads();
+        sh_store<RL, true, NBL, SH, K2_THREADS, LGM, 0, XZ, WLc>(v, rs, rows, StoreLds<V>{L});
+        pass_sync<WLc>();
     }
     // inverse passes 1 .. NP-1 (reversed radices); the last keeps the valid overlap-save
     // outputs = stitched gates
     const int gend = min(sd.gb, g0 + sd.V);
     // the inverse FFT's last pass runs the forward pass 0's radix (R0) over nb0 butterflies
-    if constexpr (WROW)
-        fft_range<LGM, 1, NP, RBL, 16, true, true, SH, K2_THREADS, CMP, PAL, XZ, false>(
-            L, rs, rows, twI, StoreLds<V>{L}, StoreRdmW<V>{rdm, mag, G, g.Gp, row0, rows_total, Lh1, g0, gend});
-    else
+    if constexpr (WROW) {
+        // inverse passes 1 .. NP-2 into LDS, then the last one (Ns = nb0, input not swizzled:
+        // XZ applies to the pass after an Ns = 1 pass only) into this wave's row of the maps
+        fft_range<LGM, 1, NP - 1, RBL, 16, true, true, SH, K2_THREADS, CMP, PAL, XZ, true, WLc>(
+            L, rs, rows, twI, StoreLds<V>{L}, StoreLds<V>{L});
+        constexpr int LGNSL = LGM - RB0;
+        static_assert(NP >= 3 || XZ == 0, "last pass input is never swizzled");
+        const V* twl_last = twI + tw_pass_off(LGM, NP - 1, true, CMP, PAL);
+        const int rho = row0 + __builtin_amdgcn_readfirstlane(tid / nb0);
+        if (rdm)
+            sh_pass<R0, true, NB0, SH, K2_THREADS, LGM, LGNSL, CMP, 0, false, WLc>(
+                L, rs, rows, twl_last, StoreRowK<V, true, nb0, R0>(rdm, mag, G, g.Gp, rho, rows_total, Lh1, g0, gend));
+        else
+            sh_pass<R0, true, NB0, SH, K2_THREADS, LGM, LGNSL, CMP, 0, false, WLc>(
+                L, rs, rows, twl_last, StoreRowK<V, false, nb0, R0>(rdm, mag, G, g.Gp, rho, rows_total, Lh1, g0, gend));
+    } else
         fft_range<LGM, 1, NP, RBL, 16, true, true, SH, K2_THREADS, CMP, PAL, XZ, false>(
             L, rs, rows, twI, StoreLds<V>{L},
             StoreRdm<V>{buf_rsrc(rdm, (unsigned)(rows_total * G * sizeof(V))),
@@ -1329,10 +1384,15 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
     shg_pass<R1, true, NB1, SH, K2_THREADS, M, NS1, CMP, XZ>(L, rs, rows, twI, StoreLds<V>{L});
     const int gend = min(sd.gb, g0 + sd.V);
     {
+        static_assert(NS2 == nb0, "last pass: thread j's outputs are j + r NS2");
         V v[NB0][R0];
         shg_load<R0, true, NB0, SH, K2_THREADS, M, NS2, CMP>(L, rs, rows, twI + TW2, v, tid);
-        shg_store<R0, true, NB0, SH, K2_THREADS, M, NS2>(
-            v, rs, rows, StoreRdmW<V>{rdm, mag, G, g.Gp, row0, rows_total, Lh1, g0, gend}, tid);
+        if (rdm)
+            shg_store<R0, true, NB0, SH, K2_THREADS, M, NS2>(
+                v, rs, rows, StoreRowK<V, true, NS2, R0>(rdm, mag, G, g.Gp, row0, rows_total, Lh1, g0, gend), tid);
+        else
+            shg_store<R0, true, NB0, SH, K2_THREADS, M, NS2>(
+                v, rs, rows, StoreRowK<V, false, NS2, R0>(rdm, mag, G, g.Gp, row0, rows_total, Lh1, g0, gend), tid);
     }
 }
 
@@ -1358,16 +1418,6 @@ __global__ __launch_bounds__(K2_THREADS, RSP_K2_MINB) void k2_pc(Geometry g, Dev
     const int lo = sd.lo, hi = sd.hi, off = sd.off;
     const int tid = threadIdx.x;
 
-#ifdef RSP_K2_ONLY   // timing-only builds: 1 = narrow FIR jobs only, 2 = power-of-two blocks only, 3 = 2560 blocks only
-    {
-        const int jt = sd.type != 1 ? 1 : (sd.logM == 0 ? 3 : 2);
-        if (jt != RSP_K2_ONLY) return;
-    }
-#endif
-#ifdef RSP_K2_CENSUS   // instruction-census builds (-S only): one job type per kernel
-    if (RSP_K2_CENSUS == 1) { k2_fft_job_mix<T, 2560, 10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); return; }
-    if (RSP_K2_CENSUS == 2) { k2_fft_job<T, 10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); return; }
-#endif
     if (sd.type == 1 && sd.logM == 0) {   // mixed-radix block
         k2_fft_job_mix<T, 2560, 10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L);
     } else if (sd.type == 1) {
@@ -1564,9 +1614,6 @@ __device__ __forceinline__ void s9_estimate(const S9Consts& k, SF sval, int P, i
 
 #define K3_QCAP 1024
 
-#ifndef RSP_K3_ABLATE
-#define RSP_K3_ABLATE 0   // timing ablations (A/B builds only): 1 = no CFAR, 2 = no map loads
-#endif
 #ifndef K3_VEC
 #define K3_VEC 8   // 16-B loads per beam per thread in flight (halo-less 98-row tiles: 8 -> 120 rows per sweep; 12 measured 43.7 vs 36.8 us)
 #endif
@@ -1665,7 +1712,7 @@ __global__ __launch_bounds__(RSP_THREADS, RSP_K3_WGS) void k3_cfar(Geometry g, D
             for (int q = 0; q < K3_VEC; ++q) {
                 xa[q] = U{};
                 xb[q] = xa[q];
-                if (colok && vb + rr + q * NTR < nv && !(RSP_K3_ABLATE & 2)) {
+                if (colok && vb + rr + q * NTR < nv) {
                     xa[q] = *reinterpret_cast<const U*>(pa + (size_t)(vb + q * NTR) * Gp);
                     xb[q] = *reinterpret_cast<const U*>(pb + (size_t)(vb + q * NTR) * Gp);
 #pragma unroll
@@ -1715,7 +1762,7 @@ __global__ __launch_bounds__(RSP_THREADS, RSP_K3_WGS) void k3_cfar(Geometry g, D
             sm[(size_t)v * G + r] = NOH ? sg(v, r) : Sv[v * W + (r - c0)];
         }
     }
-    if (v1 <= v0 || cut_hi <= cut_lo || (RSP_K3_ABLATE & 1)) return;
+    if (v1 <= v0 || cut_hi <= cut_lo) return;
     const double Tc = g.T;
     // mean() = sum / n over the slices of fsf:197-203 (max(a/n, b/n) = max(a, b)/n).  double: the
     // correctly rounded quotient, as MATLAB, without a division: q0 = x * RN(1/n), r = x - q0 n
@@ -2119,9 +2166,6 @@ static int k1p_tpw(const Geometry& g) {
 }
 
 bool k1_persistent_fits(const Geometry& g) {
-#ifdef RSP_AB_K1_TILED   // timing-only builds: the tiled K1 everywhere
-    return false;
-#endif
     const int pts = g.prec == RSP_PREC_F64 ? 8 : 16;   // FFT points per thread (k1p_pts)
     return g.pow2P && g.logP >= 6 && g.logP <= 8 && k1p_tpw(g) > 0 && k1p_lds(g) <= 160 * 1024 &&
            g.B * g.NT * g.P <= pts * K1_THREADS && g.ncu > 0 && !g.k1_tiled;
@@ -2133,10 +2177,7 @@ static hipError_t launch_k1_t(const Geometry& g, const DevConsts& k, const Frame
     if (mode == 3 && k1_persistent_fits(g)) {
         // one FFT size per instantiation keeps the prefetch registers + FFT under 256 VGPRs
         const size_t ldsp = k1p_lds(g);
-#ifndef RSP_AB_K1P_GRID4   // timing-only builds: the persistent grid on GRID4/4 of the CUs
-#define RSP_AB_K1P_GRID4 4
-#endif
-        const int grid = std::min(g.ncu * RSP_AB_K1P_GRID4 / 4, nf * g.ntiles);
+        const int grid = std::min(g.ncu, nf * g.ntiles);
         constexpr int NJ = CP / 4, MB = BMAX <= 8 ? 1 : 2, TPW = (16 / NJ) / MB > 0 ? (16 / NJ) / MB : 1;
         const bool twice = k1p_tpw(g) == 2 * TPW;
 #define K1P_LAUNCH(LGP, TW)                                                                                      \

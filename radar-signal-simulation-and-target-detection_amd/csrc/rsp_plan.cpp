@@ -494,9 +494,6 @@ FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const void* const* in, int
 #ifndef RSP_K3_RT_C128
 #define RSP_K3_RT_C128 32   // K3 tile width in range cells, complex double (32 or 64)
 #endif
-#ifndef RSP_K12_SUB
-#define RSP_K12_SUB 0
-#endif
 int launch_batch(rsp_plan* p, Lane& L, const void* const* in, const int* ids, int nf, void* smap = nullptr,
                  const int* slots = nullptr, void* const* rdm = nullptr) {
     FramePtrs fp = lane_ptrs(p, L, in, nf, rdm);
@@ -506,26 +503,6 @@ int launch_batch(rsp_plan* p, Lane& L, const void* const* in, const int* ids, in
             if (slots[f] >= 0) HIPCHK(hipStreamWaitEvent(L.stream, p->slot_ready[slots[f]], 0));
     L.timed = p->time_stages;
     if (L.timed) HIPCHK(hipEventRecord(L.tev[0], L.stream));
-#if RSP_K12_SUB > 0
-    // K1 + K2 in sub-batches of RSP_K12_SUB frames that reuse the first z slots (A/B option): the
-    // z of a sub-batch is consumed by K2 while it is still in the Infinity Cache and overwritten
-    // by the next sub-batch
-    for (int s0 = 0; s0 < nf; s0 += RSP_K12_SUB) {
-        const int ns = std::min(RSP_K12_SUB, nf - s0);
-        FramePtrs fs = fp;
-        for (int f = 0; f < ns; ++f) {
-            fs.in[f] = fp.in[s0 + f]; fs.z[f] = fp.z[f]; fs.rdm[f] = fp.rdm[s0 + f]; fs.mag[f] = fp.mag[s0 + f];
-            fs.dets[f] = fp.dets[s0 + f]; fs.count[f] = fp.count[s0 + f];
-        }
-        HIPCHK(launch_k1(p->g, p->k, fs, ns, 3, L.stream));
-        HIPCHK(launch_k2(p->g, p->k, fs, ns, p->g.B * p->g.P, L.stream));
-    }
-    if (slots)
-        for (int f = 0; f < nf; ++f)
-            if (slots[f] >= 0) HIPCHK(hipEventRecord(p->slot_free[slots[f]], L.stream));
-    if (L.timed) HIPCHK(hipEventRecord(L.tev[1], L.stream));
-    if (L.timed) HIPCHK(hipEventRecord(L.tev[2], L.stream));
-#else
     HIPCHK(launch_k1(p->g, p->k, fp, nf, 3, L.stream));
     if (slots)   // K1 has read the cubes: their slots may be written again
         for (int f = 0; f < nf; ++f)
@@ -533,7 +510,6 @@ int launch_batch(rsp_plan* p, Lane& L, const void* const* in, const int* ids, in
     if (L.timed) HIPCHK(hipEventRecord(L.tev[1], L.stream));
     HIPCHK(launch_k2(p->g, p->k, fp, nf, p->g.B * p->g.P, L.stream));
     if (L.timed) HIPCHK(hipEventRecord(L.tev[2], L.stream));
-#endif
     Geometry g3 = p->g;
     g3.max_dets = L.dcap;
     HIPCHK(launch_k3(g3, p->k, fp, nf, L.stream));

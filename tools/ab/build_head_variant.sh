@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build exp/ab/librsp_<name>.so from the kernels/plan sources of git revision REV (default HEAD),
 # against the current headers and host objects: the "before" side of an A/B (tools/ab.sh).
-# usage: tools/build_head_variant.sh NAME [REV]
+# usage: tools/ab/build_head_variant.sh NAME [REV]
 set -e
 name=$1; rev=${2:-HEAD}
 C=radar-signal-simulation-and-target-detection_amd/csrc

@@ -2,4 +2,4 @@ set -o pipefail
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_amplitude_kat.py tests/test_queue_paths.py -x -q -m gpu --timeout 200 --timeout-method thread > gpurun_out/t1.log 2>&1 || { tail -30 gpurun_out/t1.log; exit 1; }
 tail -2 gpurun_out/t1.log
-bash tools/ab.sh x2 c128 prev && bash tools/ab.sh x4 c128 prev
+bash tools/ab/ab.sh x2 c128 prev && bash tools/ab/ab.sh x4 c128 prev

@@ -6,4 +6,4 @@ tail -3 gpurun_out/t1.log
 AB_LIB=exp/ab/librsp_dbg.so RSP_MUSIC_TRACE=1 timeout -k 10 120 python3 tools/music_prof.py 1024 5 c128 > gpurun_out/mtr.log 2>&1 || exit 1
 timeout -k 10 120 python3 tools/music_prof.py 1024 5 c128 >> gpurun_out/mtr.log 2>&1 || exit 1
 cat gpurun_out/mtr.log
-bash tools/ab.sh x2 c128 old
+bash tools/ab/ab.sh x2 c128 old

@@ -1,5 +1,5 @@
 """Bank-conflict model of the K2 overlap-save passes (k2_block, radix plans k2_rad in
-rsp_internal.h) for complex-double elements, gfx950 rules as tools/lds_conflicts64.py.
+rsp_internal.h) for complex-double elements, gfx950 rules as tools/ab/lds_conflicts64.py.
 usage: lds_conflicts_k2.py [SH ...]   (prints read / write cost factors per pass; 1.0 = conflict-free)
 """
 import sys

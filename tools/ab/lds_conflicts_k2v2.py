@@ -1,6 +1,6 @@
 """Bank-conflict model of the CURRENT K2 overlap-save passes in complex double (k2_fft_job with
 its palindromic power-of-two plans, k2_fft_job_mix for 2560 = 16 x 10 x 16), gfx950 rules of
-tools/lds_conflicts64.py.  Addresses are generated exactly as sh_load/sh_store (power-of-two)
+tools/ab/lds_conflicts64.py.  Addresses are generated exactly as sh_load/sh_store (power-of-two)
 and shg_load/shg_store (mixed radix) in rsp_kernels.hip compute them.
 usage: lds_conflicts_k2v2.py [SH [rows]]      (prints per pass: reads / writes / twiddle-read cost factor,
 1.0 = conflict-free, and the LDS cycles per row weighted by instruction count)"""

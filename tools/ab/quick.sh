@@ -1,6 +1,6 @@
 #!/bin/bash
 # Fast GPU iteration: parity subset (-k expression) + per-stage HIP-event times of x2 (both precisions).
-# usage: tools/quick.sh [pytest -k expr]
+# usage: tools/ab/quick.sh [pytest -k expr]
 set -o pipefail
 mkdir -p gpurun_out
 k=${1:-"x2 or small"}

@@ -9,7 +9,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'radar-signal-simulation-and-target-detection_amd'))
-if os.environ.get('AB_LIB'):   # timing experiments only (tools/ab.sh): an A/B variant of librsp.so
+if os.environ.get('AB_LIB'):   # timing experiments only (tools/ab/ab.sh): an A/B variant of librsp.so
     from rsp import _abi  # noqa: E402
     _abi.LIB_PATH = os.environ['AB_LIB']
 
