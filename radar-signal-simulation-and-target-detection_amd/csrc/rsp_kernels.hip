@@ -86,11 +86,18 @@ __device__ __forceinline__ double cmag(d2 x) {
 // writes, and its writes before the next pass's reads.
 template <bool WL>
 __device__ __forceinline__ void pass_sync() {
+#if RSP_K2_WLBAR
+    __syncthreads();
+#else
     if constexpr (WL) __atomic_signal_fence(__ATOMIC_SEQ_CST);
     else __syncthreads();
+#endif
 }
 #ifndef RSP_K2_WLOCAL
-#define RSP_K2_WLOCAL 1   // one-row-per-wave overlap-save blocks sync their passes per wave (-1 % k2_pc)
+#define RSP_K2_WLOCAL 0
+#endif
+#ifndef RSP_K2_WLBAR
+#define RSP_K2_WLBAR 0
 #endif
 #define RSP_OOB 0x80000000u   // > any buffer this library makes (plans are validated < 2 GB/frame)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, unsigned bytes) {

@@ -768,6 +768,12 @@ __global__ __launch_bounds__(MU_THREADS, 2) void k_music_cov64(int N, int K, con
 // ---------------------------------------------------------------------------------------
 #define ME_THREADS 256
 #define ME_SECT 23   // multisection rounds: 5^23 > 2^53
+// Floor of the squared off-diagonal entries the Sturm count reads (e2[], not ee[]): an exactly
+// zero minor p_r must act as dstebz's q_r = -pivmin, i.e. a sign change after which
+// p_{r+1} = -e_r^2 p_{r-1} carries on with the opposite sign.  With e_r^2 = 0 (a decoupled row or
+// the pad rows) p_{r+1} would be 0 again and flip once more; at e_r^2 >= 2^-600 it is not, and the
+// eigenvalues move by at most ~2^-300.
+#define ME_E2MIN 0x1p-600
 #ifndef ME_WPS
 #define ME_WPS 4     // waves per SIMD the register budget is sized for (4 instances per CU)
 #endif
@@ -842,7 +848,7 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
                 taus[k] = tau;
                 dd[k] = dk;
                 ee[k] = beta;
-                e2[k] = beta * beta;
+                e2[k] = fmax(beta * beta, ME_E2MIN);
             }
         }
         __syncthreads();
@@ -924,11 +930,11 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
         // A zero minor counts as a sign change, as q_r = 0 -> -pivmin does there; both minors
         // are rescaled by a power of two every 4 rows (no overflow or underflow).
         // rows n .. n + 3 pad the count to whole blocks of 4: d = ghi + 1 > every x of the
-        // search and e^2 = 0 keep the minors' signs (p_r = (d - x) p_{r-1}, d - x > 0)
+        // search and e^2 = ME_E2MIN keep the minors' signs (p_r ~ (d - x) p_{r-1}, d - x > 0)
         __syncthreads();   // every lane has read dd / e2 (Gershgorin) before the pad rows land
         if (t < 4) {
             dd[n + t] = ghi + 1.0;
-            e2[n - 1 + t] = 0.0;
+            e2[n - 1 + t] = ME_E2MIN;
         }
         __syncthreads();
         auto sturm = [&](double x) -> int {

@@ -188,3 +188,29 @@ def test_music_host_path_equals_device_path(music_case):
     o = c['plan'].process(c['X'][:3])
     assert np.array_equal(o['peaks'], c['out']['peaks'][:3])
     assert np.abs(o['spectrum_db'] - c['out']['spectrum_db'][:3]).max() == 0.0
+
+
+@pytest.mark.gpu
+def test_music_decoupled_covariance_eigenvalues():
+    """A covariance whose tridiagonal form is decoupled (every off-diagonal exactly zero): X with
+    one snapshot per channel gives R = diag(|a_n|^2 / K), and the Householder steps are all the
+    identity.  The multisection Sturm count must then return the diagonal itself, sorted
+    descending (MUSIC_1D.m:29-31), including repeated values; rows with e = 0 are the case where
+    an exactly zero leading minor must not flip the count twice (dstebz's -pivmin rule)."""
+    from rsp.music import MusicPlan
+    N, K, M = 16, 64, 3
+    scan = np.linspace(-np.pi / 2, np.pi / 2, 50)
+    rng = np.random.default_rng(5)
+    mags = np.concatenate([rng.uniform(0.5, 4.0, N - 4), [2.0, 2.0, 1.0, 1.0]])   # repeated eigenvalues
+    X = np.zeros((2, N, K), np.complex128)
+    for i in range(2):
+        ph = np.exp(2j * np.pi * rng.random(N))
+        X[i, np.arange(N), np.arange(N)] = np.sqrt(mags * K) * ph
+    plan = MusicPlan(N, K, M, scan, 0.5, max_batch=2)
+    try:
+        o = plan.process(X)
+    finally:
+        plan.close()
+    want = np.sort(mags)[::-1]
+    for i in range(2):
+        assert np.abs(o['eig'][i] - want).max() <= 1e-12 * want.max(), (o['eig'][i], want)

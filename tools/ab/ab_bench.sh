@@ -7,6 +7,6 @@ mkdir -p gpurun_out
 for round in 1 2 3; do
   for v in base "$@"; do
     if [ $v = base ]; then lib=base; else lib=exp/ab/librsp_$v.so; fi
-    timeout -k 10 200 python3 tools/ab_bench.py $lib $args | sed "s/^/$round /" | tee -a gpurun_out/ab_bench.log || exit $?
+    timeout -k 10 200 python3 tools/ab/ab_bench.py $lib $args | sed "s/^/$round /" | tee -a gpurun_out/ab_bench.log || exit $?
   done
 done
