@@ -367,7 +367,7 @@ constexpr int tw_pass_off(int LG, int q, bool rev = false, bool cmp = false, boo
     int off = 0, lgns = 0;
     for (int i = 0; i < q; ++i) {
         const int rb = rad_bits_p(LG, i, rev, pal);
-        if (i > 0) off += (1 << lgns) * tw_row(1 << rb, cmp);
+        if (i > 0) off += (1 << lgns) * tw_row(1 << rb, rsp_tw_cmp(1 << lgns, 1 << rb, cmp));
         lgns += rb;
     }
     return off;
@@ -409,7 +409,8 @@ __device__ __forceinline__ void sh_load(const V* buf, int rs, int nrows, const V
             const int k = j & (Ns - 1);
             const V* src = XL ? buf + (row << LGL) + (j ^ ((j >> 4) & 7)) : buf + row * rs + lidx<SH>(j);
             V w[R];
-            if (LGNS > 0) load_tw<R, INV, CMP, Ns>(tw + (CMP ? k : k * tw_row(R, CMP)), w);
+            constexpr bool CQ = rsp_tw_cmp(Ns, R, CMP);   // this pass's table form
+            if (LGNS > 0) load_tw<R, INV, CQ, Ns>(tw + (CQ ? k : k * tw_row(R, CQ)), w);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 V x = src[r * nb + (SH && !XL ? (r * nb) >> SH : 0)];
@@ -530,7 +531,8 @@ __device__ __forceinline__ void shg_load(const V* buf, int rs, int nrows, const 
             const int row = beta / nb, j = beta - row * nb;
             const V* src = XL ? buf + row * L + (j ^ ((j >> 4) & 7)) : buf + row * rs + (SEP ? lidx<SH>(j) : 0);
             V w[R];
-            if (NS > 1) load_tw<R, INV, CMP, NS>(tw + (CMP ? j % NS : (j % NS) * tw_row(R, CMP)), w);
+            constexpr bool CQ = rsp_tw_cmp(NS, R, CMP);   // this pass's table form
+            if (NS > 1) load_tw<R, INV, CQ, NS>(tw + (CQ ? j % NS : (j % NS) * tw_row(R, CQ)), w);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 V x = XL ? src[r * nb] : (SEP ? src[lidx_off<SH, nb>(r)] : src[lidx<SH>(j + r * nb)]);
@@ -1159,7 +1161,7 @@ constexpr int k2_tw_lds(int LGM) {
            (k2_tw_sym(LGM) ? 0 : tw_total(LGM, true, RSP_K2_CMP, RSP_K2_PAL));
 }
 constexpr int k2_tw_lds_max() {
-    int m = 16 * tw_row(10, RSP_K2_CMP) + 160 * tw_row(16, RSP_K2_CMP);   // k2_fft_job_mix<2560>
+    int m = 16 * tw_row(10, rsp_tw_cmp(16, 10, RSP_K2_CMP)) + 160 * tw_row(16, rsp_tw_cmp(160, 16, RSP_K2_CMP));   // k2_fft_job_mix<2560>
     for (int lg = 6; lg <= 11; ++lg) m = k2_tw_lds(lg) > m ? k2_tw_lds(lg) : m;
     return m;
 }
@@ -1335,8 +1337,8 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
     constexpr int NB0 = (nb0 * rows + K2_THREADS - 1) / K2_THREADS;
     constexpr int NB1 = ((M / R1) * rows + K2_THREADS - 1) / K2_THREADS;
     constexpr int NS1 = R0, NS2 = R0 * R1;                               // Ns of passes 1 and 2
-    constexpr int TW2 = NS1 * tw_row(R1, CMP);                           // offset of pass 2's table
-    constexpr int NTWF = TW2 + NS2 * tw_row(R0, CMP);
+    constexpr int TW2 = NS1 * tw_row(R1, rsp_tw_cmp(NS1, R1, CMP));      // offset of pass 2's table
+    constexpr int NTWF = TW2 + NS2 * tw_row(R0, rsp_tw_cmp(NS2, R0, CMP));
     const int P = g.P, G = g.G;
     const int lo = sd.lo, hi = sd.hi, off = sd.off;
     const int tid = threadIdx.x;

@@ -101,6 +101,7 @@ void radix_plan(int m, int* nrad, int* rad, bool pal = false) {
 }
 
 void push_pass_twiddles(std::vector<cd>& out, int Ns, int R, bool cmp) {
+    cmp = rsp_tw_cmp(Ns, R, cmp);   // the pass's table form (rsp_internal.h)
     if (cmp) {
         for (int r = 1; r < R; r *= 2)
             for (int k = 0; k < Ns; ++k) out.push_back(root_of_unity((long long)k * r, (long long)Ns * R));

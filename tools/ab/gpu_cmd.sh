@@ -12,6 +12,8 @@ for v in ['wl','wlbar']:
     x=np.load('gpurun_out/rdm_%s.npy'%v); d=np.abs(x-b); print(v, 'maxdiff', d.max(), 'n bad', int((d>0).sum()), 'bad beams/doppler rows', sorted(set(np.argwhere(d>0)[:,2].tolist()))[:10], len(set(map(tuple,np.argwhere(d>0)[:,[0,2]].tolist()))))
 "
 timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_queue_paths.py tests/test_music.py -x -q --timeout 300 --timeout-method thread -k "x2 or small or p256 or rdm or x4 or music" > gpurun_out/par.log 2>&1; rc=$?; tail -3 gpurun_out/par.log; [ $rc -eq 0 ] || exit $rc
+bash tools/ab/ab.sh x2 c128 head || exit 1
+mv gpurun_out/ab.log gpurun_out/ab_x2.log
 bash tools/ab/ab.sh x4 c128 head || exit 1
 mv gpurun_out/ab.log gpurun_out/ab_x4.log
 bash tools/pmc_pass.sh x4 c128 || exit 1
