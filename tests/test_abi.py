@@ -210,3 +210,12 @@ def test_plan_cache_is_keyed_on_content():
     pre['MTD_win'] = np.array(pre['MTD_win'])
     pre['MTD_win'][3] += 1e-12
     assert rsp._fingerprint(s['cfg'], s['cfar'], s['clus'], pre) != a      # array contents count
+
+
+def test_abi_version_agrees_everywhere():
+    """The library, include/rsp.h and the driver's build() check name the same ABI version."""
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hv = int(re.search(r'#define RSP_ABI_VERSION (\d+)', open(os.path.join(root, 'include', 'rsp.h')).read()).group(1))
+    assert _abi.lib().rsp_abi_version() == hv
+    assert 'rsp_abi_version() == %d' % hv in open(os.path.join(root, '__graft_entry__.py')).read()
