@@ -14,7 +14,7 @@ for v in ['wl','wlbar']:
 timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_queue_paths.py tests/test_music.py -x -q --timeout 300 --timeout-method thread -k "x2 or small or p256 or rdm or x4 or music" > gpurun_out/par.log 2>&1; rc=$?; tail -3 gpurun_out/par.log; [ $rc -eq 0 ] || exit $rc
 bash tools/ab/ab.sh x2 c128 head || exit 1
 mv gpurun_out/ab.log gpurun_out/ab_x2.log
-bash tools/ab/ab.sh x4 c128 head || exit 1
+bash tools/ab/ab.sh x4 c128 preunit || exit 1
 mv gpurun_out/ab.log gpurun_out/ab_x4.log
 bash tools/pmc_pass.sh x4 c128 || exit 1
 cat gpurun_out/pmc_x4_c128/pmc_traffic_x4_c128.json
