@@ -22,3 +22,16 @@ timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tl_
 python3 tools/timeline.py gpurun_out/tl_base
 timeout -k 10 300 python3 tools/ab/cusplit.py x2 c128 | tee gpurun_out/cusplit.log
 bash tools/ab/ab_bench.sh "--steps 200" split64 split96 split128 || exit 1
+for v in base mmerge; do
+  if [ $v = base ]; then lib=""; else lib=exp/ab/librsp_$v.so; fi
+  AB_LIB=$lib timeout -k 10 120 python3 tools/ab/music_dump.py gpurun_out/music_$v.npz || exit 1
+done
+python3 -c "
+import numpy as np
+a=np.load('gpurun_out/music_base.npz'); b=np.load('gpurun_out/music_mmerge.npz')
+print('music mmerge: eig maxrel', np.abs(a['eig']-b['eig']).max()/np.abs(a['eig']).max(), 'db maxdiff', np.abs(a['db']-b['db']).max(), 'peaks same', bool((a['peaks']==b['peaks']).all()))
+"
+for r in 1 2 3; do for v in base mmerge; do
+  if [ $v = base ]; then lib=""; else lib=exp/ab/librsp_$v.so; fi
+  echo "$r $v $(AB_LIB=$lib timeout -k 10 120 python3 tools/music_prof.py 1024 20 c128 | cut -c1-200)"
+done; done
