@@ -94,9 +94,6 @@ def parse(argv=None):
                     help='every frame also writes its complex range-Doppler map (rdm_13beam, fsf:131-136) to a '
                          'device buffer of the caller (rsp_enqueue_device_rdm): the rsp_mex(\'cube\') contract; '
                          'a secondary line, not the headline')
-    ap.add_argument('--cu-split', choices=['default', 'on', 'off'], default='default',
-                    help='queue on two CU sets (K1 of the next batch beside K2/K3 of the previous one): '
-                         'the plan default, or forced on / off (RSP_PLAN_CU_SPLIT / RSP_PLAN_NO_SPLIT)')
     ap.add_argument('--stage-timing', action='store_true',
                     help='HIP events around every kernel in the timed region (diagnostic: overlapped durations)')
     return ap.parse_args(argv)
@@ -364,8 +361,7 @@ def main():
 
     cfg, cfar, clus, W, ang, k = C.named_config(a.config)
     pre = precompute(cfg, W, ang, k, C.V8_FIR)
-    plan = Plan(cfg, cfar, clus, pre, device=dev, frames_per_launch=a.fpl, precision=a.precision,
-                cu_split={'default': None, 'on': True, 'off': False}[a.cu_split])
+    plan = Plan(cfg, cfar, clus, pre, device=dev, frames_per_launch=a.fpl, precision=a.precision)
     sz = plan.sizes
     targets = scene(cfg)
     cube_bytes = plan.cube_bytes

@@ -159,10 +159,6 @@ const char* rsp_last_error(void);
 /* Plan options (rsp_plan_options_default fills the defaults shown). */
 #define RSP_PLAN_K1_TILED 1   /* force the one-tile-per-workgroup K1 instead of the persistent
                                  one (both compute the same operations; parity tests compare them) */
-#define RSP_PLAN_CU_SPLIT 2   /* throughput queue on two CU sets: K1 of the next batch on one set
-                                 while K2 + K3 of the previous batch run on the other (the same
-                                 kernels and results; only where they run) */
-#define RSP_PLAN_NO_SPLIT 4   /* the queue's batches on one stream each, every kernel on all CUs */
 typedef struct rsp_plan_options {
     int32_t device;              /* HIP device ordinal (0)                                   */
     int32_t frames_per_launch;   /* frames batched into each kernel launch by the queue (1)  */
@@ -287,13 +283,6 @@ int32_t rsp_profile_stages(rsp_plan* plan, const void* const* d_cubes, int32_t n
 int32_t rsp_profile_stages_rdm(rsp_plan* plan, const void* const* d_cubes, int32_t n_cubes, void* const* d_rdms,
                                int32_t iters, float* ms_out, int64_t* bytes_out, int32_t cap, int32_t* frames_out);
 const char* rsp_stage_name(int32_t stage);
-/* Measurement of a CU split (diagnostic): `iters` launches of K1 (a batch of min(n_cubes,
- * frames_per_launch) frames) on a stream restricted to the CUs in mask_k1, concurrently with
- * `iters` launches of K2 (another batch's z) on a stream restricted to mask_k2 (mask_words 32-bit
- * words each, CU i = bit i % 32 of word i / 32; NULL: that stage is not run).  ms_out[0] = wall
- * ms per iteration of the pair, ms_out[1] / ms_out[2] = the K1 / K2 stream's ms per launch. */
-int32_t rsp_profile_split(rsp_plan* plan, const void* const* d_cubes, int32_t n_cubes, const uint32_t* mask_k1,
-                          const uint32_t* mask_k2, int32_t mask_words, int32_t iters, float* ms_out);
 
 /* The box's streaming-copy bandwidth (SURVEY 8(d) "measured stream-copy peak"): a 16-B-per-lane
  * non-temporal copy kernel over two device buffers of `bytes` each, `iters` timed launches;

@@ -42,12 +42,6 @@
 #ifndef RSP_K2_SH64
 #define RSP_K2_SH64 5
 #endif
-// Twiddle table form of one overlap-save FFT pass (radix R after Ns points): compact (the bases
-// W^(k 2^i), the other powers formed as products in registers) only where the full table
-// [k][r-1] would be large.  The passes right after the Ns = 1 pass (Ns (R - 1) <= 256: 2560's
-// radix-10 pass, 1024's radix-4 pass) keep full rows: R - 1 LDS reads and no products.
-// Shared by the kernels (tw_pass_off, sh_load / shg_load) and the plan (push_pass_twiddles).
-constexpr bool rsp_tw_cmp(int Ns, int R, bool cmp) { return cmp && Ns * (R - 1) > 256; }
 
 // Arithmetic of a plan: every device buffer, table and operation of the chain is in one of
 // these.  PREC_F64 is MATLAB's complex double (the reference's arithmetic, fsf:47,92,101,131);

@@ -80,25 +80,6 @@ __device__ __forceinline__ double cmag(d2 x) {
 // or past num_records reads 0 / drops the store, so masked lanes need no branch or select.
 // The read/write barrier inside an in-place LDS pass (every read of the pass before any write)
 #define RSP_WAR_SYNC() __syncthreads()
-// Synchronisation between the passes of an LDS FFT: the workgroup barrier, or (WL) only a
-// compiler fence when every row of the pass belongs to one wave (rows never shared between
-// waves): a wave's LDS instructions execute in order, so its reads of a pass complete before its
-// writes, and its writes before the next pass's reads.
-template <bool WL>
-__device__ __forceinline__ void pass_sync() {
-#if RSP_K2_WLBAR
-    __syncthreads();
-#else
-    if constexpr (WL) __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    else __syncthreads();
-#endif
-}
-#ifndef RSP_K2_WLOCAL
-#define RSP_K2_WLOCAL 0
-#endif
-#ifndef RSP_K2_WLBAR
-#define RSP_K2_WLBAR 0
-#endif
 #define RSP_OOB 0x80000000u   // > any buffer this library makes (plans are validated < 2 GB/frame)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, unsigned bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
@@ -367,7 +348,7 @@ constexpr int tw_pass_off(int LG, int q, bool rev = false, bool cmp = false, boo
     int off = 0, lgns = 0;
     for (int i = 0; i < q; ++i) {
         const int rb = rad_bits_p(LG, i, rev, pal);
-        if (i > 0) off += (1 << lgns) * tw_row(1 << rb, rsp_tw_cmp(1 << lgns, 1 << rb, cmp));
+        if (i > 0) off += (1 << lgns) * tw_row(1 << rb, cmp);
         lgns += rb;
     }
     return off;
@@ -385,15 +366,7 @@ constexpr int tw_total(int LG, bool rev = false, bool cmp = false, bool pal = fa
 // With power-of-two nb, Ns and pads every 2^SH, lidx(j + r nb) = lidx(j) + r nb + ((r nb) >> SH)
 // and lidx(idxD + r Ns) = lidx(idxD) + r Ns + ((r Ns) >> SH): every LDS address of a butterfly
 // is a per-thread base plus a compile-time offset (ds_read/ds_write immediate offsets).
-// WM: row r belongs to wave r (nrows = NTHR / 64): thread (wave w, lane l) takes butterflies
-// l + 64 t of row w, so that a pass's LDS traffic stays inside the wave (WL passes).
-template <int NTHR, int LGNB, bool WM>
-__device__ __forceinline__ int sh_beta(int t) {
-    if constexpr (WM) return ((threadIdx.x >> 6) << LGNB) + (threadIdx.x & 63) + 64 * t;
-    else return threadIdx.x + t * NTHR;
-}
-template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP = false, int XL = 0, bool WM = false,
-          class V>
+template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP = false, int XL = 0, class V>
 __device__ __forceinline__ void sh_load(const V* buf, int rs, int nrows, const V* tw, V (&v)[NB][R]) {
     constexpr int lgR = clog2(R);
     constexpr int lgnb = LGL - lgR;
@@ -403,14 +376,13 @@ __device__ __forceinline__ void sh_load(const V* buf, int rs, int nrows, const V
     const int total = nb * nrows;
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
-        const int beta = sh_beta<NTHR, lgnb, WM>(t);
+        const int beta = threadIdx.x + t * NTHR;
         if (beta < total) {
             const int row = beta >> lgnb, j = beta & (nb - 1);
             const int k = j & (Ns - 1);
             const V* src = XL ? buf + (row << LGL) + (j ^ ((j >> 4) & 7)) : buf + row * rs + lidx<SH>(j);
             V w[R];
-            constexpr bool CQ = rsp_tw_cmp(Ns, R, CMP);   // this pass's table form
-            if (LGNS > 0) load_tw<R, INV, CQ, Ns>(tw + (CQ ? k : k * tw_row(R, CQ)), w);
+            if (LGNS > 0) load_tw<R, INV, CMP, Ns>(tw + (CMP ? k : k * tw_row(R, CMP)), w);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 V x = src[r * nb + (SH && !XL ? (r * nb) >> SH : 0)];
@@ -426,7 +398,7 @@ __device__ __forceinline__ void sh_load(const V* buf, int rs, int nrows, const V
 // (Ns = 1 radix-16 passes only).  Their stores write 16 j + r for lane j, which the pad layout
 // puts 2-way on the banks of every group of 8 lanes; swizzled, the 8 lanes hit 8 distinct
 // 16-B banks, and the next pass's reads (j + r nb, nb a multiple of 128) stay conflict-free.
-template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, int XL = 0, bool WM = false, class V, class St>
+template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, int XL = 0, class V, class St>
 __device__ __forceinline__ void sh_store(V (&v)[NB][R], int rs, int nrows, const St& st) {
     constexpr int lgR = clog2(R);
     constexpr int lgnb = LGL - lgR;
@@ -436,7 +408,7 @@ __device__ __forceinline__ void sh_store(V (&v)[NB][R], int rs, int nrows, const
     const int total = nb * nrows;
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
-        const int beta = sh_beta<NTHR, lgnb, WM>(t);
+        const int beta = threadIdx.x + t * NTHR;
         if (beta < total) {
             const int row = beta >> lgnb, j = beta & (nb - 1);
             const int k = j & (Ns - 1);
@@ -457,24 +429,21 @@ __device__ __forceinline__ void sh_store(V (&v)[NB][R], int rs, int nrows, const
 }
 
 // TAIL = false: no barrier after the pass (the caller's next LDS writes go to other rows).
-template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP, int XL = 0, bool TAIL = true,
-          bool WL = false, class V, class St>
+template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP, int XL = 0, bool TAIL = true, class V,
+          class St>
 __device__ __forceinline__ void sh_pass(V* buf, int rs, int nrows, const V* tw, const St& st) {
     V v[NB][R];
-    sh_load<R, INV, NB, SH, NTHR, LGL, LGNS, CMP, XL, WL>(buf, rs, nrows, tw, v);
-    if constexpr (StoresLds<St>::value) {
-        if constexpr (WL) pass_sync<true>();
-        else RSP_WAR_SYNC();
-    }
-    sh_store<R, INV, NB, SH, NTHR, LGL, LGNS, 0, WL>(v, rs, nrows, st);
-    if constexpr (TAIL) pass_sync<WL>();
+    sh_load<R, INV, NB, SH, NTHR, LGL, LGNS, CMP, XL>(buf, rs, nrows, tw, v);
+    if constexpr (StoresLds<St>::value) RSP_WAR_SYNC();
+    sh_store<R, INV, NB, SH, NTHR, LGL, LGNS>(v, rs, nrows, st);
+    if constexpr (TAIL) __syncthreads();
 }
 
 // Passes Q..QEND-1 of a 2^LG-point FFT (radix order reversed if REV) over `nrows` rows;
 // pass n_passes - 1 stores through `last`, the others through `mid`.  tw = this plan's
 // concatenated tables.  PTS = complex points per thread (nrows * L / NTHR).
 template <int LG, int Q, int QEND, int LGNS, int PTS, bool INV, bool REV, int SH, int NTHR, bool CMP, bool PAL = false,
-          int XIN = 0, bool TAIL = true, bool WL = false, class V, class StMid, class StLast>
+          int XIN = 0, bool TAIL = true, class V, class StMid, class StLast>
 __device__ __forceinline__ void fft_range(V* buf, int rs, int nrows, const V* tw, const StMid& mid, const StLast& last) {
     constexpr int NP = n_passes(LG);
     if constexpr (Q < QEND) {
@@ -483,11 +452,10 @@ __device__ __forceinline__ void fft_range(V* buf, int rs, int nrows, const V* tw
         constexpr int NB = (PTS + R - 1) / R;
         const V* twq = tw + tw_pass_off(LG, Q, REV, CMP, PAL);
         if constexpr (Q == NP - 1)
-            sh_pass<R, INV, NB, SH, NTHR, LG, LGNS, CMP, XIN, TAIL, WL>(buf, rs, nrows, twq, last);
+            sh_pass<R, INV, NB, SH, NTHR, LG, LGNS, CMP, XIN, TAIL>(buf, rs, nrows, twq, last);
         else
-            sh_pass<R, INV, NB, SH, NTHR, LG, LGNS, CMP, XIN, true, WL>(buf, rs, nrows, twq, mid);
-        fft_range<LG, Q + 1, QEND, LGNS + RB, PTS, INV, REV, SH, NTHR, CMP, PAL, 0, TAIL, WL>(buf, rs, nrows, tw, mid,
-                                                                                             last);
+            sh_pass<R, INV, NB, SH, NTHR, LG, LGNS, CMP, XIN>(buf, rs, nrows, twq, mid);
+        fft_range<LG, Q + 1, QEND, LGNS + RB, PTS, INV, REV, SH, NTHR, CMP, PAL, 0, TAIL>(buf, rs, nrows, tw, mid, last);
     }
 }
 
@@ -531,8 +499,7 @@ __device__ __forceinline__ void shg_load(const V* buf, int rs, int nrows, const 
             const int row = beta / nb, j = beta - row * nb;
             const V* src = XL ? buf + row * L + (j ^ ((j >> 4) & 7)) : buf + row * rs + (SEP ? lidx<SH>(j) : 0);
             V w[R];
-            constexpr bool CQ = rsp_tw_cmp(NS, R, CMP);   // this pass's table form
-            if (NS > 1) load_tw<R, INV, CQ, NS>(tw + (CQ ? j % NS : (j % NS) * tw_row(R, CQ)), w);
+            if (NS > 1) load_tw<R, INV, CMP, NS>(tw + (CMP ? j % NS : (j % NS) * tw_row(R, CMP)), w);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 V x = XL ? src[r * nb] : (SEP ? src[lidx_off<SH, nb>(r)] : src[lidx<SH>(j + r * nb)]);
@@ -1161,7 +1128,7 @@ constexpr int k2_tw_lds(int LGM) {
            (k2_tw_sym(LGM) ? 0 : tw_total(LGM, true, RSP_K2_CMP, RSP_K2_PAL));
 }
 constexpr int k2_tw_lds_max() {
-    int m = 16 * tw_row(10, rsp_tw_cmp(16, 10, RSP_K2_CMP)) + 160 * tw_row(16, rsp_tw_cmp(160, 16, RSP_K2_CMP));   // k2_fft_job_mix<2560>
+    int m = 16 * tw_row(10, RSP_K2_CMP) + 160 * tw_row(16, RSP_K2_CMP);   // k2_fft_job_mix<2560>
     for (int lg = 6; lg <= 11; ++lg) m = k2_tw_lds(lg) > m ? k2_tw_lds(lg) : m;
     return m;
 }
@@ -1201,8 +1168,6 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     // one row per wave (nb0 a multiple of 64, one butterfly per thread): the row's sample window
     // is a scalar buffer resource, and a load's offset needs no mask
     constexpr bool WROW = nb0 >= 64 && NB0 == 1;
-    // RSP_K2_WLOCAL: one row per wave in every pass too (rows == 4), so passes sync the wave only
-    constexpr bool WLc = RSP_K2_WLOCAL && WROW && rows == K2_THREADS / 64;
     if constexpr (WROW) {
         const int rl = __builtin_amdgcn_readfirstlane(tid / nb0);
         // waves past the block's rows (fewer rows than 256 / nb0) load nothing
@@ -1268,23 +1233,22 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     sh_store<R0, false, NB0, SH, K2_THREADS, LGM, 0, XZ>(v0, rs, rows, StoreLds<V>{L});
     __syncthreads();
     // forward passes 1 .. NP-2
-    fft_range<LGM, 1, NP - 1, RB0, 16, false, false, SH, K2_THREADS, CMP, PAL, XZ, true, WLc>(L, rs, rows, twF,
-                                                                                          StoreLds<V>{L}, StoreLds<V>{L});
+    fft_range<LGM, 1, NP - 1, RB0, 16, false, false, SH, K2_THREADS, CMP, PAL, XZ>(L, rs, rows, twF, StoreLds<V>{L},
+                                                                               StoreLds<V>{L});
     // fused: forward last pass, x H (1/M folded in), inverse pass 0 of the reversed plan
     {
         V v[NBL][RL];
-        sh_load<RL, false, NBL, SH, K2_THREADS, LGM, LGM - RBL, CMP, 0, WLc>(
-            L, rs, rows, twF + tw_pass_off(LGM, NP - 1, false, CMP, PAL), v);
-        if constexpr (WLc) pass_sync<true>();
-        else RSP_WAR_SYNC();
+        sh_load<RL, false, NBL, SH, K2_THREADS, LGM, LGM - RBL, CMP>(L, rs, rows,
+                                                                      twF + tw_pass_off(LGM, NP - 1, false, CMP, PAL), v);
+        RSP_WAR_SYNC();
 #pragma unroll
         for (int t = 0; t < NBL; ++t) {
             Dft<RL, false, V>::run(v[t]);
 #pragma unroll
             for (int r = 0; r < RL; ++r) v[t][r] = vmul(v[t][r], hreg[(t % NHT) * RL + r]);
         }
-        sh_store<RL, true, NBL, SH, K2_THREADS, LGM, 0, XZ, WLc>(v, rs, rows, StoreLds<V>{L});
-        pass_sync<WLc>();
+        sh_store<RL, true, NBL, SH, K2_THREADS, LGM, 0, XZ>(v, rs, rows, StoreLds<V>{L});
+        __syncthreads();
     }
     // inverse passes 1 .. NP-1 (reversed radices); the last keeps the valid overlap-save
     // outputs = stitched gates
@@ -1293,17 +1257,17 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     if constexpr (WROW) {
         // inverse passes 1 .. NP-2 into LDS, then the last one (Ns = nb0, input not swizzled:
         // XZ applies to the pass after an Ns = 1 pass only) into this wave's row of the maps
-        fft_range<LGM, 1, NP - 1, RBL, 16, true, true, SH, K2_THREADS, CMP, PAL, XZ, true, WLc>(
-            L, rs, rows, twI, StoreLds<V>{L}, StoreLds<V>{L});
+        fft_range<LGM, 1, NP - 1, RBL, 16, true, true, SH, K2_THREADS, CMP, PAL, XZ>(L, rs, rows, twI, StoreLds<V>{L},
+                                                                                   StoreLds<V>{L});
         constexpr int LGNSL = LGM - RB0;
         static_assert(NP >= 3 || XZ == 0, "last pass input is never swizzled");
         const V* twl_last = twI + tw_pass_off(LGM, NP - 1, true, CMP, PAL);
         const int rho = row0 + __builtin_amdgcn_readfirstlane(tid / nb0);
         if (rdm)
-            sh_pass<R0, true, NB0, SH, K2_THREADS, LGM, LGNSL, CMP, 0, false, WLc>(
+            sh_pass<R0, true, NB0, SH, K2_THREADS, LGM, LGNSL, CMP, 0, false>(
                 L, rs, rows, twl_last, StoreRowK<V, true, nb0, R0>(rdm, mag, G, g.Gp, rho, rows_total, Lh1, g0, gend));
         else
-            sh_pass<R0, true, NB0, SH, K2_THREADS, LGM, LGNSL, CMP, 0, false, WLc>(
+            sh_pass<R0, true, NB0, SH, K2_THREADS, LGM, LGNSL, CMP, 0, false>(
                 L, rs, rows, twl_last, StoreRowK<V, false, nb0, R0>(rdm, mag, G, g.Gp, rho, rows_total, Lh1, g0, gend));
     } else
         fft_range<LGM, 1, NP, RBL, 16, true, true, SH, K2_THREADS, CMP, PAL, XZ, false>(
@@ -1337,8 +1301,8 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
     constexpr int NB0 = (nb0 * rows + K2_THREADS - 1) / K2_THREADS;
     constexpr int NB1 = ((M / R1) * rows + K2_THREADS - 1) / K2_THREADS;
     constexpr int NS1 = R0, NS2 = R0 * R1;                               // Ns of passes 1 and 2
-    constexpr int TW2 = NS1 * tw_row(R1, rsp_tw_cmp(NS1, R1, CMP));      // offset of pass 2's table
-    constexpr int NTWF = TW2 + NS2 * tw_row(R0, rsp_tw_cmp(NS2, R0, CMP));
+    constexpr int TW2 = NS1 * tw_row(R1, CMP);                           // offset of pass 2's table
+    constexpr int NTWF = TW2 + NS2 * tw_row(R0, CMP);
     const int P = g.P, G = g.G;
     const int lo = sd.lo, hi = sd.hi, off = sd.off;
     const int tid = threadIdx.x;

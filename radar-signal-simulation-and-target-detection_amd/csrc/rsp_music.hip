@@ -774,9 +774,6 @@ __global__ __launch_bounds__(MU_THREADS, 2) void k_music_cov64(int N, int K, con
 // the pad rows) p_{r+1} would be 0 again and flip once more; at e_r^2 >= 2^-600 it is not, and the
 // eigenvalues move by at most ~2^-300.
 #define ME_E2MIN 0x1p-600
-#ifndef ME_MERGE
-#define ME_MERGE 0   // one barrier for the p^H v partials and p (w formed per lane), A/B builds
-#endif
 #ifndef ME_WPS
 #define ME_WPS 4     // waves per SIMD the register budget is sized for (4 instances per CU)
 #endif
@@ -881,31 +878,17 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
         pv.x = wsumd(pv.x);
         pv.y = wsumd(pv.y);
         if (lane == 0) red[w] = pv;
-#if ME_MERGE
-        // p itself goes out with the partial sums (one barrier): every lane then forms the
-        // w_j = p_j + alpha v_j of its own rows (p_j = 0 for the finished columns j <= k)
-        if (q == 0) wk[i] = p;
-        __syncthreads();
-        const double2 sp = zadd(zadd(red[0], red[1]), zadd(red[2], red[3]));
-        const double2 alpha = zsc(-0.5, zm(tau, sp));
-        const double2 wi = act ? zadd(p, zm(alpha, vi)) : z2;
-#else
         __syncthreads();
         const double2 sp = zadd(zadd(red[0], red[1]), zadd(red[2], red[3]));
         const double2 alpha = zsc(-0.5, zm(tau, sp));
         const double2 wi = act ? zadd(p, zm(alpha, vi)) : z2;
         if (q == 0) wk[i] = wi;
         __syncthreads();
-#endif
         if (act) {   // A(j, i) -= v_j conj(w_i) + w_j conj(v_i) (v_j = w_j = 0 for j <= k): 8 FMAs
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
                 const int j = 16 * q + u;
-#if ME_MERGE
-                const double2 vj = vk[j], wj = zadd(wk[j], zm(alpha, vj));
-#else
                 const double2 vj = vk[j], wj = wk[j];
-#endif
                 double ax = a[u].x, ay = a[u].y;
                 ax = fma(-vj.x, wi.x, ax);
                 ax = fma(-vj.y, wi.y, ax);

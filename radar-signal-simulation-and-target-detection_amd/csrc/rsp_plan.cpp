@@ -101,7 +101,6 @@ void radix_plan(int m, int* nrad, int* rad, bool pal = false) {
 }
 
 void push_pass_twiddles(std::vector<cd>& out, int Ns, int R, bool cmp) {
-    cmp = rsp_tw_cmp(Ns, R, cmp);   // the pass's table form (rsp_internal.h)
     if (cmp) {
         for (int r = 1; r < R; r *= 2)
             for (int k = 0; k < Ns; ++k) out.push_back(root_of_unity((long long)k * r, (long long)Ns * R));
@@ -148,7 +147,6 @@ struct Lane {
     hipEvent_t tev[4] = {};         // live stage timing: before K1, after K1, K2, K3
     bool timed = false;
     hipEvent_t done = nullptr;
-    hipEvent_t k1done = nullptr;   // CU split: K2 + K3 of the batch after its K1
     void* z = nullptr;          // F frames
     void* rdm = nullptr;        // ONE frame: the synchronous paths' RDM (queue frames write the caller's maps)
     void* mag = nullptr;        // F frames
@@ -249,10 +247,6 @@ struct rsp_plan {
     size_t h_stage_bytes = 0;
     Lane lanes[RSP_LANES];
     int nlanes = RSP_NLANES;   // lanes (streams) of the throughput queue
-    // CU split of the queue (RSP_PLAN_CU_SPLIT): every batch's K1 on s_k1 (restricted to split_k1
-    // CUs, the persistent grid sized to them), its K2 + K3 + read-back on s_k2 (the other CUs)
-    int split_k1 = 0;
-    hipStream_t s_k1 = nullptr, s_k2 = nullptr;
     int next_lane = 0;
     // live stage timing of the queue (rsp_set_stage_timing): HIP events around K1/K2/K3 of
     // every batch, summed at harvest
@@ -346,16 +340,10 @@ rsp_plan::~rsp_plan() {
         if (L.h_dets) (void)hipHostFree(L.h_dets);
         if (L.dets) (void)hipFree(L.dets);
         if (L.done) (void)hipEventDestroy(L.done);
-        if (L.k1done) (void)hipEventDestroy(L.k1done);
         for (auto& e : L.tev)
             if (e) (void)hipEventDestroy(e);
         if (L.stream) (void)hipStreamDestroy(L.stream);
     }
-    for (hipStream_t st : {s_k1, s_k2})
-        if (st) {
-            (void)hipStreamSynchronize(st);
-            (void)hipStreamDestroy(st);
-        }
     if (up_stream) (void)hipStreamSynchronize(up_stream);
     for (auto e : slot_ready) if (e) (void)hipEventDestroy(e);
     for (auto e : slot_free) if (e) (void)hipEventDestroy(e);
@@ -469,7 +457,6 @@ int pow2_at_least(int x) {
 int setup_lane(rsp_plan* p, Lane& L) {
     HIPCHK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&L.done, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&L.k1done, hipEventDisableTiming));
     for (auto& e : L.tev) HIPCHK(hipEventCreate(&e));
     int rc;
     if ((rc = p->dalloc_bytes(&L.z, p->z_elems * p->F * p->esz))) return rc;
@@ -501,50 +488,36 @@ FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const void* const* in, int
 
 // Enqueue K1 -> K2 -> K3 for nf frames on lane L, plus the async detection read-back.
 // smap (optional, one frame): K3 also writes rdm_for_cfar_all there.
-#ifndef RSP_SPLIT_DEFAULT
-#define RSP_SPLIT_DEFAULT 0   // the queue's CU split without RSP_PLAN_CU_SPLIT (A/B builds)
-#endif
-#ifndef RSP_SPLIT_K1
-#define RSP_SPLIT_K1 96       // CUs (of 256) the split gives K1
-#endif
 #ifndef RSP_K3_TILE_KB
 #define RSP_K3_TILE_KB 48   // KB of S per K3 tile (48: 2 Doppler bands at P = 128, 3 workgroups per CU)
 #endif
 #ifndef RSP_K3_RT_C128
 #define RSP_K3_RT_C128 32   // K3 tile width in range cells, complex double (32 or 64)
 #endif
-// split (the queue with RSP_PLAN_CU_SPLIT): K1 on p->s_k1, the rest on p->s_k2 behind L.k1done.
 // A lane's buffers are reused only after harvest has waited for the lane's previous batch.
 int launch_batch(rsp_plan* p, Lane& L, const void* const* in, const int* ids, int nf, void* smap = nullptr,
-                 const int* slots = nullptr, void* const* rdm = nullptr, bool split = false) {
+                 const int* slots = nullptr, void* const* rdm = nullptr) {
     FramePtrs fp = lane_ptrs(p, L, in, nf, rdm);
     fp.smap[0] = smap;
-    hipStream_t s1 = split ? p->s_k1 : L.stream, s2 = split ? p->s_k2 : L.stream;
     if (slots)   // producer-ring frames: K1 after their upload / synthesis
         for (int f = 0; f < nf; ++f)
-            if (slots[f] >= 0) HIPCHK(hipStreamWaitEvent(s1, p->slot_ready[slots[f]], 0));
+            if (slots[f] >= 0) HIPCHK(hipStreamWaitEvent(L.stream, p->slot_ready[slots[f]], 0));
     L.timed = p->time_stages;
-    if (L.timed) HIPCHK(hipEventRecord(L.tev[0], s1));
-    Geometry g1 = p->g;
-    if (split) g1.ncu = p->split_k1;   // the persistent K1's grid: one workgroup per CU of its set
-    HIPCHK(launch_k1(g1, p->k, fp, nf, 3, s1));
+    if (L.timed) HIPCHK(hipEventRecord(L.tev[0], L.stream));
+    HIPCHK(launch_k1(p->g, p->k, fp, nf, 3, L.stream));
     if (slots)   // K1 has read the cubes: their slots may be written again
         for (int f = 0; f < nf; ++f)
-            if (slots[f] >= 0) HIPCHK(hipEventRecord(p->slot_free[slots[f]], s1));
-    if (L.timed) HIPCHK(hipEventRecord(L.tev[1], s1));
-    if (split) {
-        HIPCHK(hipEventRecord(L.k1done, s1));
-        HIPCHK(hipStreamWaitEvent(s2, L.k1done, 0));
-    }
-    HIPCHK(launch_k2(p->g, p->k, fp, nf, p->g.B * p->g.P, s2));
-    if (L.timed) HIPCHK(hipEventRecord(L.tev[2], s2));
+            if (slots[f] >= 0) HIPCHK(hipEventRecord(p->slot_free[slots[f]], L.stream));
+    if (L.timed) HIPCHK(hipEventRecord(L.tev[1], L.stream));
+    HIPCHK(launch_k2(p->g, p->k, fp, nf, p->g.B * p->g.P, L.stream));
+    if (L.timed) HIPCHK(hipEventRecord(L.tev[2], L.stream));
     Geometry g3 = p->g;
     g3.max_dets = L.dcap;
-    HIPCHK(launch_k3(g3, p->k, fp, nf, s2));
-    if (L.timed) HIPCHK(hipEventRecord(L.tev[3], s2));
+    HIPCHK(launch_k3(g3, p->k, fp, nf, L.stream));
+    if (L.timed) HIPCHK(hipEventRecord(L.tev[3], L.stream));
     // every frame's count and detections into the lane's mapped pinned lists (only what exists)
-    HIPCHK(launch_dets_to_host(L.dets, L.dcap, L.h_dets_dev, L.hcap, nf, s2));
-    HIPCHK(hipEventRecord(L.done, s2));
+    HIPCHK(launch_dets_to_host(L.dets, L.dcap, L.h_dets_dev, L.hcap, nf, L.stream));
+    HIPCHK(hipEventRecord(L.done, L.stream));
     L.fp = fp;
     L.nf = nf;
     for (int f = 0; f < nf; ++f) L.frame_ids[f] = ids[f];
@@ -625,7 +598,7 @@ int flush_pending(rsp_plan* p) {
     Lane& L = p->lanes[p->next_lane];
     int rc = harvest(p, L);
     if (rc) return rc;
-    rc = launch_batch(p, L, p->pend_in, p->pend_ids, p->npend, nullptr, p->pend_slot, p->pend_rdm, p->split_k1 > 0);
+    rc = launch_batch(p, L, p->pend_in, p->pend_ids, p->npend, nullptr, p->pend_slot, p->pend_rdm);
     p->npend = 0;
     p->next_lane = (p->next_lane + 1) % p->nlanes;
     return rc;
@@ -831,10 +804,7 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
     const int device = opt->device, frames_per_launch = opt->frames_per_launch;
     if (opt->precision != RSP_C64 && opt->precision != RSP_C128)
         return fail(RSP_ERR_INVALID, "precision must be RSP_C128 or RSP_C64, got %d", opt->precision);
-    if (opt->flags & ~(RSP_PLAN_K1_TILED | RSP_PLAN_CU_SPLIT | RSP_PLAN_NO_SPLIT))
-        return fail(RSP_ERR_INVALID, "unknown plan flags 0x%x", opt->flags);
-    if ((opt->flags & RSP_PLAN_CU_SPLIT) && (opt->flags & RSP_PLAN_NO_SPLIT))
-        return fail(RSP_ERR_INVALID, "RSP_PLAN_CU_SPLIT and RSP_PLAN_NO_SPLIT together");
+    if (opt->flags & ~RSP_PLAN_K1_TILED) return fail(RSP_ERR_INVALID, "unknown plan flags 0x%x", opt->flags);
     const int C = cfg->channel_num, B = cfg->beam_num, P = cfg->prtNum, N = cfg->point_PRT;
     const int g1 = pre->N_gate_narrow, g2 = pre->N_gate_medium, g3 = pre->N_gate_long, G = pre->N_total_gate;
     if (C < 1 || C > 32 || B < 1 || B > 16 || P < 2 || N < 2)
@@ -1136,27 +1106,6 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
     if ((rc = p->dalloc_bytes(&p->d_cube, (size_t)std::max(C, B) * g.cpitch * esz))) return bail(rc);
     for (auto& L : p->lanes)
         if ((rc = setup_lane(p, L))) return bail(rc);
-    // CU split of the queue: K1 (HBM-bound) on RSP_SPLIT_K1 / 256 of the CUs -- the same share of
-    // every XCD's 32 -- and K2 + K3 (bound by VALU / LDS latency) on the rest, so that the next
-    // batch's K1 streams while this batch's K2 computes
-    const bool want_split = (opt->flags & RSP_PLAN_CU_SPLIT) || (RSP_SPLIT_DEFAULT && !(opt->flags & RSP_PLAN_NO_SPLIT));
-    if (want_split && g.ncu >= 64 && p->F > 1 && k1_persistent_fits(g)) {
-        const int per = std::max(1, std::min(31, (RSP_SPLIT_K1 * 32 + 128) / 256));   // K1 CUs of each 32
-        const int words = (g.ncu + 31) / 32;
-        std::vector<uint32_t> m1(words, 0u), m2(words, 0u);
-        int n1 = 0;
-        for (int c = 0; c < g.ncu; ++c) {
-            if (c % 32 < per) {
-                m1[c / 32] |= 1u << (c % 32);
-                ++n1;
-            } else {
-                m2[c / 32] |= 1u << (c % 32);
-            }
-        }
-        HIPCHK(hipExtStreamCreateWithCUMask(&p->s_k1, (uint32_t)words, m1.data()));
-        HIPCHK(hipExtStreamCreateWithCUMask(&p->s_k2, (uint32_t)words, m2.data()));
-        p->split_k1 = n1;
-    }
     *out = p;
     return RSP_OK;
 }
@@ -1561,67 +1510,6 @@ int32_t rsp_profile_stages_rdm(rsp_plan* p, const void* const* d_cubes, int32_t 
         if (cap > 1) bytes_out[1] = nf * (z + mag + rdm);
         if (cap > 2) bytes_out[2] = nf * mag;
     }
-    return RSP_OK;
-}
-
-int32_t rsp_profile_split(rsp_plan* p, const void* const* d_cubes, int32_t n_cubes, const uint32_t* mask_k1,
-                          const uint32_t* mask_k2, int32_t mask_words, int32_t iters, float* ms_out) {
-    if (!p || !d_cubes || n_cubes < 1 || iters < 1 || !ms_out || mask_words < 0 || mask_words > 64)
-        return fail(RSP_ERR_INVALID, "bad argument");
-    HIPCHK(hipSetDevice(p->device));
-    int rc = drain_all(p);
-    if (rc) return rc;
-    const int nf = std::min(n_cubes, p->F);
-    const void* in[RSP_MAX_F];
-    for (int f = 0; f < nf; ++f) in[f] = d_cubes[f % n_cubes];
-    // K2 reads lane 0's z (made once below by K1), K1 writes lane 1's: the two never touch the same buffer
-    const FramePtrs f2 = lane_ptrs(p, p->lanes[0], in, nf, nullptr);
-    const FramePtrs f1 = lane_ptrs(p, p->lanes[1], in, nf, nullptr);
-    auto popc = [&](const uint32_t* m) {
-        int c = 0;
-        for (int i = 0; i < mask_words; ++i) c += __builtin_popcount(m[i]);
-        return c;
-    };
-    Geometry g1 = p->g, g2 = p->g;
-    if (mask_k1) g1.ncu = std::max(1, std::min(g1.ncu, popc(mask_k1)));   // persistent K1: one workgroup per CU
-    hipStream_t sa = nullptr, sb = nullptr;
-    hipEvent_t e0 = nullptr, ea = nullptr, eb = nullptr;
-    hipError_t e = hipSuccess;
-    auto mk = [&](hipStream_t* st, const uint32_t* m) {
-        return m ? hipExtStreamCreateWithCUMask(st, (uint32_t)mask_words, m) : hipStreamCreateWithFlags(st, hipStreamNonBlocking);
-    };
-    if ((e = mk(&sa, mask_k1)) == hipSuccess && (e = mk(&sb, mask_k2)) == hipSuccess && (e = hipEventCreate(&e0)) == hipSuccess &&
-        (e = hipEventCreate(&ea)) == hipSuccess && (e = hipEventCreate(&eb)) == hipSuccess) {
-        e = launch_k1(p->g, p->k, f2, nf, 3, sb);   // lane 0's z for K2
-        for (int w = 0; w < 2 && e == hipSuccess; ++w) {   // warm-up
-            if (mask_k1) e = launch_k1(g1, p->k, f1, nf, 3, sa);
-            if (e == hipSuccess && mask_k2) e = launch_k2(g2, p->k, f2, nf, g2.B * g2.P, sb);
-        }
-        if (e == hipSuccess) e = hipStreamSynchronize(sa);
-        if (e == hipSuccess) e = hipStreamSynchronize(sb);
-        if (e == hipSuccess) e = hipEventRecord(e0, sa);
-        if (e == hipSuccess) e = hipStreamWaitEvent(sb, e0, 0);
-        for (int i = 0; i < iters && e == hipSuccess; ++i) {
-            if (mask_k1) e = launch_k1(g1, p->k, f1, nf, 3, sa);
-            if (e == hipSuccess && mask_k2) e = launch_k2(g2, p->k, f2, nf, g2.B * g2.P, sb);
-        }
-        if (e == hipSuccess) e = hipEventRecord(ea, sa);
-        if (e == hipSuccess) e = hipEventRecord(eb, sb);
-        if (e == hipSuccess) e = hipEventSynchronize(ea);
-        if (e == hipSuccess) e = hipEventSynchronize(eb);
-        float ta = 0.f, tb = 0.f;
-        if (e == hipSuccess) e = hipEventElapsedTime(&ta, e0, ea);
-        if (e == hipSuccess) e = hipEventElapsedTime(&tb, e0, eb);
-        ms_out[0] = std::max(ta, tb) / iters;
-        ms_out[1] = ta / iters;
-        ms_out[2] = tb / iters;
-    }
-    if (e0) (void)hipEventDestroy(e0);
-    if (ea) (void)hipEventDestroy(ea);
-    if (eb) (void)hipEventDestroy(eb);
-    if (sa) (void)hipStreamDestroy(sa);
-    if (sb) (void)hipStreamDestroy(sb);
-    if (e != hipSuccess) return fail(RSP_ERR_DEVICE, "split profile: %s", hipGetErrorString(e));
     return RSP_OK;
 }
 

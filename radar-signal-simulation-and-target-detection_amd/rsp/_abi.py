@@ -72,8 +72,6 @@ class Sizes(ct.Structure):
 
 
 RSP_PLAN_K1_TILED = 1
-RSP_PLAN_CU_SPLIT = 2
-RSP_PLAN_NO_SPLIT = 4
 
 
 class PlanOptions(ct.Structure):
@@ -170,8 +168,6 @@ PROTOTYPES = {
     'rsp_profile_stages_rdm': (ct.c_int32, [_P, ct.POINTER(_P), ct.c_int32, ct.POINTER(_P), ct.c_int32,
                                             ct.POINTER(ct.c_float), ct.POINTER(ct.c_int64), ct.c_int32,
                                             ct.POINTER(ct.c_int32)]),
-    'rsp_profile_split': (ct.c_int32, [_P, ct.POINTER(_P), ct.c_int32, ct.POINTER(ct.c_uint32), ct.POINTER(ct.c_uint32),
-                                       ct.c_int32, ct.c_int32, ct.POINTER(ct.c_float)]),
     'rsp_stage_name': (ct.c_char_p, [ct.c_int32]),
     'rsp_hbm_copy_probe': (ct.c_int32, [ct.c_int32, ct.c_int64, ct.c_int32, ct.POINTER(ct.c_double)]),
     'rsp_set_stage_timing': (ct.c_int32, [_P, ct.c_int32]),

@@ -36,7 +36,7 @@ class Plan:
     """
 
     def __init__(self, config, cfar_params, cluster_params, precomputed_data, device=0, frames_per_launch=1,
-                 precision='c128', k1_tiled=False, cu_split=None):
+                 precision='c128', k1_tiled=False):
         sc = config['Sig_Config']
         pre = precomputed_data
         self.config = config
@@ -80,8 +80,7 @@ class Plan:
         check(lib().rsp_plan_options_default(ct.byref(opt)))
         opt.device, opt.frames_per_launch = int(device), int(frames_per_launch)
         opt.precision = _abi.RSP_C128 if precision == 'c128' else _abi.RSP_C64
-        opt.flags = (_abi.RSP_PLAN_K1_TILED if k1_tiled else 0) | \
-            {None: 0, True: _abi.RSP_PLAN_CU_SPLIT, False: _abi.RSP_PLAN_NO_SPLIT}[cu_split]
+        opt.flags = _abi.RSP_PLAN_K1_TILED if k1_tiled else 0
         h = ct.c_void_p()
         check(lib().rsp_plan_create_ex(ct.byref(self.cfg), ct.byref(self.cfar), ct.byref(self.cluster),
                                        ct.byref(self.pre), ct.byref(opt), ct.byref(h)))
