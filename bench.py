@@ -475,7 +475,9 @@ def main():
         dom = max(stages, key=lambda s: s['ms_per_launch'])
         achieved = dom['achieved_GBps']
         traffic = None
-        tf = os.path.join(ROOT, 'profiles', 'pmc_traffic_%s_%s.json' % (a.config, a.precision))
+        # the PMC passes of the same workload (with the RD map written: tools/pmc_pass.sh CFG PREC rdm)
+        tf = os.path.join(ROOT, 'profiles', 'pmc_traffic_%s_%s%s.json' % (a.config, a.precision,
+                                                                         '_rdm' if a.want_rdm else ''))
         if os.path.exists(tf):
             with open(tf) as f:
                 tj = json.load(f)

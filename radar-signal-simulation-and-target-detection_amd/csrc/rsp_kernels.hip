@@ -1030,26 +1030,6 @@ struct StoreRdm {   // last inverse pass: keep outputs i in [Lh-1, Lh-1+V) that 
         buf_st1(mag, ok ? (unsigned)(rho * Gp + gg) * (unsigned)sizeof(scal<V>) : RSP_OOB, cmag(x));
     }
 };
-// The same for a pass whose wave covers one row (nb >= 64, one butterfly per thread): the row's
-// kept gates [g0, gend) get their own buffer resources (scalar), so the output's offset
-// (o - Lh1) masks both ends by itself -- o < Lh1 wraps past num_records, o - Lh1 >= gend - g0
-// is past it -- and a row beyond rows_total has num_records 0.  One VALU add per store.
-// (Skipping |x| of the discarded outputs behind a branch measured +9 us per 8 x2 frames.)
-template <class V>
-struct StoreRdmW {
-    typedef scal<V> S;
-    V* rdm; S* mag; int G; int Gp; int row0; int rows_total; int Lh1; int g0; int gend;
-    __device__ __forceinline__ void put(int, int row, int o, int, V x) const {
-        const int rho = row0 + __builtin_amdgcn_readfirstlane(row);
-        const unsigned n = rho < rows_total ? (unsigned)(gend - g0) : 0u;
-        const __amdgpu_buffer_rsrc_t rr = buf_rsrc(rdm + (size_t)rho * G + g0, n * (unsigned)sizeof(V));
-        const __amdgpu_buffer_rsrc_t mr = buf_rsrc(mag + (size_t)rho * Gp + g0, n * (unsigned)sizeof(S));
-        // (o - Lh1) * size, written so that o's constant part folds into one add per store
-        if (rdm)   // uniform: null when the launch keeps the RDM on chip (lane_ptrs)
-            buf_st<RSP_RDM_AUX>(rr, (unsigned)o * (unsigned)sizeof(V) - (unsigned)Lh1 * (unsigned)sizeof(V), x);
-        buf_st1(mr, (unsigned)o * (unsigned)sizeof(S) - (unsigned)Lh1 * (unsigned)sizeof(S), cmag(x));
-    }
-};
 // The same for a pass whose output rows are uniform per wave (or per workgroup): the row's
 // resources are built once, before the pass, by the caller; RDM (compile-time) says whether the
 // complex map is stored.  The pass is the overlap-save block's last inverse pass with nb = NS
@@ -1074,8 +1054,15 @@ struct StoreRowK {
     __device__ __forceinline__ void put(int idx, int, int o, int, V x) const {
         const int r = idx % R;
         if (r < R / 2 && r < rskip) return;
-        if (RDM) buf_st<RSP_RDM_AUX>(rr, (unsigned)o * (unsigned)sizeof(V) - lh1v, x);
-        buf_st1(mr, (unsigned)o * (unsigned)sizeof(S) - lh1s, cmag(x));
+        // The masked outputs rely on the wrapped offset being past num_records.  Left visible,
+        // (o - Lh1) size = j size - Lh1 size + r NS size is split by the compiler into a wrapped
+        // VGPR offset plus an immediate r NS size, and the range check of that sum is not the
+        // modular one: the first kept gate of a block was dropped (complex single, maps without
+        // the RDM).  The opaque offset keeps the whole (wrapped) value in the VGPR.
+        unsigned ov = (unsigned)o * (unsigned)sizeof(V) - lh1v, os = (unsigned)o * (unsigned)sizeof(S) - lh1s;
+        asm volatile("" : "+v"(ov), "+v"(os));
+        if (RDM) buf_st<RSP_RDM_AUX>(rr, ov, x);
+        buf_st1(mr, os, cmag(x));
     }
 };
 

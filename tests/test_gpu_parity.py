@@ -66,8 +66,11 @@ def case(request):
     st = {k: st[k] for k in ('rdm', 'S_all', 'dets', 'par')}
     plan = Plan(s['cfg'], s['cfar'], s['clus'], s['pre_p'], precision=prec)
     gpu = plan.process_cube(cube, frame_idx=1, want_rdm=True, want_cfar=True)
+    # the same frame with the complex map kept on chip (K2's magnitude-only store path, as the
+    # throughput queue runs it)
+    gpu_mag = plan.process_cube(cube, frame_idx=1, want_rdm=False, want_cfar=True)
     plan.close()
-    yield dict(name=name, prec=prec, s=s, tg=tg, fin=fin, st=st, gpu=gpu)
+    yield dict(name=name, prec=prec, s=s, tg=tg, fin=fin, st=st, gpu=gpu, gpu_mag=gpu_mag)
 
 
 def _map_close(a, b, tol):
@@ -86,6 +89,15 @@ def test_rdm_parity(case):
 def test_cfar_map_parity(case):
     """rdm_for_cfar_all as produced on the device (K3's S tile), not recomputed on the host."""
     _map_close(case['gpu']['cfar_maps'], case['st']['S_all'], MAP_TOL[case['prec']])
+
+
+def test_cfar_map_without_rdm(case):
+    """K2 without the complex RD map stores the same magnitudes: the CFAR maps and the detection
+    list are bit-identical to the run that also writes the RDM."""
+    a, b = case['gpu_mag'], case['gpu']
+    assert np.array_equal(a['cfar_maps'], b['cfar_maps']), 'max diff %g' % np.abs(a['cfar_maps'] - b['cfar_maps']).max()
+    assert [(d['v_idx'], d['r_idx'], d['pair_idx']) for d in a['detections']] == \
+        [(d['v_idx'], d['r_idx'], d['pair_idx']) for d in b['detections']]
 
 
 def _keys(dets):

@@ -3,7 +3,7 @@ usage: ab_pytest.py LIB_PATH [pytest args...]"""
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, 'radar-signal-simulation-and-target-detection_amd'))
 sys.path.insert(0, ROOT)
 from rsp import _abi   # noqa: E402

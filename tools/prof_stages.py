@@ -1,7 +1,8 @@
 """Profiling driver: time/profile each device stage of one config #2 frame N times.
 
 Used under rocprofv3 (kernel trace / PMC passes); prints the in-process HIP-event
-stage times as JSON.
+stage times as JSON.  usage: prof_stages.py [CONFIG] [ITERS] [FRAMES_PER_LAUNCH] [PREC] [rdm]
+(rdm: K2 also writes every frame's complex RD map, as rsp_enqueue_device_rdm)
 """
 import json
 import os
@@ -32,8 +33,13 @@ def main():
     for i, p in enumerate(cubes):
         plan.synthesize_device(p, tg, 1 + i)
         tg = C.evolve_targets(tg, cfg)
-    st = plan.profile_stages(cubes, iters=iters)
+    rdms = None
+    if len(sys.argv) > 5 and sys.argv[5] == 'rdm':
+        rdms = [plan.device_alloc(plan.sizes.rdm_elems * plan.sizes.elem_bytes) for _ in range(nf)]
+    st = plan.profile_stages(cubes, iters=iters, d_rdms=rdms)
     print(json.dumps(st))
+    for p in rdms or []:
+        plan.device_free(p)
     for p in cubes:
         plan.device_free(p)
     plan.close()
