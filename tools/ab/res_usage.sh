@@ -1,7 +1,7 @@
 #!/bin/bash
 # Per-kernel VGPR / scratch / occupancy of rsp_kernels.hip (hipcc resource-usage remarks), one line each.
 cd "$(dirname "$0")/../../radar-signal-simulation-and-target-detection_amd/csrc"
-/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../../include -Wno-unused-function -x hip -c ${1:-rsp_kernels.hip} \
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../../include -Wno-unused-function -x hip -c ${1:-rsp_kernels.hip} ${@:2} \
   -o /dev/null -Rpass-analysis=kernel-resource-usage 2>&1 | python3 -c '
 import sys, re, subprocess
 cur = None
