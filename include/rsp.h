@@ -435,7 +435,8 @@ typedef struct rsp_music_scene {
 /* Caller-owned outputs for n_inst instances; any pointer may be NULL (not produced). */
 typedef struct rsp_music_out {
     double* spectrum_db;      /* [n_scan x I] P_MUSIC_dB (MUSIC_1D.m:41)                      */
-    double* eigenvalues;      /* [N x I] descending (MUSIC_1D.m:30-31)                         */
+    double* eigenvalues;      /* [N x I] descending (MUSIC_1D.m:30-31); when NULL, complex double
+                                 finds only the M signal eigenvalues the spectrum needs        */
     int32_t* peak_idx;        /* [M x I] 1-based scan indices of the M largest peaks (:43-47), 0 = none */
     int32_t* n_peaks;         /* [I] number of findpeaks peaks                                 */
     double* covariance;       /* complex [N x N x I] R (MUSIC_1D.m:28), column-major           */
@@ -454,7 +455,8 @@ int32_t rsp_music_process_device(rsp_music_plan* plan, const void* d_X, int32_t 
 int32_t rsp_music_synthesize_device(rsp_music_plan* plan, const rsp_music_scene* scene, int32_t n_inst,
                                     int32_t inst0, uint64_t seed, void* d_X);
 /* HIP-event timing of the two device stages (ms_out[0] covariance, ms_out[1] eig + spectrum)
- * averaged over `iters` launches on the plan's stream. */
+ * averaged over `iters` launches on the plan's stream, in the peaks-only form of a call (the
+ * eigenvalues not requested: complex double then finds only the M signal eigenvalues). */
 int32_t rsp_music_profile(rsp_music_plan* plan, const void* d_X, int32_t n_inst, int32_t iters, float* ms_out);
 int32_t rsp_music_device_alloc(rsp_music_plan* plan, int64_t bytes, void** d_ptr);
 int32_t rsp_music_device_free(rsp_music_plan* plan, void* d_ptr);

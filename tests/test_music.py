@@ -191,6 +191,24 @@ def test_music_host_path_equals_device_path(music_case):
 
 
 @pytest.mark.gpu
+def test_music_peaks_only_call_equals_full_call(music_case):
+    """Without the eigenvalues requested (the bench's step), complex double finds only the M signal
+    eigenvalues; the peaks and their count are those of the call that returns every output."""
+    c = music_case
+    n = c['n']
+    peaks = np.zeros((n, c['M']), np.int32)
+    npk = np.zeros(n, np.int32)
+    d_X = c['plan'].device_alloc(n)
+    try:
+        c['plan'].synthesize_device(d_X, c['scene'], n, inst0=0, seed=SEED)
+        c['plan'].peaks_device(d_X, n, peaks, npk)
+    finally:
+        c['plan'].device_free(d_X)
+    assert np.array_equal(peaks, c['out']['peaks'])
+    assert np.array_equal(npk, c['out']['n_peaks'])
+
+
+@pytest.mark.gpu
 def test_music_decoupled_covariance_eigenvalues():
     """A covariance whose tridiagonal form is decoupled (every off-diagonal exactly zero): X with
     one snapshot per channel gives R = diag(|a_n|^2 / K), and the Householder steps are all the
