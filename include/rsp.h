@@ -159,6 +159,11 @@ const char* rsp_last_error(void);
 /* Plan options (rsp_plan_options_default fills the defaults shown). */
 #define RSP_PLAN_K1_TILED 1   /* force the one-tile-per-workgroup K1 instead of the persistent
                                  one (both compute the same operations; parity tests compare them) */
+#define RSP_PLAN_MONOPULSE_COMPLEX 2   /* S9's angle from the complex ratio
+                                 real((S_A - S_B) / (S_A + S_B + eps)) of the RD map, as the inline S9
+                                 of main_plot_snr_vs_angle_error.m:455-462, instead of fsf:282-290's
+                                 amplitude ratio (|S_A| - |S_B|) / (|S_A| + |S_B| + eps).  K2 then
+                                 writes every frame's complex RD map (the caller's, or plan-owned) */
 typedef struct rsp_plan_options {
     int32_t device;              /* HIP device ordinal (0)                                   */
     int32_t frames_per_launch;   /* frames batched into each kernel launch by the queue (1)  */

@@ -160,8 +160,10 @@ def _spline_peak(cells, data, step):
     return q[int(np.argmax(val))]
 
 
-def parameter_estimation(dets, S_all, rdm, pre):
-    """S9, fun_parameter_estimation_9 (fsf:226-299)."""
+def parameter_estimation(dets, S_all, rdm, pre, monopulse='amplitude'):
+    """S9, fun_parameter_estimation_9 (fsf:226-299).  monopulse='complex': the angle from
+    real((S_A - S_B) / (S_A + S_B + eps)) of the complex map, as the inline S9 of
+    main_plot_snr_vs_angle_error.m:455-462 does, instead of fsf:282-290's amplitude ratio."""
     out = []
     if dets.shape[0] == 0:
         return out
@@ -178,9 +180,13 @@ def parameter_estimation(dets, S_all, rdm, pre):
         vc = vc[(vc >= 1) & (vc <= P)]
         vmax = v if len(vc) < 3 else _spline_peak(vc, S[vc - 1, r - 1], 1.0 / vI)
         est_v = pre['velocity_axis'][v - 1] + (vmax - v) * pre['deltaV']    # fsf:278
-        SA = abs(rdm[v - 1, r - 1, p - 1])                                  # fsf:282-283
-        SB = abs(rdm[v - 1, r - 1, p])
-        ratio = (SA - SB) / (SA + SB + EPS)
+        if monopulse == 'complex':                                          # mpsae:455-458
+            SA, SB = rdm[v - 1, r - 1, p - 1], rdm[v - 1, r - 1, p]
+            ratio = ((SA - SB) / (SA + SB + EPS)).real
+        else:
+            SA = abs(rdm[v - 1, r - 1, p - 1])                              # fsf:282-283
+            SB = abs(rdm[v - 1, r - 1, p])
+            ratio = (SA - SB) / (SA + SB + EPS)
         ang = (pre['beam_angles_deg'][p - 1] + pre['beam_angles_deg'][p]) / 2 \
             + pre['k_slopes_LUT'][p - 1] * ratio                             # fsf:285-290
         out.append({'Range': est_r, 'Velocity': est_v, 'Angle': ang, 'Power': power,
@@ -243,13 +249,13 @@ def cluster_stage2(tg, cp):
     return out
 
 
-def process_cube(raw_noisy, config, cfar, cluster, pre, keep=False):
+def process_cube(raw_noisy, config, cfar, cluster, pre, keep=False, monopulse='amplitude'):
     """S5..S11 of fsf on a given noisy cube raw[m, n, c]; returns final targets (+ stages)."""
     iq = dbf(raw_noisy, pre['DBF_coeffs_data_C'])
     pc = pulse_compress(iq, pre)
     rdm = mtd(pc, pre)
     dets, S_all = goca_cfar(rdm, cfar)
-    par = parameter_estimation(dets, S_all, rdm, pre)
+    par = parameter_estimation(dets, S_all, rdm, pre, monopulse)
     st1 = cluster_stage1(par, cluster)
     fin = cluster_stage2(st1, cluster)
     if keep:

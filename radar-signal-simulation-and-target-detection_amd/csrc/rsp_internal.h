@@ -115,6 +115,7 @@ struct Geometry {
     int max_dets;    // detection-list capacity per frame of the launch (grows on demand, rsp_plan.cpp)
     int ncu;         // compute units of the device (persistent K1 grid)
     int k1_tiled;    // force the one-tile-per-workgroup K1 (RSP_PLAN_K1_TILED, parity tests)
+    int mono_c;      // S9 angle from the complex ratio of the RD map (RSP_PLAN_MONOPULSE_COMPLEX)
     // used fast-time samples as <= RSP_MAX_IVL intervals: compacted n' in [ivl_start[q],
     // ivl_start[q+1]) is sample ivl_lo[q] + n' - ivl_start[q] (kernel-argument lookup, no
     // dependent global load before the cube loads)

@@ -1542,9 +1542,11 @@ struct S9Consts {
 
 // S9 of one detection from the workgroup's S tile (fsf:237-290).
 // sval(v, r) = S at Doppler row v, range cell r (the tile, or the maps when the tile lacks it).
+// RA / RB (RSP_PLAN_MONOPULSE_COMPLEX, else null): the complex RD map rows of beams pair, pair + 1.
 template <class T, class SF>
 __device__ __forceinline__ void s9_estimate(const S9Consts& k, SF sval, int P, int G, int Gp, int v, int r, int pair,
-                                            const T* __restrict__ MA, const T* __restrict__ MB, DevDet* out) {
+                                            const T* __restrict__ MA, const T* __restrict__ MB,
+                                            const cx<T>* __restrict__ RA, const cx<T>* __restrict__ RB, DevDet* out) {
     // the 5-cell windows clipped to the map (fsf:241-250): cells first .. first + n - 1
     const int rfirst = max(r - 2, 0), nrc = min(r + 2, G - 1) - rfirst + 1;
     const int vfirst = max(v - 2, 0), nvc = min(v + 2, P - 1) - vfirst + 1;
@@ -1556,10 +1558,17 @@ __device__ __forceinline__ void s9_estimate(const S9Consts& k, SF sval, int P, i
     }
     const double rmax = (nrc < 3) ? (double)r : rfirst + spline_peak<8>(yr, nrc);
     const double vmax = (nvc < 3) ? (double)v : vfirst + spline_peak<4>(yv, nvc);
-    // amplitude monopulse on the integer cell (fsf:282-290)
-    const double SA = (double)MA[(size_t)v * Gp + r];
-    const double SB = (double)MB[(size_t)v * Gp + r];
-    const double ratio = (SA - SB) / (SA + SB + 2.220446049250313e-16);
+    double ratio;
+    if (RA) {   // complex ratio real((S_A - S_B) / (S_A + S_B + eps)) (main_plot_snr_vs_angle_error.m:455-462)
+        const cx<T> a = RA[(size_t)v * G + r], b = RB[(size_t)v * G + r];
+        const double nx = (double)a.x - (double)b.x, ny = (double)a.y - (double)b.y;
+        const double dx = (double)a.x + (double)b.x + 2.220446049250313e-16, dy = (double)a.y + (double)b.y;
+        ratio = (nx * dx + ny * dy) / (dx * dx + dy * dy);
+    } else {    // amplitude monopulse on the integer cell (fsf:282-290)
+        const double SA = (double)MA[(size_t)v * Gp + r];
+        const double SB = (double)MB[(size_t)v * Gp + r];
+        ratio = (SA - SB) / (SA + SB + 2.220446049250313e-16);
+    }
     DevDet d;
     d.v_idx = v + 1;
     d.r_idx = r + 1;
@@ -1649,6 +1658,8 @@ __global__ __launch_bounds__(RSP_THREADS, RSP_K3_WGS) void k3_cfar(Geometry g, D
     const int Gp = g.Gp;
     const T* __restrict__ MA = static_cast<const T*>(fp.mag[f]) + (size_t)pair * P * Gp;   // |RDM| of beams pair, pair+1
     const T* __restrict__ MB = MA + (size_t)P * Gp;
+    const cx<T>* __restrict__ RA = g.mono_c ? static_cast<const cx<T>*>(fp.rdm[f]) + (size_t)pair * P * G : nullptr;
+    const cx<T>* __restrict__ RB = RA ? RA + (size_t)P * G : nullptr;
     // S(v, r) from the maps: the same two values and the same add as the tile load below
     auto sg = [&](int vv, int rr) -> T {
         const size_t o = (size_t)vv * Gp + rr;
@@ -1931,7 +1942,7 @@ __global__ __launch_bounds__(RSP_THREADS, RSP_K3_WGS) void k3_cfar(Geometry g, D
         if (idx >= g.max_dets) break;   // counted; the host grows the list and runs K3 again
         const int e = queue[i];
         const int v = e >> 16, c = e & 0xFFFF;
-        s9_estimate<T>(s9c, st, P, G, Gp, v, c0 + c, pair, MA, MB, &fp.dets[f][idx]);
+        s9_estimate<T>(s9c, st, P, G, Gp, v, c0 + c, pair, MA, MB, RA, RB, &fp.dets[f][idx]);
     }
     if (nhit <= K3_QCAP) return;   // uniform
     // Overflow pass (more than K3_QCAP hits in this tile: a cluttered frame or a low T_CFAR).  The
@@ -1971,7 +1982,7 @@ __global__ __launch_bounds__(RSP_THREADS, RSP_K3_WGS) void k3_cfar(Geometry g, D
         }
         if (st(v, r) > (T)Tc * noise2(lr, tr, lv, tv)) {
             const int idx = atomicAdd(fp.count[f], 1);
-            if (idx < g.max_dets) s9_estimate<T>(s9c, st, P, G, Gp, v, r, pair, MA, MB, &fp.dets[f][idx]);
+            if (idx < g.max_dets) s9_estimate<T>(s9c, st, P, G, Gp, v, r, pair, MA, MB, RA, RB, &fp.dets[f][idx]);
         }
     }
 }

@@ -460,7 +460,8 @@ int setup_lane(rsp_plan* p, Lane& L) {
     for (auto& e : L.tev) HIPCHK(hipEventCreate(&e));
     int rc;
     if ((rc = p->dalloc_bytes(&L.z, p->z_elems * p->F * p->esz))) return rc;
-    if ((rc = p->dalloc_bytes(&L.rdm, p->rdm_elems * p->esz))) return rc;   // one frame (sync paths)
+    // one frame (sync paths); F frames when S9 reads the complex map (RSP_PLAN_MONOPULSE_COMPLEX)
+    if ((rc = p->dalloc_bytes(&L.rdm, p->rdm_elems * p->esz * (p->g.mono_c ? p->F : 1)))) return rc;
     if ((rc = p->dalloc_bytes(&L.mag, p->mag_elems * p->F * p->rsz))) return rc;
     if ((rc = lane_dets_alloc(p, L, std::min(p->det_bound, 4096)))) return rc;
     return lane_host_alloc(p, L, std::min(p->det_bound, 1024));
@@ -471,13 +472,14 @@ int setup_lane(rsp_plan* p, Lane& L) {
 // rdm_13beam is an intermediate, so the throughput queue does not write it to HBM (-10% k2_pc)
 // unless the caller hands a map for the frame (rsp_enqueue_device_rdm).  rdm == nullptr: no
 // frame writes its map.  The synchronous paths (rsp_process_* with out->rdm, process_stage2)
-// run one frame into the lane's own map L.rdm.
+// run one frame into the lane's own map L.rdm.  With RSP_PLAN_MONOPULSE_COMPLEX K3's S9 reads
+// the complex map, so every frame writes one: the caller's, or the lane's own (F frames).
 FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const void* const* in, int nf, void* const* rdm) {
     FramePtrs fp{};
     for (int f = 0; f < nf; ++f) {
         fp.in[f] = in[f];
         fp.z[f] = (char*)L.z + p->z_elems * p->esz * f;
-        fp.rdm[f] = rdm ? rdm[f] : nullptr;
+        fp.rdm[f] = rdm && rdm[f] ? rdm[f] : (p->g.mono_c ? (char*)L.rdm + p->rdm_elems * p->esz * f : nullptr);
         fp.mag[f] = (char*)L.mag + p->mag_elems * p->rsz * f;
         DevDet* rec = L.dets + (size_t)(L.dcap + 1) * f;
         fp.count[f] = reinterpret_cast<int*>(rec);   // zeroed by K1, bumped by K3
@@ -804,7 +806,8 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
     const int device = opt->device, frames_per_launch = opt->frames_per_launch;
     if (opt->precision != RSP_C64 && opt->precision != RSP_C128)
         return fail(RSP_ERR_INVALID, "precision must be RSP_C128 or RSP_C64, got %d", opt->precision);
-    if (opt->flags & ~RSP_PLAN_K1_TILED) return fail(RSP_ERR_INVALID, "unknown plan flags 0x%x", opt->flags);
+    if (opt->flags & ~(RSP_PLAN_K1_TILED | RSP_PLAN_MONOPULSE_COMPLEX))
+        return fail(RSP_ERR_INVALID, "unknown plan flags 0x%x", opt->flags);
     const int C = cfg->channel_num, B = cfg->beam_num, P = cfg->prtNum, N = cfg->point_PRT;
     const int g1 = pre->N_gate_narrow, g2 = pre->N_gate_medium, g3 = pre->N_gate_long, G = pre->N_total_gate;
     if (C < 1 || C > 32 || B < 1 || B > 16 || P < 2 || N < 2)
@@ -837,6 +840,7 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
     Geometry& g = p->g;
     g.prec = f64 ? RSP_PREC_F64 : RSP_PREC_F32;
     g.k1_tiled = (opt->flags & RSP_PLAN_K1_TILED) ? 1 : 0;
+    g.mono_c = (opt->flags & RSP_PLAN_MONOPULSE_COMPLEX) ? 1 : 0;
     g.C = C; g.B = B; g.P = P; g.N = N; g.G = G;
     g.cpitch = N * P;
     g.refR = cfar->refCells_R; g.guardR = cfar->guardCells_R; g.refV = cfar->refCells_V; g.guardV = cfar->guardCells_V;

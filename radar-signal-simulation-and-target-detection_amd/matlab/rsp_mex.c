@@ -20,7 +20,8 @@
  *   rsp_mex('clear')      -- destroys the cached plans.
  *
  * opts (optional struct): seed (20250101), device (0), precision ('double' (default) | 'single'),
- * frames_per_launch (1), gate_cols.
+ * frames_per_launch (1), gate_cols, monopulse ('amplitude' (default, fsf:282-290) | 'complex': the
+ * complex ratio of main_plot_snr_vs_angle_error.m:455-462, RSP_PLAN_MONOPULSE_COMPLEX).
  * The plan is cached between calls and rebuilt whenever the converted inputs differ from the
  * ones it was built from (every scalar field and the contents of every array are compared), so
  * a driver that changes config / cfar_params / cluster_params / precomputed_data between
@@ -190,6 +191,12 @@ static void read_opts(const mxArray* o, rsp_plan_options* opt, uint64_t* seed, i
         mxGetString(mxGetField(o, 0, "precision"), s, sizeof s);
         if (!strcmp(s, "single")) opt->precision = RSP_C64;
         else if (strcmp(s, "double")) mexErrMsgIdAndTxt("radar:rsp", "opts.precision must be 'double' or 'single'");
+    }
+    if (mxGetField(o, 0, "monopulse")) {
+        char s[16];
+        mxGetString(mxGetField(o, 0, "monopulse"), s, sizeof s);
+        if (!strcmp(s, "complex")) opt->flags |= RSP_PLAN_MONOPULSE_COMPLEX;
+        else if (strcmp(s, "amplitude")) mexErrMsgIdAndTxt("radar:rsp", "opts.monopulse must be 'amplitude' or 'complex'");
     }
     if (mxGetField(o, 0, "gate_cols")) {   /* 3 x 2: [first last] per segment, 1-based */
         const mxArray* g = mxGetField(o, 0, "gate_cols");

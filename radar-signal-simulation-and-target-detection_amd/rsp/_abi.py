@@ -72,6 +72,7 @@ class Sizes(ct.Structure):
 
 
 RSP_PLAN_K1_TILED = 1
+RSP_PLAN_MONOPULSE_COMPLEX = 2
 
 
 class PlanOptions(ct.Structure):

@@ -33,10 +33,13 @@ class Plan:
     ``precision``: 'c128' (complex double, MATLAB's arithmetic; default) or 'c64'.
     ``k1_tiled``: force the one-tile-per-workgroup K1 (parity tests compare it with the
     persistent K1 the plan otherwise picks).
+    ``monopulse``: 'amplitude' (fsf:282-290, the default) or 'complex' -- S9's angle from
+    real((S_A - S_B) / (S_A + S_B + eps)) of the complex map, the estimator of the inline S9 in
+    main_plot_snr_vs_angle_error.m:455-462 (RSP_PLAN_MONOPULSE_COMPLEX).
     """
 
     def __init__(self, config, cfar_params, cluster_params, precomputed_data, device=0, frames_per_launch=1,
-                 precision='c128', k1_tiled=False):
+                 precision='c128', k1_tiled=False, monopulse='amplitude'):
         sc = config['Sig_Config']
         pre = precomputed_data
         self.config = config
@@ -80,7 +83,11 @@ class Plan:
         check(lib().rsp_plan_options_default(ct.byref(opt)))
         opt.device, opt.frames_per_launch = int(device), int(frames_per_launch)
         opt.precision = _abi.RSP_C128 if precision == 'c128' else _abi.RSP_C64
-        opt.flags = _abi.RSP_PLAN_K1_TILED if k1_tiled else 0
+        if monopulse not in ('amplitude', 'complex'):
+            raise ValueError("monopulse must be 'amplitude' (fsf:282-290) or 'complex' "
+                             "(main_plot_snr_vs_angle_error.m:455-462), got %r" % (monopulse,))
+        opt.flags = (_abi.RSP_PLAN_K1_TILED if k1_tiled else 0) | \
+            (_abi.RSP_PLAN_MONOPULSE_COMPLEX if monopulse == 'complex' else 0)
         h = ct.c_void_p()
         check(lib().rsp_plan_create_ex(ct.byref(self.cfg), ct.byref(self.cfar), ct.byref(self.cluster),
                                        ct.byref(self.pre), ct.byref(opt), ct.byref(h)))

@@ -8,10 +8,11 @@ trials each under parfor with fresh MATLAB randn noise (:167-211), records final
 
 Here every trial is rsp_process_targets on the device (complex double): S4 synthesis + S4.1
 Philox noise with seed 20250101 + 1000 * i_snr + trial (MATLAB randn is irreproducible), then
-S5-S11.  What is checked is the per-frame kernel's estimator -- S9's AMPLITUDE monopulse on the
-integer cell, (|A| - |B|) / (|A| + |B| + eps) (fsf:280-290) -- and not the script's own inline
-copy of S9, which uses the complex ratio real((A - B) / (A + B)) (main_plot_snr_vs_angle_error.m:
-455-458): this build replaces fun_process_single_frame, so its statistics are the kernel's.
+S5-S11.  test_snr_vs_angle_error checks the per-frame kernel's estimator -- S9's AMPLITUDE
+monopulse on the integer cell, (|A| - |B|) / (|A| + |B| + eps) (fsf:280-290);
+test_snr_vs_angle_error_script_estimator runs the script's own inline copy of S9, which uses the
+complex ratio real((A - B) / (A + B + eps)) (main_plot_snr_vs_angle_error.m:455-462), through the
+plan option monopulse='complex' on a shorter sweep.
 
 Checks:
   * oracle on the same seeds: at -4, 4, 12 and 24 dB the first 8 trials' noisy cubes (downloaded
@@ -62,18 +63,19 @@ ORACLE_SNRS = (-4, 4, 12, 24)
 ORACLE_TRIALS = 8
 
 
-def _oracle_worker(path):
+def _oracle_worker(job):
     """One oracle trial on a downloaded device cube (a worker process: no GPU use)."""
+    path, monopulse = job
     from threadpoolctl import threadpool_limits
     from _scen import scenario as sc_
     from oracle import chain as ch
     s = sc_('reference')
     cube = np.load(path)
     with threadpool_limits(2):   # 8 workers x 2 BLAS threads: the box's 16-core share
-        return ch.process_cube(cube, s['cfg'], s['cfar'], s['clus'], s['pre_o'])
+        return ch.process_cube(cube, s['cfg'], s['cfar'], s['clus'], s['pre_o'], monopulse=monopulse)
 
 
-def _oracle_trials(plan, todo, tmpdir, workers=8):
+def _oracle_trials(plan, todo, tmpdir, workers=8, monopulse='amplitude'):
     """{(snr, trial): oracle final targets} on the device's own noisy cubes, `workers` at a time."""
     import multiprocessing as mp
     out = {}
@@ -87,7 +89,7 @@ def _oracle_trials(plan, todo, tmpdir, workers=8):
                 pth = os.path.join(tmpdir, 'cube_%d_%d.npy' % (snr + 100, t))
                 np.save(pth, cube)
                 paths.append(pth)
-            for key, fo, pth in zip(chunk, pool.map(_oracle_worker, paths), paths):
+            for key, fo, pth in zip(chunk, pool.map(_oracle_worker, [(q, monopulse) for q in paths]), paths):
                 out[key] = fo
                 os.remove(pth)
     return out
@@ -165,3 +167,53 @@ def test_snr_vs_angle_error(tmp_path):
     for a, b in zip(table, table[1:]):
         assert b['pd'] >= a['pd'] - 0.1, (a, b)
     assert by[30]['pd'] == 1.0
+
+
+def test_snr_vs_angle_error_script_estimator(tmp_path):
+    """The script's own estimator: its inline S9 takes the angle from the complex ratio
+    real((S_A - S_B) / (S_A + S_B + eps)) (main_plot_snr_vs_angle_error.m:455-462), which the plan
+    runs with monopulse='complex' (RSP_PLAN_MONOPULSE_COMPLEX).  A shorter sweep than the script's
+    (4 SNRs x 32 trials): every one of the first 4 trials per SNR equals the oracle's complex-ratio
+    chain on the same cube, Pd = 1 from 0 dB up, and the angle-error std stays below the script's
+    curve |k| sqrt(2) / sqrt(SNR) wherever Pd >= 0.9."""
+    s = scenario('reference')
+    plan = Plan(s['cfg'], s['cfar'], s['clus'], s['pre_p'], monopulse='complex')
+    snrs, trials, n_orc = (-4, 4, 12, 24), 32, 4
+    table, dev = [], {}
+    try:
+        for snr in snrs:
+            i = SNRS.index(snr)
+            tg = [dict(TRUE, SNR_dB=float(snr))]
+            errs, n_det = [], 0
+            for t in range(trials):
+                fin = plan.process_targets(tg, frame_idx=1, seed=_seed(i, t))['final_targets']
+                if t < n_orc:
+                    dev[(snr, t)] = fin
+                if fin:
+                    n_det += 1
+                    errs.append(fin[0]['Angle'] - TRUE['ElevationAngle'])
+            table.append(dict(snr_db=snr, pd=n_det / trials, n_detected=len(errs),
+                              angle_err_std=float(np.std(errs, ddof=1)) if len(errs) > 1 else float('nan'),
+                              angle_err_mean=float(np.mean(errs)) if errs else float('nan'),
+                              theory=abs(K_PAIR5) * np.sqrt(2) / np.sqrt(10 ** (snr / 10))))
+        orc = _oracle_trials(plan, sorted(dev), str(tmp_path), workers=8, monopulse='complex')
+        for key, fin in sorted(dev.items()):
+            fo = orc[key]
+            assert len(fo) == len(fin), key
+            for a, b in zip(fo, fin):
+                for f in ('Range', 'Velocity', 'Angle', 'Power'):
+                    assert b[f] == pytest.approx(a[f], rel=1e-9, abs=1e-9), (key, f)
+    finally:
+        plan.close()
+    print()
+    for r in table:
+        print('complex ratio: SNR %+3d dB  Pd %.2f  std %.4f deg  (curve %.4f)  mean %+.4f' % (
+            r['snr_db'], r['pd'], r['angle_err_std'], r['theory'], r['angle_err_mean']))
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'gpurun_out')
+    if os.path.isdir(out):
+        json.dump(table, open(os.path.join(out, 'montecarlo_complex.json'), 'w'), indent=1)
+    for r in table:
+        if r['snr_db'] >= 0:
+            assert r['pd'] == 1.0, r
+        if r['pd'] >= 0.9:
+            assert r['angle_err_std'] < r['theory'], r
