@@ -780,8 +780,11 @@ __global__ __launch_bounds__(MU_THREADS, 2) void k_music_cov64(int N, int K, con
 #endif
 #define ME_VW 68                         // padded length of a v / w buffer
 #define ME_PX(j) ((j) + ((j) >> 4))      // row j's slot in it
+// the inverse iteration's [5][64][M] LU / y array; the back-transform stages a wave's 16
+// reflectors ([16][ME_VW] complex) in the same space once the vectors have left it
+__host__ __device__ constexpr int me_lu_doubles(int M) { return 5 * 64 * M > 32 * ME_VW ? 5 * 64 * M : 32 * ME_VW; }
 __host__ __device__ constexpr size_t me_lds_bytes(int M, int S) {
-    return (size_t)4 * ME_VW * 16 + 64 * 16 + 8 * 16 + 3 * 68 * 8 + 64 * 8 + (size_t)5 * 64 * M * 8 + (size_t)M * 64 * 16 +
+    return (size_t)4 * ME_VW * 16 + 64 * 16 + 8 * 16 + 3 * 68 * 8 + 64 * 8 + (size_t)me_lu_doubles(M) * 8 + (size_t)M * 64 * 16 +
            ((size_t)S + 8) * 8 + 8 * 16;
 }
 
@@ -806,7 +809,7 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
     double* e2 = ee + 68;                // beta_k^2 (+ pad)
     double* lam = e2 + 68;               // ascending eigenvalues
     double* lu = lam + 64;               // [5][64][M]: U diag, U super 1, U super 2, mult, y
-    double2* Qs = reinterpret_cast<double2*>(lu + 5 * 64 * M);   // [M][64]
+    double2* Qs = reinterpret_cast<double2*>(lu + me_lu_doubles(M));   // [M][64]
     double* den = reinterpret_cast<double*>(Qs + M * 64);        // [S]
     int* ired = reinterpret_cast<int*>(den + S + 8);             // [8] + the peak selection
     double* dred = den + S;                                      // [8]
@@ -1026,28 +1029,40 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
             const double lj = lam[n - 1 - lane];
             double ak = dd[0] - lj;
             double bk = n > 1 ? ee[0] : 0.0;
-            for (int k = 0; k < n - 1; ++k) {
-                const double ck = ee[k];
-                const double an = dd[k + 1] - lj;
-                const double bn = k < n - 2 ? ee[k + 1] : 0.0;
-                if (fabs(ak) >= fabs(ck)) {
-                    const double a0 = fabs(ak) < ptol ? copysign(ptol, ak) : ak;
-                    const double mult = ck / a0;
-                    LU(0, k) = 1.0 / a0; LU(1, k) = bk; LU(2, k) = 0.0; LU(3, k) = mult;
-                    ak = an - mult * bk;
-                    bk = bn;
-                } else {
-                    swp |= 1ull << k;
-                    const double mult = ak / ck;
-                    LU(0, k) = 1.0 / ck; LU(1, k) = an; LU(2, k) = bn; LU(3, k) = mult;
-                    ak = bk - mult * an;
-                    bk = -mult * bn;
+            for (int k0 = 0; k0 < n - 1; k0 += 4) {   // 4 rows of T per LDS round trip
+                double ckv[4], anv[4], bnv[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int k = min(k0 + j, n - 2);
+                    ckv[j] = ee[k];
+                    anv[j] = dd[k + 1] - lj;
+                    bnv[j] = k < n - 2 ? ee[k + 1] : 0.0;
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int k = k0 + j;
+                    if (k < n - 1) {   // branch-free over the lanes' interchange choices, one division
+                        const double ck = ckv[j], an = anv[j], bn = bnv[j];
+                        const bool keep = fabs(ak) >= fabs(ck);
+                        const double a0 = fabs(ak) < ptol ? copysign(ptol, ak) : ak;
+                        const double r0 = 1.0 / (keep ? a0 : ck);
+                        const double mult = (keep ? ck : ak) * r0;
+                        LU(0, k) = r0;
+                        LU(1, k) = keep ? bk : an;
+                        LU(2, k) = keep ? 0.0 : bn;
+                        LU(3, k) = mult;
+                        if (!keep) swp |= 1ull << k;
+                        const double akn = keep ? an - mult * bk : bk - mult * an;
+                        bk = keep ? bn : -mult * bn;
+                        ak = akn;
+                    }
                 }
             }
             LU(0, n - 1) = 1.0 / (fabs(ak) < ptol ? copysign(ptol, ak) : ak);   // U's diagonal stored inverted:
                                                                                    // the solves multiply
             for (int r = 0; r < n; ++r) LU(4, r) = 1.0 + 0.0625 * (double)((r * 37 + lane * 11) % 17);   // start
         }
+        ME_STAMP(7);   // diagnostic builds: the end of dlagtf (printed apart)
         for (int it = 0; it < MU_ITER; ++it) {
             if (lane < M) {   // dlagts, 4 rows at a time: the rows' LDS loads issue ahead of the chain
                 double yk = LU(4, 0);
@@ -1122,13 +1137,17 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
             double2 y[M];
 #pragma unroll
             for (int j = 0; j < M; ++j) y[j] = Qs[j * 64 + lane];
-            for (int k = min(n - 2, 16 * wv + 15); k >= 16 * wv; --k) {
-                if (i == k) {
+            // the wave's reflectors (its 16 columns, quad i holds v_i) into LDS at once, so the
+            // loop below only reads them (lu is dead: the vectors are in Qs)
+            double2* blk = reinterpret_cast<double2*>(lu);   // [16][ME_VW]
+            const int klast = min(n - 2, 16 * wv + 15);
+            if (i <= klast) {
 #pragma unroll
-                    for (int u = 0; u < 16; ++u) vb[ME_PX(16 * q + u)] = a[u];
-                }
-                wsync();
-                const double2 vl = vb[ME_PX(lane)], tau = taus[k];
+                for (int u = 0; u < 16; ++u) blk[(i - 16 * wv) * ME_VW + ME_PX(16 * q + u)] = a[u];
+            }
+            wsync();
+            for (int k = klast; k >= 16 * wv; --k) {
+                const double2 vl = blk[(k - 16 * wv) * ME_VW + ME_PX(lane)], tau = taus[k];
 #pragma unroll
                 for (int j = 0; j < M; ++j) {
                     double2 d = zmc(vl, y[j]);   // v^H y
@@ -1136,7 +1155,6 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
                     d.y = wsumd(d.y);
                     y[j] = zsub(y[j], zm(vl, zm(tau, d)));
                 }
-                wsync();
             }
 #pragma unroll
             for (int j = 0; j < M; ++j) Qs[j * 64 + lane] = y[j];
@@ -1564,9 +1582,11 @@ int32_t rsp_music_profile(rsp_music_plan* p, const void* d_X, int32_t n_inst, in
         double ph[6] = {0, 0, 0, 0, 0, 0};
         for (int i = 0; i < n_inst; ++i)
             for (int q = 0; q < 6; ++q) ph[q] += (double)(t[(size_t)i * 8 + q + 1] - t[(size_t)i * 8 + q]) * 0.01 / n_inst;
-        fprintf(stderr, "k_music_eig%s phases (us/instance): tridiag %.2f eigenvalues %.2f inviter %.2f backxf %.2f spectrum %.2f peaks %.2f\n",
+        double tf = 0;   // stamp 7 (complex double): dlagtf's end, inside the inverse-iteration phase
+        for (int i = 0; i < n_inst && p->f64; ++i) tf += (double)(t[(size_t)i * 8 + 7] - t[(size_t)i * 8 + 2]) * 0.01 / n_inst;
+        fprintf(stderr, "k_music_eig%s phases (us/instance): tridiag %.2f eigenvalues %.2f inviter %.2f (dlagtf %.2f) backxf %.2f spectrum %.2f peaks %.2f\n",
                 p->f64 ? "64" : "",
-                ph[0], ph[1], ph[2], ph[3], ph[4], ph[5]);
+                ph[0], ph[1], ph[2], tf, ph[3], ph[4], ph[5]);
     }
     return RSP_OK;
 }
