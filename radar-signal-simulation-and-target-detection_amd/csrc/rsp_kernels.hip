@@ -988,13 +988,18 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
         }
     };
     const int lgNT = ilog2(NT), half = P >> 1;
+    // EARLY (P <= 128): the next tile's loads go out as soon as this wave's DBF has read xv, before
+    // the tile barrier (x2: K1 -0.6 %, bench +0.6 %); at P = 256 the xv registers live across the
+    // Stockham passes and K1 takes 36 % longer, so there they go out after the barrier
+    constexpr bool EARLY = LGP <= 7;
     issue(TT);
     dbf(Y);
+    if (EARLY && TT + (int)gridDim.x < total) issue(TT + gridDim.x);
     __syncthreads();
     int cur = 0;
     for (; TT < total; TT += gridDim.x) {
         const int Tn = TT + gridDim.x;
-        if (Tn < total) issue(Tn);   // next tile's loads fly during this tile's FFT + z stores
+        if (!EARLY && Tn < total) issue(Tn);   // next tile's loads fly during this tile's FFT + z stores
         const int f = __builtin_amdgcn_readfirstlane(TT / g.ntiles), tile = TT - f * g.ntiles;
         if (tile == 0 && threadIdx.x == 0 && fp.count[f]) *fp.count[f] = 0;   // K3's detection counter
         V* __restrict__ z = static_cast<V*>(fp.z[f]);
@@ -1008,7 +1013,10 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
         else
             fft_passes<LGP, k1p_pts<T>(), K1_SH, K1_THREADS, false>(Y + cur * bufsz, Ppad, B * NT, twl,
                                                                      StoreLds<V>{Y + cur * bufsz}, sz);
-        if (Tn < total) dbf(Y + (cur ^ 1) * bufsz);
+        if (Tn < total) {
+            dbf(Y + (cur ^ 1) * bufsz);
+            if (EARLY && Tn + (int)gridDim.x < total) issue(Tn + gridDim.x);
+        }
         __syncthreads();
         cur ^= 1;
     }
