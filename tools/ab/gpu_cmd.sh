@@ -1,9 +1,5 @@
 set -o pipefail
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-timeout -k 10 400 python3 tools/ab/ab_pytest.py exp/ab/librsp_msect.so tests/test_music.py -x -q -m gpu -p no:cacheprovider 2>&1 | tail -2 || exit 1
-RSP_MUSIC_TRACE=1 AB_LIB=exp/ab/librsp_mtrace.so timeout -k 10 120 python3 tools/music_prof.py 1024 5 c128 2>&1 | cut -c1-300 || exit 1
-for r in 1 2 3; do for v in base msect; do
-  if [ $v = base ]; then lib=""; else lib=exp/ab/librsp_$v.so; fi
-  echo "$r $v $(AB_LIB=$lib timeout -k 10 120 python3 tools/music_prof.py 1024 20 c128 | cut -c1-120)" || exit 1
-done; done
+mkdir -p gpurun_out; rm -f gpurun_out/ab_bench.log
+bash tools/ab/ab_bench.sh "--steps 300" lanes4 lanes2 || exit 1
+for r in 1 2; do for f in 8 4; do echo "$r fpl $f $(timeout -k 10 200 python3 bench.py --steps 300 --fpl $f --no-cpu-baseline | cut -c100-200)" || exit 1; done; done
