@@ -953,22 +953,25 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
     const unsigned cube_bytes = (unsigned)((size_t)C * NPc * sizeof(V));
     typename D::Ld xv[TPW][NJ];
     bool vld[TPW];   // wave-uniform: sub-tile u of the tile in flight lies inside the used samples
-    auto issue = [&](int Tn) {   // cube loads of tile Tn (fsf:93 operands) into xv
+    auto issue_u = [&](int Tn, int u) {   // cube loads of sub-tile u of tile Tn (fsf:93 operands) into xv[u]
         const int f = __builtin_amdgcn_readfirstlane(Tn / g.ntiles), tile = Tn - f * g.ntiles;
         const __amdgpu_buffer_rsrc_t xr = buf_rsrc(fp.in[f], cube_bytes);
+        const int np = tile * NT + nlv[u];
+        vld[u] = nlv[u] >= 0 && np < g.nU;
+        if (vld[u]) {   // no else: zeroing xv here would wait (vmcnt) on the pending z stores
+            const int soff = used_sample(g, np) * P * (int)sizeof(V);
 #pragma unroll
-        for (int u = 0; u < TPW; ++u) {
-            const int np = tile * NT + nlv[u];
-            vld[u] = nlv[u] >= 0 && np < g.nU;
-            if (vld[u]) {   // no else: zeroing xv here would wait (vmcnt) on the pending z stores
-                const int soff = used_sample(g, np) * P * (int)sizeof(V);
-#pragma unroll
-                for (int j = 0; j < NJ; ++j)   // non-temporal: the cube is read exactly once
-                    xv[u][j] = D::bits(__builtin_amdgcn_raw_buffer_load_b128(xr, (int)loff[u][j], soff, 2));
-            }
+            for (int j = 0; j < NJ; ++j)   // non-temporal: the cube is read exactly once
+                xv[u][j] = D::bits(__builtin_amdgcn_raw_buffer_load_b128(xr, (int)loff[u][j], soff, 2));
         }
     };
-    auto dbf = [&](V* buf) {   // MFMA DBF + window of xv into buf (padded rows, K1_SH)
+    auto issue = [&](int Tn) {
+#pragma unroll
+        for (int u = 0; u < TPW; ++u) issue_u(Tn, u);
+    };
+    // Tnext >= 0 (EARLY2 below): sub-tile u of tile Tnext is loaded into xv[u] as soon as the
+    // DBF has read it
+    auto dbf = [&](V* buf, int Tnext) {   // MFMA DBF + window of xv into buf (padded rows, K1_SH)
         T* Yf = reinterpret_cast<T*>(buf);
 #pragma unroll
         for (int u = 0; u < TPW; ++u) {
@@ -984,6 +987,7 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
 #pragma unroll
                     for (int j = 0; j < NJ; ++j) D::mma(acc[mb], are[mb][j], aim[mb][j], xv[u][j]);
             }
+            if (Tnext >= 0) issue_u(Tnext, u);
             dbf_store<T, MB>(Yf, acc, grp, B, NT, Ppad, nlv[u], pv[u], wv_[u], K1_SH);
         }
     };
@@ -992,9 +996,13 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
     // the tile barrier (x2: K1 -0.6 %, bench +0.6 %); at P = 256 the xv registers live across the
     // Stockham passes and K1 takes 36 % longer, so there they go out after the barrier
     constexpr bool EARLY = LGP <= 7;
+    // EARLY2 (complex single): each sub-tile's loads of the next tile go out inside the DBF, right
+    // after the sub-tile's MFMAs have read xv[u] (c64 K1 158-163 -> 151 us; in complex double
+    // 226-227 -> 236-238, so double issues after the DBF)
+    constexpr bool EARLY2 = EARLY && sizeof(T) == 4;
     issue(TT);
-    dbf(Y);
-    if (EARLY && TT + (int)gridDim.x < total) issue(TT + gridDim.x);
+    dbf(Y, EARLY2 && TT + (int)gridDim.x < total ? TT + (int)gridDim.x : -1);
+    if (EARLY && !EARLY2 && TT + (int)gridDim.x < total) issue(TT + gridDim.x);
     __syncthreads();
     int cur = 0;
     for (; TT < total; TT += gridDim.x) {
@@ -1014,8 +1022,8 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
             fft_passes<LGP, k1p_pts<T>(), K1_SH, K1_THREADS, false>(Y + cur * bufsz, Ppad, B * NT, twl,
                                                                      StoreLds<V>{Y + cur * bufsz}, sz);
         if (Tn < total) {
-            dbf(Y + (cur ^ 1) * bufsz);
-            if (EARLY && Tn + (int)gridDim.x < total) issue(Tn + gridDim.x);
+            dbf(Y + (cur ^ 1) * bufsz, EARLY2 && Tn + (int)gridDim.x < total ? Tn + (int)gridDim.x : -1);
+            if (EARLY && !EARLY2 && Tn + (int)gridDim.x < total) issue(Tn + gridDim.x);
         }
         __syncthreads();
         cur ^= 1;
