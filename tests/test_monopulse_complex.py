@@ -86,3 +86,26 @@ def test_complex_ratio_queue_equals_sync():
         for a, b in zip(tg, want):
             for f in ('Range', 'Velocity', 'Angle', 'Power'):
                 assert a[f] == b[f], (r['frame_idx'], f)
+
+
+def test_complex_ratio_c64():
+    """Complex single: the complex-ratio angle of every detection the oracle also has (same
+    complex64-rounded cube) within the c64 tolerance of tests/test_gpu_parity.py (1e-3 deg)."""
+    s, cube = _frame('x2')
+    cube = cube.astype(np.complex64)
+    _, st = chain.process_cube(cube.astype(np.complex128), s['cfg'], s['cfar'], s['clus'], s['pre_o'], keep=True,
+                               monopulse='complex')
+    p = Plan(s['cfg'], s['cfar'], s['clus'], s['pre_p'], precision='c64', monopulse='complex')
+    try:
+        got = p.process_cube(cube, frame_idx=1)['detections']
+    finally:
+        p.close()
+    want = {(int(d[0]), int(d[1]), int(d[2])): e for d, e in zip(st['dets'], st['par'])}
+    n = 0
+    for d in got:
+        e = want.get((d['v_idx'], d['r_idx'], d['pair_idx']))
+        if e is None:
+            continue
+        n += 1
+        assert d['Angle'] == pytest.approx(e['Angle'], abs=1e-3)
+    assert n > 0.95 * len(want)
