@@ -1,4 +1,8 @@
 set -o pipefail
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-timeout -k 10 500 python -u -m pytest tests/test_monopulse_complex.py -x -v -m gpu --timeout 300 --timeout-method thread 2>&1 | grep -E "PASS|FAIL|Error|assert|passed|failed" | head -20
+o=gpurun_out/r04n
+mkdir -p $o
+timeout -k 10 300 python3 bench.py --frames-total 512 --no-cpu-baseline > $o/bench_config3.json 2> $o/bench_config3.err || exit 1
+timeout -k 10 300 python3 bench.py --gpus 2 --same-device --dist-backend gloo --steps 100 > $o/bench_2rank.json 2> $o/bench_2rank.err || exit 1
+timeout -k 10 300 python3 bench.py --e2e --steps 100 --no-cpu-baseline > $o/bench_e2e.json 2> $o/bench_e2e.err || exit 1
+for f in $o/bench*.json; do echo "$f $(cut -c1-220 $f)"; done
