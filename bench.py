@@ -102,7 +102,7 @@ def parse(argv=None):
 def launch_mode(gpus, env_world, visible, same_device, backend):
     """What `bench.py --gpus N` does: ('run', None) in this process (N = 1, or a torchrun rank whose
     WORLD_SIZE is N), ('spawn', None) to start N ranks, or ('error', message).  Pure: no GPU call;
-    `visible` = torch.cuda.device_count() (which does not initialise the GPU on this image)."""
+    `visible` = visible_gpus() (counted without the HIP runtime)."""
     if gpus < 1:
         return 'error', '--gpus must be >= 1, got %d' % gpus
     if env_world is not None:   # a rank started by torchrun / torch.distributed.run
@@ -120,6 +120,74 @@ def launch_mode(gpus, env_world, visible, same_device, backend):
         return 'error', '--gpus %d but only %d GPU(s) visible (rehearse on one GPU with --same-device ' \
                         '--dist-backend gloo)' % (gpus, visible)
     return 'spawn', None
+
+
+def visible_gpus():
+    """GPUs this process could open, counted without HIP (no torch.cuda, no amdsmi, no HIP
+    runtime loaded): KFD topology nodes with a non-zero gpu_id whose DRM render node opens
+    read-write here (a container or cgroup that hides a GPU makes its node absent or its open
+    fail), then filtered by ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES
+    the way the ROCm runtime applies them (a list of ordinals; empty = none)."""
+    import glob
+    n = 0
+    for node in sorted(glob.glob('/sys/class/kfd/kfd/topology/nodes/*')):
+        try:
+            with open(os.path.join(node, 'gpu_id')) as f:
+                if int(f.read().strip() or 0) == 0:
+                    continue   # a CPU node
+            minor = None
+            with open(os.path.join(node, 'properties')) as f:
+                for line in f:
+                    if line.startswith('drm_render_minor'):
+                        minor = int(line.split()[1])
+            if minor is None:
+                continue
+            fd = os.open('/dev/dri/renderD%d' % minor, os.O_RDWR | os.O_CLOEXEC)
+            os.close(fd)
+            n += 1
+        except (OSError, ValueError):
+            continue
+    for var in ('ROCR_VISIBLE_DEVICES', 'HIP_VISIBLE_DEVICES', 'CUDA_VISIBLE_DEVICES'):
+        v = os.environ.get(var)
+        if v is not None:
+            ids = [s for s in v.split(',') if s.strip() != '']
+            n = min(n, len(ids))
+    return n
+
+
+def rank_census(dist, dev):
+    """What the process group actually is, for the JSON line: world size and backend as
+    torch.distributed reports them, and every rank's device (ordinal, PCI location, UUID)
+    gathered to all ranks.  A collective: every rank calls it."""
+    import torch
+    me = {'rank': dist.get_rank(), 'local_rank': int(os.environ.get('LOCAL_RANK', 0)), 'device': dev,
+          'pid': os.getpid()}
+    try:
+        pr = torch.cuda.get_device_properties(dev)
+        me['device_name'] = pr.name
+        for k in ('pci_domain_id', 'pci_bus_id', 'pci_device_id'):
+            if hasattr(pr, k):
+                me[k] = int(getattr(pr, k))
+        if hasattr(pr, 'uuid'):
+            me['uuid'] = str(pr.uuid)
+    except Exception as e:   # the census must not fail the run
+        me['device_error'] = repr(e)
+    allr = [None] * dist.get_world_size()
+    dist.all_gather_object(allr, me)
+    devs = {(r.get('pci_domain_id'), r.get('pci_bus_id'), r.get('pci_device_id'), r.get('uuid'), r['device'])
+            for r in allr}
+    return {'world_size': dist.get_world_size(), 'backend': str(dist.get_backend()),
+            'distinct_devices': len(devs), 'ranks': allr}
+
+
+def validate_args(a):
+    """Argument combinations that would report work that is not done: an error message or None."""
+    if a.want_rdm and a.e2e:
+        return ('--want-rdm with --e2e: the end-to-end queue (rsp_enqueue_host) does not write the '
+                'complex RD map, so the line would claim map bytes that were never stored')
+    if a.want_rdm and a.config == 'music5':
+        return '--want-rdm applies to the radar chain, not --config music5'
+    return None
 
 
 def spawn_ranks(gpus, argv):
@@ -217,15 +285,50 @@ def music_cpu_baseline(scene, scan, dl, N, K, M, per_core=48):
                       'instances, one BLAS thread each, slowest %.2f s' % (n, cores, per_core, el)}
 
 
+def kernel_hashes():
+    """{kernel: code hash} of the built librsp.so (tools/kernel_hashes.py, written by the Makefile)."""
+    p = os.path.join(PKG, 'rsp', 'kernel_hashes.json')
+    if not os.path.exists(p):
+        return {}
+    with open(p) as f:
+        return json.load(f)
+
+
+def pmc_traffic(path, kernels, now=None):
+    """HBM bytes per launch of the first of `kernels` a PMC traffic file (tools/pmc_traffic.py)
+    holds, with its provenance.  The bytes are returned only while the file is fresh: it recorded
+    the kernel's code hash when it was measured and the built kernel still has that hash;
+    otherwise (kernel changed since, or a file without hashes) the traffic is None and the source
+    says why.  Returns (bytes or None, file's frames per launch, source dict or None)."""
+    import hashlib
+    if not os.path.exists(path):
+        return None, None, None
+    with open(path, 'rb') as f:
+        raw = f.read()
+    tj = json.loads(raw)
+    now = kernel_hashes() if now is None else now
+    src = {'file': os.path.relpath(path, ROOT),
+           'git_blob': hashlib.sha1(b'blob %d\0' % len(raw) + raw).hexdigest()}   # = git hash-object
+    for k in kernels:
+        if k in tj:
+            measured = (tj.get('_kernel_hashes') or {}).get(k)
+            src.update(kernel=k, kernel_hash_measured=measured, kernel_hash_built=now.get(k))
+            src['fresh'] = measured is not None and measured == now.get(k)
+            if not src['fresh']:
+                src['stale_reason'] = ('the PMC file records no kernel hash' if measured is None else
+                                       'the kernel changed since the PMC passes')
+                return None, tj.get('_frames_per_launch'), src
+            return tj[k], tj.get('_frames_per_launch'), src
+    src.update(kernel=None, fresh=False, stale_reason='no entry for %s' % '/'.join(kernels))
+    return None, None, src
+
+
 def music_traffic(prec):
     """k_music_cov HBM bytes per 1024-instance launch from the PMC passes (profiles/, made by
-    tools/pmc_traffic.py over tools/music_prof.py 1024), or None."""
+    tools/pmc_traffic.py over tools/music_prof.py 1024) and its provenance, or (None, source)."""
     tf = os.path.join(ROOT, 'profiles', 'pmc_traffic_music5%s.json' % ('' if prec == 'c64' else '_c128'))
-    if not os.path.exists(tf):
-        return None
-    with open(tf) as f:
-        tj = json.load(f)
-    return tj.get('k_music_cov64', tj.get('k_music_cov'))
+    tr, _, src = pmc_traffic(tf, ['k_music_cov64', 'k_music_cov'])
+    return tr, src
 
 
 def main_music(a):
@@ -273,6 +376,7 @@ def main_music(a):
         t = torch.tensor([el], dtype=torch.float64, device='cuda' if a.dist_backend == 'nccl' else 'cpu')
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    census = rank_census(dist, dev) if dist is not None else None
     out = None
     if rank == 0:
         pr = plan.profile(ring[0], I, iters=a.profile_iters)
@@ -296,6 +400,7 @@ def main_music(a):
                             'one wave per instance, Householder + bisection + inverse iteration + spectrum in '
                             'single') + '; latency-bound (neither HBM nor MFMA), see DESIGN.md'}]
         dom = max(stages, key=lambda st: st['ms_per_launch'])
+        mtraffic = music_traffic(a.precision)
         out = {'metric': 'MUSIC_1D DOA instances/sec, 64ch x 1024 snapshots (BASELINE config #5)',
                'value': I * a.steps * world / el, 'unit': 'instances/s', 'n_gpus': world, 'steps': a.steps,
                'warmup': a.warmup, 'ms_per_step': el / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
@@ -307,7 +412,8 @@ def main_music(a):
                             'achieved': dom['achieved_TFLOPs'],
                             'peak': mfma_peak if dom is stages[0] else valu_peak, 'unit': 'TFLOP/s',
                             'frac': dom['achieved_TFLOPs'] / (mfma_peak if dom is stages[0] else valu_peak),
-                            'traffic': music_traffic(a.precision) if dom is stages[0] else None,
+                            'traffic': mtraffic[0] if dom is stages[0] else None,
+                            'traffic_source': mtraffic[1] if dom is stages[0] else None,
                             'kernel_ms': dom['ms_per_launch'],
                             'timing': 'HIP events on the plan stream, %d launches' % a.profile_iters,
                             'note': 'the dominant kernel of the step; k_music_cov%s: %.3f of the %s MFMA peak, '
@@ -317,6 +423,8 @@ def main_music(a):
                             'stages': stages},
                'cpu_baseline': music_cpu_baseline(scene, scan, dl, N, K, M) if (world == 1 and not a.no_cpu_baseline)
                else None}
+        if census is not None:
+            out['distributed'] = census
     for d in ring:
         plan.device_free(d)
     plan.close()
@@ -328,11 +436,14 @@ def main_music(a):
 
 def main():
     a = parse()
+    bad = validate_args(a)
+    if bad:
+        sys.stderr.write('bench.py: %s\n' % bad)
+        return 2
     env_world = int(os.environ['WORLD_SIZE']) if 'WORLD_SIZE' in os.environ else None
     visible = 0
     if env_world is None and a.gpus > 1 and not a.same_device:
-        import torch
-        visible = torch.cuda.device_count()   # does not initialise the GPU (no HIP context)
+        visible = visible_gpus()   # no HIP in this process: it only spawns the ranks
     mode, msg = launch_mode(a.gpus, env_world, visible, a.same_device, a.dist_backend)
     if mode == 'error':
         sys.stderr.write('bench.py: %s\n' % msg)
@@ -446,6 +557,7 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device='cuda' if a.dist_backend == 'nccl' else 'cpu')
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    census = rank_census(dist, dev) if dist is not None else None
 
     frames = a.frames_total if a.frames_total else a.steps * a.fpl * world
     fps = frames / el
@@ -475,17 +587,16 @@ def main():
         dom = max(stages, key=lambda s: s['ms_per_launch'])
         achieved = dom['achieved_GBps']
         traffic = None
-        # the PMC passes of the same workload (with the RD map written: tools/pmc_pass.sh CFG PREC rdm)
+        # the PMC passes of the same workload (with the RD map written: tools/pmc_pass.sh CFG PREC rdm),
+        # quoted only while the kernel's code is the one they were collected on (pmc_traffic)
         tf = os.path.join(ROOT, 'profiles', 'pmc_traffic_%s_%s%s.json' % (a.config, a.precision,
                                                                          '_rdm' if a.want_rdm else ''))
-        if os.path.exists(tf):
-            with open(tf) as f:
-                tj = json.load(f)
-            # PMC files are keyed by kernel name: stage k1_dbf_mtd runs as k1p_dbf_mtd (persistent K1)
-            tr = tj.get(dom['stage'], tj.get({'k1_dbf_mtd': 'k1p_dbf_mtd'}.get(dom['stage'], '')))
-            if tr is not None:   # scaled from the PMC passes' frames per launch to this run's
-                traffic = tr * dom['frames_per_launch'] / float(tj.get('_frames_per_launch', 4))
-                dom['pmc_traffic_bytes'] = traffic
+        # PMC files are keyed by kernel name: stage k1_dbf_mtd runs as k1p_dbf_mtd (persistent K1)
+        tr, tf_fpl, traffic_src = pmc_traffic(tf, [dom['stage']] + (['k1p_dbf_mtd'] if dom['stage'] == 'k1_dbf_mtd'
+                                                                    else []))
+        if tr is not None:   # scaled from the PMC passes' frames per launch to this run's
+            traffic = tr * dom['frames_per_launch'] / float(tf_fpl or 4)
+            dom['pmc_traffic_bytes'] = traffic
         esz = sz.elem_bytes
         frame_alg_bytes = sz.C * sz.N * sz.P * esz + cells * esz   # cube read + RD map write
         metric = 'frames/sec + range-Doppler cells/sec, %dch×%dbeam×%dsamp×%dpulse' % (sz.C, sz.B, sz.N, sz.P)
@@ -520,6 +631,7 @@ def main():
                 'targets_reported': n_targets_all},
             'roofline': {'bound': 'hbm', 'kernel': dom['stage'], 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                         'traffic_source': traffic_src,
                          'kernel_ms': dom['ms_per_launch'], 'alg_bytes_per_launch': dom['alg_bytes_per_launch'],
                          'frames_per_launch': dom['frames_per_launch'],
                          'timing': 'roofline leg: %d isolated launches per stage, HIP events on the kernel stream '
@@ -545,6 +657,8 @@ def main():
             out['cpu_baseline'] = cpu_baseline(cfg, cfar, clus, W, ang, k, targets, nframes=a.cpu_frames, name=a.config)
         else:
             out['cpu_baseline'] = None
+        if census is not None:   # what RCCL / gloo actually joined: world size, backend, each rank's GPU
+            out['distributed'] = census
     for p in ring + rdm_ring:
         plan.device_free(p)
     for h in hring:

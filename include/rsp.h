@@ -219,7 +219,8 @@ int32_t rsp_synthesize_device(rsp_plan* plan, const rsp_target_in* targets, int3
  * on the host.  rsp_drain waits for everything queued.  Results are kept in
  * enqueue order until rsp_results_clear. */
 int32_t rsp_enqueue_device(rsp_plan* plan, const void* d_cube, int32_t frame_idx);
-/* rsp_enqueue_device for n frames in one call (d_cubes[i], frame_idx[i]). */
+/* rsp_enqueue_device for n frames in one call (d_cubes[i], frame_idx[i]).  All or nothing: a null
+ * d_cubes[i] (or d_rdms[i] in the _rdm_n form) is refused before any frame is queued. */
 int32_t rsp_enqueue_device_n(rsp_plan* plan, const void* const* d_cubes, const int32_t* frame_idx, int32_t n);
 /* rsp_enqueue_device that also produces the frame's complex range-Doppler map rdm_13beam
  * (fsf:131-136, the rsp_mex('cube') output): K2 writes it straight into the caller's device buffer
@@ -284,7 +285,11 @@ int32_t rsp_process_stage2_gated(rsp_plan* plan, const void* iq_gated, int32_t d
 int32_t rsp_profile_stages(rsp_plan* plan, const void* const* d_cubes, int32_t n_cubes, int32_t iters,
                            float* ms_out, int64_t* bytes_out, int32_t cap, int32_t* frames_out);
 /* rsp_profile_stages with K2 writing every frame's complex RD map (d_rdms[f], f < nf, as
- * rsp_enqueue_device_rdm); bytes_out[1] then includes the map.  d_rdms = NULL: rsp_profile_stages. */
+ * rsp_enqueue_device_rdm); bytes_out[1] then includes the map.  d_rdms = NULL: rsp_profile_stages.
+ * d_rdms must hold nf = min(n_cubes, frames_per_launch) non-null maps (a null one is refused with
+ * RSP_ERR_INVALID; the array's length cannot be checked here, so the caller sizes it).  A plan with
+ * RSP_PLAN_MONOPULSE_COMPLEX writes the map into its own lane buffer on every launch, so its
+ * bytes_out[1] includes the map whether or not d_rdms is given. */
 int32_t rsp_profile_stages_rdm(rsp_plan* plan, const void* const* d_cubes, int32_t n_cubes, void* const* d_rdms,
                                int32_t iters, float* ms_out, int64_t* bytes_out, int32_t cap, int32_t* frames_out);
 const char* rsp_stage_name(int32_t stage);

@@ -772,8 +772,9 @@ __global__ __launch_bounds__(MU_THREADS, 2) void k_music_cov64(int N, int K, con
 // Floor of the squared off-diagonal entries the Sturm count reads (e2[], not ee[]): an exactly
 // zero minor p_r must act as dstebz's q_r = -pivmin, i.e. a sign change after which
 // p_{r+1} = -e_r^2 p_{r-1} carries on with the opposite sign.  With e_r^2 = 0 (a decoupled row or
-// the pad rows) p_{r+1} would be 0 again and flip once more; at e_r^2 >= 2^-600 it is not, and the
-// eigenvalues move by at most ~2^-300.
+// the pad rows) p_{r+1} would be 0 again and flip once more; at e_r^2 >= 2^-600 it is not.  The
+// count runs on T scaled by 2^-s, 2^s ~ ||T|| (exact: a power of two), so the floor is relative --
+// the eigenvalues move by at most ~2^-300 ||T|| and the solver is scale-invariant like eig.
 #define ME_E2MIN 0x1p-600
 #ifndef ME_WPS
 #define ME_WPS 4     // waves per SIMD the register budget is sized for (4 instances per CU)
@@ -855,8 +856,7 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
             if (lane == 0) {
                 taus[k] = tau;
                 dd[k] = dk;
-                ee[k] = beta;
-                e2[k] = fmax(beta * beta, ME_E2MIN);
+                ee[k] = beta;   // e2 (scaled, floored) is formed in phase 2
             }
         }
         __syncthreads();
@@ -931,7 +931,7 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
             const double rad = (r > 0 ? fabs(ee[r - 1]) : 0.0) + (r < n - 1 ? fabs(ee[r]) : 0.0);
             glo = fmin(glo, dd[r] - rad);
             ghi = fmax(ghi, dd[r] + rad);
-            if (r < n - 1) emax = fmax(emax, e2[r]);
+            if (r < n - 1) emax = fmax(emax, ee[r] * ee[r]);
         }
         const double tn = fmax(fabs(glo), fabs(ghi));
         const double pivmin = 2.2250738585072014e-308 * fmax(1.0, emax);   // dstebz PIVMIN
@@ -943,23 +943,32 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
         // are rescaled by a power of two every 4 rows (no overflow or underflow).
         // rows n .. n + 3 pad the count to whole blocks of 4: d = ghi + 1 > every x of the
         // search and e^2 = ME_E2MIN keep the minors' signs (p_r ~ (d - x) p_{r-1}, d - x > 0)
-        __syncthreads();   // every lane has read dd / e2 (Gershgorin) before the pad rows land
+        // The count runs on 2^-s T, 2^s ~ ||T|| (x, d scaled as they are read; e^2 formed here from
+        // the scaled e): powers of two, so for any T whose scaled entries neither underflow nor
+        // overflow the signs are those of T itself, and the floor ME_E2MIN is relative to ||T||.
+        const double isg = __builtin_amdgcn_ldexp(1.0, -__builtin_amdgcn_frexp_exp(tn));
+        __syncthreads();   // every lane has read dd / ee (Gershgorin) before the pad rows land
+        for (int r = t; r < n - 1; r += ME_THREADS) {
+            const double es = ee[r] * isg;
+            e2[r] = fmax(es * es, ME_E2MIN);
+        }
         if (t < 4) {
-            dd[n + t] = ghi + 1.0;
+            dd[n + t] = ghi + fmax(tn, 1.0);   // > hi at any scale
             e2[n - 1 + t] = ME_E2MIN;
         }
         __syncthreads();
-        auto sturm = [&](double x) -> int {
-            double pm = 1.0, pc = dd[0] - x;
+        auto sturm = [&](double xu) -> int {
+            const double x = xu * isg;
+            double pm = 1.0, pc = dd[0] * isg - x;
             bool sc = !(pc > 0.0);   // effective sign of p_0 (zero -> negative, as -pivmin)
             int c = sc;
-            double dn = dd[1], en = e2[0];   // row r's (d_r, e_{r-1}^2), loaded a row ahead
+            double dn = dd[1] * isg, en = e2[0];   // row r's (d_r, e_{r-1}^2), loaded a row ahead
             for (int r0 = 1; r0 < n; r0 += 4) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int r = r0 + j;
                     const double d = dn, e = en;
-                    dn = dd[r + 1];   // r + 1 <= n + 3 (padded)
+                    dn = dd[r + 1] * isg;   // r + 1 <= n + 3 (padded)
                     en = e2[r];
                     const double pn = fma(d - x, pc, -e * pm);
                     const bool sn = (pn < 0.0) | ((pn == 0.0) & !sc);

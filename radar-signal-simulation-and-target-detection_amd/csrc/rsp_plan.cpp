@@ -1205,8 +1205,9 @@ int32_t rsp_enqueue_device(rsp_plan* p, const void* d_cube, int32_t frame_idx) {
 int32_t rsp_enqueue_device_n(rsp_plan* p, const void* const* d_cubes, const int32_t* frame_idx, int32_t n) {
     if (!p || (n > 0 && (!d_cubes || !frame_idx)) || n < 0) return fail(RSP_ERR_INVALID, "bad argument");
     HIPCHK(hipSetDevice(p->device));
-    for (int i = 0; i < n; ++i) {
+    for (int i = 0; i < n; ++i)   // all or nothing: no frame is queued when any pointer is bad
         if (!d_cubes[i]) return fail(RSP_ERR_INVALID, "cube %d is null", i);
+    for (int i = 0; i < n; ++i) {
         int rc = enqueue_frame(p, d_cubes[i], -1, frame_idx[i]);
         if (rc) return rc;
     }
@@ -1223,8 +1224,9 @@ int32_t rsp_enqueue_device_rdm_n(rsp_plan* p, const void* const* d_cubes, const 
                                  int32_t n) {
     if (!p || (n > 0 && (!d_cubes || !frame_idx || !d_rdms)) || n < 0) return fail(RSP_ERR_INVALID, "bad argument");
     HIPCHK(hipSetDevice(p->device));
-    for (int i = 0; i < n; ++i) {
+    for (int i = 0; i < n; ++i)   // all or nothing: no frame is queued when any pointer is bad
         if (!d_cubes[i] || !d_rdms[i]) return fail(RSP_ERR_INVALID, "cube or map %d is null", i);
+    for (int i = 0; i < n; ++i) {
         int rc = enqueue_frame(p, d_cubes[i], -1, frame_idx[i], d_rdms[i]);
         if (rc) return rc;
     }
@@ -1467,6 +1469,8 @@ int32_t rsp_profile_stages_rdm(rsp_plan* p, const void* const* d_cubes, int32_t 
     if (rc) return rc;
     Lane& L = p->lanes[0];
     const int nf = std::min(n_cubes, p->F);
+    for (int f = 0; f < nf && d_rdms; ++f)   // d_rdms holds (at least) one map per frame of the batch
+        if (!d_rdms[f]) return fail(RSP_ERR_INVALID, "map %d is null (d_rdms needs min(n_cubes, F) maps)", f);
     // batches rotate over all n_cubes cubes (cube (j nf + f) mod n_cubes in batch j), so that a
     // ring larger than the 256 MiB Infinity Cache makes K1 read its input from HBM as in the queue
     const int nsets = (n_cubes + nf - 1) / nf;
@@ -1510,7 +1514,10 @@ int32_t rsp_profile_stages_rdm(rsp_plan* p, const void* const* d_cubes, int32_t 
         const int64_t z = (int64_t)g.B * g.nU * g.P * es;          // Doppler-domain rows
         const int64_t mag = (int64_t)g.B * g.P * g.G * rs;         // |RD| map (the RDM stays on chip)
         if (cap > 0) bytes_out[0] = nf * (cube + z);
-        const int64_t rdm = d_rdms ? (int64_t)g.B * g.P * g.G * es : 0;   // the RD map, when written
+        // the complex RD map, when written: into d_rdms, or (complex-ratio monopulse) into the
+        // lane's own map, which K3 then reads only at the detected cells (2 values per detection,
+        // not a map-sized stream, so K3's bytes stay the magnitude maps)
+        const int64_t rdm = (d_rdms || g.mono_c) ? (int64_t)g.B * g.P * g.G * es : 0;
         if (cap > 1) bytes_out[1] = nf * (z + mag + rdm);
         if (cap > 2) bytes_out[2] = nf * mag;
     }

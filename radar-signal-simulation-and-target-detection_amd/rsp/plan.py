@@ -97,6 +97,7 @@ class Plan:
         self.sizes = s
         self.P, self.N, self.C, self.B, self.G = s.P, s.N, s.C, s.B, s.G
         self.precision = precision
+        self.frames_per_launch = int(frames_per_launch)   # F: frames per kernel launch (1..RSP_MAX_F)
         self.cdtype = np.complex128 if precision == 'c128' else np.complex64   # device cube / map element
         self.cube_bytes = s.cube_elems * s.elem_bytes
 
@@ -343,6 +344,10 @@ class Plan:
         by = (ct.c_int64 * n)()
         arr = (ct.c_void_p * len(d_cubes))(*d_cubes)
         nf = ct.c_int32()
+        if d_rdms:   # the C call reads min(len(d_cubes), F) maps: a shorter list would be read past its end
+            need = min(len(d_cubes), self.frames_per_launch)
+            if len(d_rdms) < need or any(r is None or not int(r) for r in d_rdms[:need]):
+                raise ValueError('d_rdms needs %d non-null device maps (one per frame of the batch)' % need)
         ra = (ct.c_void_p * len(d_rdms))(*d_rdms) if d_rdms else None
         check(lib().rsp_profile_stages_rdm(self.h, arr, len(d_cubes), ra, int(iters), ms, by, n, ct.byref(nf)))
         return [{'stage': lib().rsp_stage_name(i).decode(), 'ms': ms[i], 'bytes': by[i], 'frames': nf.value}

@@ -50,3 +50,72 @@ def test_too_few_visible_devices_exits_nonzero():
     r = _run(['--gpus', '8'], HIP_VISIBLE_DEVICES='')
     assert r.returncode == 2 and '--gpus 8 but only' in r.stderr
     assert r.stdout == ''
+
+
+_PROBE = r'''
+import sys
+sys.path.insert(0, %r)
+import bench
+def spawn(gpus, argv):   # stands in for torch.distributed.run: report what this process has loaded
+    maps = open('/proc/self/maps').read()
+    print('SPAWN', gpus, 'hip=%%d' %% ('libamdhip64' in maps), 'torch=%%d' %% ('torch' in sys.modules))
+    return 0
+bench.spawn_ranks = spawn
+sys.argv = ['bench.py'] + sys.argv[1:]
+rc = bench.main()
+maps = open('/proc/self/maps').read()
+print('END rc=%%d hip=%%d' %% (rc, 'libamdhip64' in maps))
+'''
+
+
+@pytest.mark.parametrize('args,want', [
+    (['--gpus', '2', '--same-device', '--dist-backend', 'gloo'], 'SPAWN 2 hip=0 torch=0'),
+    (['--gpus', '8'], 'END rc=2 hip=0'),   # counts the devices, refuses, never loads HIP
+])
+def test_launcher_never_loads_hip(args, want):
+    """The `--gpus N` parent decides and spawns without the HIP runtime in its address space
+    (no torch.cuda / amdsmi / hipGetDeviceCount): its fork/exec of torchrun can never follow a
+    GPU initialisation."""
+    e = dict(os.environ)
+    for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK'):
+        e.pop(k, None)
+    r = subprocess.run([sys.executable, '-c', _PROBE % ROOT] + args, env=e, capture_output=True, text=True,
+                       timeout=120)
+    assert want in r.stdout, (r.stdout, r.stderr)
+    assert 'hip=1' not in r.stdout
+
+
+def test_want_rdm_with_e2e_refused():
+    """--want-rdm --e2e would report RD-map bytes the host queue never writes (ADVICE r4)."""
+    r = _run(['--want-rdm', '--e2e'])
+    assert r.returncode == 2 and '--want-rdm with --e2e' in r.stderr
+    assert r.stdout == ''
+
+
+def test_visible_gpus_honours_visible_devices_env(monkeypatch):
+    monkeypatch.setenv('HIP_VISIBLE_DEVICES', '')
+    assert bench.visible_gpus() == 0
+
+
+def test_pmc_traffic_staleness(tmp_path):
+    """roofline.traffic is quoted only while the kernel's code hash equals the one the PMC file
+    recorded at measurement (VERDICT r4 #8); git_blob is the file's `git hash-object`."""
+    import hashlib
+    import json
+    f = tmp_path / 'pmc.json'
+    body = {'k2_pc': 1000, 'k1p_dbf_mtd': 2000, '_frames_per_launch': 8,
+            '_kernel_hashes': {'k2_pc': 'aaaa', 'k1p_dbf_mtd': 'bbbb'}}
+    f.write_text(json.dumps(body))
+    raw = f.read_bytes()
+    blob = hashlib.sha1(b'blob %d\0' % len(raw) + raw).hexdigest()
+    tr, fpl, src = bench.pmc_traffic(str(f), ['k2_pc'], now={'k2_pc': 'aaaa'})
+    assert (tr, fpl, src['fresh'], src['git_blob']) == (1000, 8, True, blob)
+    tr, _, src = bench.pmc_traffic(str(f), ['k2_pc'], now={'k2_pc': 'cccc'})          # kernel rebuilt since
+    assert tr is None and not src['fresh'] and 'changed' in src['stale_reason']
+    tr, _, src = bench.pmc_traffic(str(f), ['k1_dbf_mtd', 'k1p_dbf_mtd'], now={'k1p_dbf_mtd': 'bbbb'})
+    assert tr == 2000 and src['kernel'] == 'k1p_dbf_mtd'
+    del body['_kernel_hashes']
+    f.write_text(json.dumps(body))
+    tr, _, src = bench.pmc_traffic(str(f), ['k2_pc'], now={'k2_pc': 'aaaa'})          # no hashes recorded
+    assert tr is None and 'no kernel hash' in src['stale_reason']
+    assert bench.pmc_traffic(str(tmp_path / 'missing.json'), ['k2_pc']) == (None, None, None)

@@ -88,3 +88,38 @@ def test_gather_two_ranks_equals_single_process():
         for t, u in zip(tl, w['final_targets']):
             assert t == pytest.approx((u['Range'], u['Velocity'], u['Angle'], u['Power']), rel=1e-12)
     assert sum(len(tl) for _, _, tl in got) > 0
+
+
+def _census_worker(rank, world, port, q):
+    import sys
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), LOCAL_RANK=str(rank))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        q.put((rank, bench.rank_census(dist, rank)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_rank_census_two_ranks():
+    """The census bench.py puts in an N > 1 line: world size and backend from torch.distributed
+    itself, and every rank's device ordinal, gathered (gloo here; RCCL on the node)."""
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_census_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        c = outs[r]
+        assert c['world_size'] == world and c['backend'] == 'gloo'
+        assert [x['rank'] for x in c['ranks']] == [0, 1]
+        assert [x['device'] for x in c['ranks']] == [0, 1]
+        assert c['distinct_devices'] == 2

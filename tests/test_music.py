@@ -232,3 +232,22 @@ def test_music_decoupled_covariance_eigenvalues():
     want = np.sort(mags)[::-1]
     for i in range(2):
         assert np.abs(o['eig'][i] - want).max() <= 1e-12 * want.max(), (o['eig'][i], want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('scale', [1e-60, 1e40])
+def test_music_scale_invariance(music_case, scale):
+    """eig is scale-invariant: X scaled by 1e-60 (R by 1e-120) or 1e40 gives eigenvalues scaled by
+    scale^2 (to the c128 tolerance) and the same spectrum, peaks and findpeaks count (ADVICE r4:
+    the Sturm count's e^2 floor is relative to ||T||, not an absolute 2^-600)."""
+    c = music_case
+    if c['prec'] != 'c128':
+        pytest.skip('complex single cannot hold R at 1e-120 / 1e80')
+    o = c['plan'].process(c['X'][:2] * scale)
+    for i in range(2):
+        d = c['out']['eig'][i]
+        assert np.abs(o['eig'][i] / scale ** 2 - d).max() <= c['tol']['eig'] * d.max()
+        assert list(o['peaks'][i]) == list(c['out']['peaks'][i])
+        assert o['n_peaks'][i] == c['out']['n_peaks'][i]
+        live = c['out']['spectrum_db'][i] > -60.0
+        assert np.abs(o['spectrum_db'][i][live] - c['out']['spectrum_db'][i][live]).max() <= 1e-6

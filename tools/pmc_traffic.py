@@ -10,6 +10,7 @@ import collections
 import csv
 import glob
 import json
+import os
 import statistics
 import sys
 
@@ -41,6 +42,13 @@ def main():
                     'tools/prof_stages.py ' + ' '.join(sys.argv[4:]))
     if len(sys.argv) > 6:
         res['_frames_per_launch'] = int(sys.argv[6])
+    # the code the counters were collected on: bench.py reports this file's traffic for a kernel
+    # only while the built kernel still has the same hash (tools/kernel_hashes.py)
+    kh = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                      'radar-signal-simulation-and-target-detection_amd', 'rsp', 'kernel_hashes.json')
+    if os.path.exists(kh):
+        hashes = json.load(open(kh))
+        res['_kernel_hashes'] = {k: hashes.get(k) for k in res if not k.startswith('_')}
     json.dump(res, open(out, 'w'), indent=1)
     print(json.dumps(res))
 
