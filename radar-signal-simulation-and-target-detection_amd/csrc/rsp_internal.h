@@ -14,7 +14,10 @@
 #define RSP_Z_LINE 0   // bytes of one row's z chunk (0: NT samples, the K1 tile width)
 #endif
 #ifndef RSP_K2_POINTS
-#define RSP_K2_POINTS 4096   // complex points per pulse-compression workgroup
+#define RSP_K2_POINTS 4096   // complex points per pulse-compression workgroup (Geometry::k2_pts)
+#endif
+#ifndef RSP_K2_MIXPTS
+#define RSP_K2_MIXPTS 2560   // Geometry::k2_pts of a complex-double plan with a 2560-point block
 #endif
 #define K2_THREADS 256       // threads per pulse-compression workgroup (16 points each)
 #define RSP_THREADS 256
@@ -108,6 +111,10 @@ struct Geometry {
     int twPp_elems;  // per-pass twiddles of the P-point FFT
     int pow2P, logP;
     int nseg, njobs, nwg_k2;
+    // complex points of LDS rows per pulse-compression workgroup: RSP_K2_POINTS, or 2560 in a
+    // complex-double plan with a 2560-point block (3 workgroups per CU: 53.5 KB of LDS each);
+    // power-of-two blocks then take 2048 / M rows
+    int k2_pts;
     int cfar_RT, cfar_hR, cfar_W;
     int cfar_VB, cfar_nband, cfar_rows;   // K3 Doppler bands: cells under test per band, bands, tile rows
     int refR, guardR, refV, guardV;

@@ -118,6 +118,34 @@ __device__ __forceinline__ void buf_st1(__amdgpu_buffer_rsrc_t r, unsigned off, 
 #define RSP_RDM_AUX 2   // K2's RDM stores
 #endif
 
+// Diagnostic builds (-DRSP_DEBUG_KNOBS) only: K2 phase stamps.  Workgroup (f, x) of a k2_pc
+// launch writes s_memrealtime (100 MHz) at its phase boundaries into rsp_k2_trace[(f G + x) 8 +
+// i], i < 6, plus its job type [6] and hardware position (HW_ID | XCC_ID << 32) [7]
+// (tools/ab/k2_phases.py).  The shipped library has neither the variable nor the stamps.
+#ifdef RSP_DEBUG_KNOBS
+__device__ unsigned long long* rsp_k2_trace;
+#define K2_STAMP(i)                                                                                     \
+    do {                                                                                                \
+        if (rsp_k2_trace && threadIdx.x == 0)                                                           \
+            rsp_k2_trace[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + (i)] = wall_clock64();    \
+    } while (0)
+#define K2_TAG(v)                                                                                       \
+    do {                                                                                                \
+        if (rsp_k2_trace && threadIdx.x == 0) {                                                         \
+            unsigned long long* t_ = rsp_k2_trace + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8;  \
+            t_[6] = (v);                                                                                \
+            t_[7] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |                     \
+                    ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);             \
+        }                                                                                               \
+    } while (0)
+extern "C" int rsp_debug_set_k2_trace(unsigned long long* p) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(rsp_k2_trace), &p, sizeof(p));
+}
+#else
+#define K2_STAMP(i) ((void)0)
+#define K2_TAG(v) ((void)0)
+#endif
+
 // ---- radix-R DFT kernels in registers -------------------------------------------------
 // Radix-2 butterfly with a twiddle, (a, b) <- (a + w b, a - w b): four FMAs for a + w b and one
 // per component for a - w b = 2a - (a + w b) -- 6 operations instead of a complex multiply (4)
@@ -1114,7 +1142,8 @@ __device__ __forceinline__ ZWin zrow_window(const Geometry& g, const V* z, int r
 // onto lane 12's bank), and the stride-16 stores of the two radix-16 Ns = 1 passes 2-way
 // (tools/ab/lds_conflicts64.py)
 template <class T> constexpr int k2_sh() { return sizeof(T) == 4 ? 5 : RSP_K2_SH64; }
-#define K2_LDS_DATA(SH) (RSP_K2_POINTS + (RSP_K2_POINTS >> (SH)))
+// LDS complex slots of a workgroup's rows: pts points (Geometry::k2_pts) + their pads
+__host__ __device__ constexpr int k2_lds_data(int pts, int sh) { return pts + (pts >> sh); }
 
 // The block's twiddle tables are staged in LDS next to the rows: a pass's twiddles then arrive
 // with its LDS data reads instead of after an L2 round trip (-6% for k2_pc in complex double).
@@ -1136,20 +1165,66 @@ constexpr int k2_tw_lds_max() {
     return m;
 }
 
-// One overlap-save block of one FFT segment for RSP_K2_POINTS / 2^LGM adjacent rows.
+// The kept overlap-save outputs of `rows` rows from LDS (in natural order after the inverse FFT's
+// last pass) to the maps: output o = Lh1 + e is stitched gate g0 + e (fsf:123-126); |x| into the
+// magnitude map (the CFAR input, fsf:184-185) and, when the frame's RD map is requested, x into
+// it.  Consecutive lanes take consecutive gates (coalesced, conflict-free LDS reads), and the
+// square roots run a few at a time instead of 16 per thread at once at the end of the last pass:
+// that pass was k2_pc's register peak (188 VGPRs; with this epilogue 3 workgroups fit per CU).
+template <class T, int SH>
+__device__ __forceinline__ void k2_epilogue(const cx<T>* L, int rs, int rows, int row0, int rows_total, int Lh1, int g0,
+                                            int gend, cx<T>* __restrict__ rdm, T* __restrict__ mag, int G, int Gp) {
+    typedef cx<T> V;
+    const int nkeep = gend - g0;
+    for (int r = 0; r < rows; ++r) {
+        const int rho = row0 + r;   // uniform
+        if (rho >= rows_total) break;
+        const V* src = L + r * rs + Lh1;
+        const int pad0 = SH ? Lh1 : 0;
+        const __amdgpu_buffer_rsrc_t mr = buf_rsrc(mag + (size_t)rho * Gp + g0, (unsigned)nkeep * (unsigned)sizeof(T));
+        if (rdm) {
+            const __amdgpu_buffer_rsrc_t rr = buf_rsrc(rdm + (size_t)rho * G + g0, (unsigned)nkeep * (unsigned)sizeof(V));
+            for (int e = threadIdx.x; e < nkeep; e += K2_THREADS) {
+                const V x = src[e + (SH ? ((pad0 + e) >> SH) : 0)];
+                buf_st<RSP_RDM_AUX>(rr, (unsigned)e * (unsigned)sizeof(V), x);
+                buf_st1(mr, (unsigned)e * (unsigned)sizeof(T), cmag(x));
+            }
+        } else {
+            for (int e = threadIdx.x; e < nkeep; e += K2_THREADS)
+                buf_st1(mr, (unsigned)e * (unsigned)sizeof(T), cmag(src[e + (SH ? ((pad0 + e) >> SH) : 0)]));
+        }
+    }
+}
+
+// x[r] *= H[j + r S] (the filter spectrum, 1/M folded in) for the fused pass's R outputs, loaded
+// after the forward DFT that produces them: H then occupies registers only from here to the
+// product (an empty asm keeps the loads below the DFT; loaded with the samples it held 64 VGPRs
+// of complex double through the whole forward FFT)
+template <int R, int S, class V>
+__device__ __forceinline__ void k2_apply_h(V (&x)[R], __amdgpu_buffer_rsrc_t hr, int j) {
+    asm volatile("" ::: "memory");
+    V h[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) h[r] = buf_ld<V>(hr, (unsigned)(j + r * S) * (unsigned)sizeof(V));
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = vmul(x[r], h[r]);
+}
+
+// One overlap-save block of one FFT segment for PTS / 2^LGM adjacent rows (PTS = 4096, or 2048
+// in a plan whose workgroups are sized for the 2560-point block, Geometry::k2_pts).
 // LDS round trips: forward pass 0 runs on the samples as loaded from z; the forward FFT's
 // last pass, the filter-spectrum product and the inverse FFT's first pass (radices in
 // reverse order, so that pass has the same butterflies) run in registers back to back;
 // the inverse FFT's last pass stores the kept gates to HBM.  2 (log2 M / 4) round trips
 // instead of 2 (log2 M / 4) + 3.  Twiddles are compact rows, staged in LDS.
-template <class T, int LGM>
+template <class T, int LGM, int PTS, bool EPI>
 __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k, const SegDesc& sd, const K2Job& job,
                                            const cx<T>* __restrict__ z, cx<T>* __restrict__ rdm, T* __restrict__ mag,
                                            int row0, int rows_total, cx<T>* L) {
     typedef cx<T> V;
     constexpr int SH = k2_sh<T>();
     constexpr int M = 1 << LGM;
-    constexpr int rows = RSP_K2_POINTS / M;
+    constexpr int rows = PTS / M > 0 ? PTS / M : 1;
     constexpr int rs = M + (M >> SH);
     constexpr int NP = n_passes(LGM);
     static_assert(NP >= 2, "overlap-save block needs >= 2 FFT passes");
@@ -1214,19 +1289,21 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
             }
         }
     }
-    // H for the last forward pass's outputs j + r M/RL; butterflies t and t + (M/RL)/NTHR of a
-    // thread have the same j (different rows), so only the distinct ones are loaded
-    constexpr int NHT = (M / RL) / K2_THREADS >= NBL ? NBL : ((M / RL) / K2_THREADS > 0 ? (M / RL) / K2_THREADS : 1);
-    V hreg[NHT * RL];
     const __amdgpu_buffer_rsrc_t hr = buf_rsrc(H + sd.H_off, (unsigned)(M * sizeof(V)));
+    // !EPI: H for the last forward pass's outputs j + r M/RL loaded with the samples; butterflies t
+    // and t + (M/RL)/NTHR of a thread have the same j (different rows), so only the distinct ones
+    constexpr int NHT = !EPI ? ((M / RL) / K2_THREADS >= NBL ? NBL : ((M / RL) / K2_THREADS > 0 ? (M / RL) / K2_THREADS : 1)) : 1;
+    V hreg[NHT * RL];
+    if constexpr (!EPI) {
 #pragma unroll
-    for (int t = 0; t < NHT; ++t) {
-        const int j = (tid + t * K2_THREADS) & (M / RL - 1);   // last pass: Ns = nb = M / RL, idxD = j
+        for (int t = 0; t < NHT; ++t) {
+            const int j = (tid + t * K2_THREADS) & (M / RL - 1);   // last pass: Ns = nb = M / RL, idxD = j
 #pragma unroll
-        for (int r = 0; r < RL; ++r) hreg[t * RL + r] = buf_ld<V>(hr, (unsigned)(j + r * (M / RL)) * (unsigned)sizeof(V));
+            for (int r = 0; r < RL; ++r) hreg[t * RL + r] = buf_ld<V>(hr, (unsigned)(j + r * (M / RL)) * (unsigned)sizeof(V));
+        }
     }
     constexpr int NTWF = tw_total(LGM, false, CMP, PAL);
-    V* twL = L + K2_LDS_DATA(SH);
+    V* twL = L + k2_lds_data(g.k2_pts, SH);
     for (int e = tid; e < k2_tw_lds(LGM); e += K2_THREADS) twL[e] = twl[e];   // visible after the pass-0 barrier
     const V* twF = twL;
     const V* twI = k2_tw_sym(LGM) ? twL : twL + NTWF;
@@ -1235,6 +1312,7 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     constexpr int XZ = (NP == 3 && R0 == 16 && RL == 16 && RSP_K2_XOR) ? 1 : 0;
     sh_store<R0, false, NB0, SH, K2_THREADS, LGM, 0, XZ>(v0, rs, rows, StoreLds<V>{L});
     __syncthreads();
+    K2_STAMP(1);
     // forward passes 1 .. NP-2
     fft_range<LGM, 1, NP - 1, RB0, 16, false, false, SH, K2_THREADS, CMP, PAL, XZ>(L, rs, rows, twF, StoreLds<V>{L},
                                                                                StoreLds<V>{L});
@@ -1247,19 +1325,29 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
 #pragma unroll
         for (int t = 0; t < NBL; ++t) {
             Dft<RL, false, V>::run(v[t]);
+            // last forward pass: Ns = nb = M / RL, thread j's outputs j + r M / RL
+            if constexpr (EPI) {
+                k2_apply_h<RL, M / RL>(v[t], hr, (tid + t * K2_THREADS) & (M / RL - 1));
+            } else {
 #pragma unroll
-            for (int r = 0; r < RL; ++r) v[t][r] = vmul(v[t][r], hreg[(t % NHT) * RL + r]);
+                for (int r = 0; r < RL; ++r) v[t][r] = vmul(v[t][r], hreg[(t % NHT) * RL + r]);
+            }
         }
         sh_store<RL, true, NBL, SH, K2_THREADS, LGM, 0, XZ>(v, rs, rows, StoreLds<V>{L});
         __syncthreads();
     }
-    // inverse passes 1 .. NP-1 (reversed radices); the last keeps the valid overlap-save
-    // outputs = stitched gates
+    K2_STAMP(3);
     const int gend = min(sd.gb, g0 + sd.V);
-    // the inverse FFT's last pass runs the forward pass 0's radix (R0) over nb0 butterflies
-    if constexpr (WROW) {
+    if constexpr (EPI) {
+        // inverse passes 1 .. NP-1 (reversed radices) into LDS; then the valid overlap-save outputs
+        // = stitched gates go to the maps
+        fft_range<LGM, 1, NP, RBL, 16, true, true, SH, K2_THREADS, CMP, PAL, XZ>(L, rs, rows, twI, StoreLds<V>{L},
+                                                                               StoreLds<V>{L});
+        k2_epilogue<T, SH>(L, rs, rows, row0, rows_total, Lh1, g0, gend, rdm, mag, G, g.Gp);
+    } else if constexpr (WROW) {
         // inverse passes 1 .. NP-2 into LDS, then the last one (Ns = nb0, input not swizzled:
-        // XZ applies to the pass after an Ns = 1 pass only) into this wave's row of the maps
+        // XZ applies to the pass after an Ns = 1 pass only) stores the kept gates straight into
+        // this wave's row of the maps
         fft_range<LGM, 1, NP - 1, RBL, 16, true, true, SH, K2_THREADS, CMP, PAL, XZ>(L, rs, rows, twI, StoreLds<V>{L},
                                                                                    StoreLds<V>{L});
         constexpr int LGNSL = LGM - RB0;
@@ -1272,14 +1360,14 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
         else
             sh_pass<R0, true, NB0, SH, K2_THREADS, LGM, LGNSL, CMP, 0, false>(
                 L, rs, rows, twl_last, StoreRowK<V, false, nb0, R0>(rdm, mag, G, g.Gp, rho, rows_total, Lh1, g0, gend));
-    } else
+    } else {
         fft_range<LGM, 1, NP, RBL, 16, true, true, SH, K2_THREADS, CMP, PAL, XZ, false>(
             L, rs, rows, twI, StoreLds<V>{L},
             StoreRdm<V>{buf_rsrc(rdm, (unsigned)(rows_total * G * sizeof(V))),
                         buf_rsrc(mag, (unsigned)(rows_total * g.Gp * sizeof(T))), G, g.Gp, row0, rows_total, Lh1, g0,
                         gend, rdm != nullptr});
+    }
 }
-
 
 // Mixed-radix overlap-save block M = 16 x R1 x 16 (2560 = 16 x 10 x 16): one block of M = 2560
 // covers x2's long segment (Lh = 700, 1860 gates), which takes two 2048-point blocks in powers of
@@ -1288,7 +1376,7 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
 // so the inverse FFT runs the same radices, the fused middle pass (forward radix-16 pass, x H,
 // inverse radix-16 pass 0) has the same butterflies on both sides as in k2_fft_job, and the
 // inverse twiddle table equals the forward one (conjugated in load_tw).
-template <class T, int M, int R1>
+template <class T, int M, int R1, bool EPI>
 __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConsts& k, const SegDesc& sd, const K2Job& job,
                                                const cx<T>* __restrict__ z, cx<T>* __restrict__ rdm, T* __restrict__ mag,
                                                int row0, int rows_total, cx<T>* L) {
@@ -1316,7 +1404,7 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
     const V* __restrict__ H = static_cast<const V*>(k.H);
     static_assert(rows == 1 && NB0 == 1, "one row per workgroup, one radix-16 butterfly per thread");
     V v0[NB0][R0];
-    V hreg[NB0][R0];
+    V hreg[EPI ? 1 : NB0][R0];   // !EPI: the fused pass's H, loaded with the samples
     // threads nb0.. have no radix-16 butterfly (waves past nb0 skip the loads); the row's samples
     // are one scalar buffer window (zrow_window), so the loads need no masks
     if (tid < nb0) {
@@ -1331,36 +1419,50 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
 #pragma unroll
             for (int r = 0; r < R0; ++r) v0[0][r] = buf_ld<V>(zw.r, (unsigned)zw.rel(np0 + r * nb0) * (unsigned)sizeof(V));
         }
-        const __amdgpu_buffer_rsrc_t hr = buf_rsrc(H + sd.H_off, (unsigned)(M * sizeof(V)));
+        if constexpr (!EPI) {
+            const __amdgpu_buffer_rsrc_t hr = buf_rsrc(H + sd.H_off, (unsigned)(M * sizeof(V)));
 #pragma unroll
-        for (int r = 0; r < R0; ++r)   // fused pass outputs j + r M/16
-            hreg[0][r] = buf_ld<V>(hr, (unsigned)(j + r * nb0) * (unsigned)sizeof(V));
+            for (int r = 0; r < R0; ++r)   // fused pass outputs j + r M/16
+                hreg[0][r] = buf_ld<V>(hr, (unsigned)(j + r * nb0) * (unsigned)sizeof(V));
+        }
     }
-    V* twL = L + K2_LDS_DATA(SH);
+    V* twL = L + k2_lds_data(g.k2_pts, SH);
     for (int e = threadIdx.x; e < NTWF; e += K2_THREADS) twL[e] = twl[e];
     const V* twF = twL;
     const V* twI = twF;   // palindrome: the reversed plan's table is the forward one
     constexpr int XZ = RSP_K2_XOR;   // Ns = 1 outputs XOR-swizzled (see sh_store)
     shg_store<R0, false, NB0, SH, K2_THREADS, M, 1, XZ>(v0, rs, rows, StoreLds<V>{L}, tid);
     __syncthreads();
+    K2_STAMP(1);
     shg_pass<R1, false, NB1, SH, K2_THREADS, M, NS1, CMP, XZ>(L, rs, rows, twF, StoreLds<V>{L});
+    K2_STAMP(2);
     {
         V v[NB0][R0];
         shg_load<R0, false, NB0, SH, K2_THREADS, M, NS2, CMP>(L, rs, rows, twF + TW2, v, tid);
         RSP_WAR_SYNC();
+        const __amdgpu_buffer_rsrc_t hr = buf_rsrc(H + sd.H_off, (unsigned)(M * sizeof(V)));
 #pragma unroll
         for (int t = 0; t < NB0; ++t) {
             Dft<R0, false, V>::run(v[t]);
+            if constexpr (EPI) {
+                k2_apply_h<R0, nb0>(v[t], hr, tid);   // fused pass outputs j + r M/16
+            } else {
 #pragma unroll
-            for (int r = 0; r < R0; ++r) v[t][r] = vmul(v[t][r], hreg[t][r]);
+                for (int r = 0; r < R0; ++r) v[t][r] = vmul(v[t][r], hreg[t][r]);
+            }
         }
         shg_store<R0, true, NB0, SH, K2_THREADS, M, 1, XZ>(v, rs, rows, StoreLds<V>{L}, tid);
         __syncthreads();
     }
+    K2_STAMP(3);
     shg_pass<R1, true, NB1, SH, K2_THREADS, M, NS1, CMP, XZ>(L, rs, rows, twI, StoreLds<V>{L});
+    K2_STAMP(4);
     const int gend = min(sd.gb, g0 + sd.V);
-    {
-        static_assert(NS2 == nb0, "last pass: thread j's outputs are j + r NS2");
+    static_assert(NS2 == nb0, "last pass: thread j's outputs are j + r NS2");
+    if constexpr (EPI) {
+        shg_pass<R0, true, NB0, SH, K2_THREADS, M, NS2, CMP>(L, rs, rows, twI + TW2, StoreLds<V>{L});
+        k2_epilogue<T, SH>(L, rs, rows, row0, rows_total, Lh1, g0, gend, rdm, mag, G, g.Gp);
+    } else {
         V v[NB0][R0];
         shg_load<R0, true, NB0, SH, K2_THREADS, M, NS2, CMP>(L, rs, rows, twI + TW2, v, tid);
         if (rdm)
@@ -1372,11 +1474,21 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
     }
 }
 
-#ifndef RSP_K2_MINB
-#define RSP_K2_MINB (512 / K2_THREADS)   // workgroups per CU the compiler sizes k2_pc for
+// k2_pc<T, WGS>: sized for WGS workgroups per CU.  WGS = 3 (a complex-double plan with a
+// 2560-point block, Geometry::k2_pts = 2560: 53.5 KB of LDS and <= 168 VGPRs per workgroup) runs
+// the blocks with EPI (the filter spectrum loaded after the forward DFT, the kept gates stored by
+// k2_epilogue): without them the last pass peaks at 188 VGPRs.  WGS = 2 (4096-point workgroups,
+// 76 KB of LDS) keeps H in registers from the start and stores the gates from the last pass,
+// which measured faster at that occupancy (x2 at 2 per CU: 225 vs 248 us per 8 frames).
+#ifndef RSP_K2_EPI3
+#define RSP_K2_EPI3 1
 #endif
-template <class T>
-__global__ __launch_bounds__(K2_THREADS, RSP_K2_MINB) void k2_pc(Geometry g, DevConsts k, FramePtrs fp, int rows_total) {
+#ifndef RSP_K2_EPI2
+#define RSP_K2_EPI2 0
+#endif
+template <class T, int WGS>
+__global__ __launch_bounds__(K2_THREADS, WGS) void k2_pc(Geometry g, DevConsts k, FramePtrs fp, int rows_total) {
+    constexpr bool EPI = WGS >= 3 ? RSP_K2_EPI3 : RSP_K2_EPI2;
     typedef cx<T> V;
     V* L = reinterpret_cast<V*>(rsp_lds);   // overlap-save rows | narrow: staged rows + taps
     const int f = blockIdx.y;
@@ -1393,17 +1505,30 @@ __global__ __launch_bounds__(K2_THREADS, RSP_K2_MINB) void k2_pc(Geometry g, Dev
     const int P = g.P, G = g.G;
     const int lo = sd.lo, hi = sd.hi, off = sd.off;
     const int tid = threadIdx.x;
+    K2_STAMP(0);
+    K2_TAG((unsigned long long)(sd.type * 16 + sd.logM));
 
     if (sd.type == 1 && sd.logM == 0) {   // mixed-radix block
-        k2_fft_job_mix<T, 2560, 10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L);
+        k2_fft_job_mix<T, 2560, 10, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L);
     } else if (sd.type == 1) {
-        switch (sd.logM) {
-            case 6: k2_fft_job<T, 6>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-            case 7: k2_fft_job<T, 7>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-            case 8: k2_fft_job<T, 8>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-            case 9: k2_fft_job<T, 9>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-            case 10: k2_fft_job<T, 10>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-            default: k2_fft_job<T, 11>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+        if constexpr (WGS >= 3) {   // workgroups sized for the 2560-point block: 2048 points of 2^k rows
+            switch (sd.logM) {
+                case 6: k2_fft_job<T, 6, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                case 7: k2_fft_job<T, 7, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                case 8: k2_fft_job<T, 8, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                case 9: k2_fft_job<T, 9, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                case 10: k2_fft_job<T, 10, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                default: k2_fft_job<T, 11, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+            }
+        } else {
+            switch (sd.logM) {
+                case 6: k2_fft_job<T, 6, RSP_K2_POINTS, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                case 7: k2_fft_job<T, 7, RSP_K2_POINTS, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                case 8: k2_fft_job<T, 8, RSP_K2_POINTS, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                case 9: k2_fft_job<T, 9, RSP_K2_POINTS, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                case 10: k2_fft_job<T, 10, RSP_K2_POINTS, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                default: k2_fft_job<T, 11, RSP_K2_POINTS, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+            }
         }
     } else {
         // direct FIR (narrow segment): filter() + circshift(-fir_delay) (fsf:111-112).  Each
@@ -1437,6 +1562,7 @@ __global__ __launch_bounds__(K2_THREADS, RSP_K2_MINB) void k2_pc(Geometry g, Dev
         const T* __restrict__ taps = static_cast<const T*>(k.taps);
         for (int e = tid; e < sd.ntaps; e += K2_THREADS) tp[e] = taps[sd.taps_off + e];
         __syncthreads();
+        K2_STAMP(1);
         const int nout = sd.gb - sd.ga;
         // 4 consecutive gates per thread: the 4 outputs share a register window that slides one
         // sample per tap (1 LDS read + 4 FMAs per tap); a group whose circshift index wraps
@@ -1482,6 +1608,7 @@ __global__ __launch_bounds__(K2_THREADS, RSP_K2_MINB) void k2_pc(Geometry g, Dev
             }
         }
     }
+    K2_STAMP(5);
 }
 
 // ======================================================================================
@@ -2213,10 +2340,16 @@ hipError_t launch_k1(const Geometry& g, const DevConsts& k, const FramePtrs& fp,
 template <class T>
 static hipError_t launch_k2_p(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int rows,
                               hipStream_t s) {
-    const size_t lds = (size_t)(K2_LDS_DATA(k2_sh<T>()) + k2_tw_lds_max()) * sizeof(cx<T>);
-    hipError_t e = allow_lds(k2_pc<T>, lds);
+    const size_t lds = (size_t)(k2_lds_data(g.k2_pts, k2_sh<T>()) + k2_tw_lds_max()) * sizeof(cx<T>);
+    const bool w3 = g.k2_pts != RSP_K2_POINTS;   // workgroups sized for the 2560-point block: 3 per CU
+    hipError_t e = w3 ? allow_lds(k2_pc<T, 3>, lds) : allow_lds(k2_pc<T, 2>, lds);
     if (e != hipSuccess) return e;
-    if (g.nwg_k2 > 0) hipLaunchKernelGGL(k2_pc<T>, dim3(g.nwg_k2, nf), dim3(K2_THREADS), lds, s, g, k, fp, rows);
+    if (g.nwg_k2 > 0) {
+        if (w3)
+            hipLaunchKernelGGL((k2_pc<T, 3>), dim3(g.nwg_k2, nf), dim3(K2_THREADS), lds, s, g, k, fp, rows);
+        else
+            hipLaunchKernelGGL((k2_pc<T, 2>), dim3(g.nwg_k2, nf), dim3(K2_THREADS), lds, s, g, k, fp, rows);
+    }
     return hipGetLastError();
 }
 

@@ -397,7 +397,6 @@ int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga,
     const bool mix = !is_pow2(M);
     s.M = M; s.logM = mix ? 0 : ilog2i(M); s.V = M - Lh + 1;
     s.nblocks = (nout + s.V - 1) / s.V;
-    s.rows_per_wg = RSP_K2_POINTS / M;
     // spectrum of h zero-padded to M, natural order, 1/M folded in
     std::vector<cd> hm(M, 0.0);
     for (int i = 0; i < Lh; ++i) hm[i] = h[i];
@@ -879,14 +878,6 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
             hi = std::max(hi, top);
         }
         s.lo = lo; s.hi = hi;
-        const int W = hi - lo + 1;
-        const int WP = W + s.ntaps - 1;   // staged row: ntaps - 1 leading zeros (k2_pc narrow path)
-        // up to 8 rows per workgroup (measured best of 1/2/4/8 at x2), within the workgroup's LDS:
-        // rows * WP complex + the taps (ntaps reals = ntaps / 2 complex)
-        const int lds_c = RSP_K2_POINTS + (RSP_K2_POINTS >> 5);
-        s.rows_per_wg = std::max(1, std::min(8, (lds_c - (s.ntaps + 1) / 2) / WP));
-        if (WP * s.rows_per_wg + (s.ntaps + 1) / 2 > lds_c)
-            return bail(fail(RSP_ERR_UNSUPPORTED, "narrow segment window %d samples too long", W));
         s.taps_off = (int)taps.size();
         for (int j = 0; j < s.ntaps; ++j) taps.push_back(pre->MF_narrow[j]);
         p->segs.push_back(s);
@@ -905,9 +896,27 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
         if (rc) return bail(rc);
         p->segs.push_back(s);
     }
+    // K2 workgroup size in LDS points: a complex-double plan with a 2560-point block sizes every
+    // workgroup for it (53.5 KB of LDS: 3 per CU, k2_pc's 168-VGPR budget), power-of-two blocks
+    // then holding 2048 / M rows; otherwise RSP_K2_POINTS (4096: 2 per CU in complex double)
+    g.k2_pts = RSP_K2_POINTS;
+    for (auto& s : p->segs)
+        if (f64 && s.type == 1 && s.M == 2560) g.k2_pts = RSP_K2_MIXPTS;
     for (auto& s : p->segs) {
         if (s.seg_lo < 0 || s.seg_lo >= N) return bail(fail(RSP_ERR_INVALID, "segment start out of range"));
         if (s.hi >= s.lo) need.push_back({s.lo, s.hi});
+        if (s.type == 1) {
+            const int pts = (g.k2_pts == RSP_K2_POINTS) ? RSP_K2_POINTS : 2048;   // k2_pc's PTS
+            s.rows_per_wg = s.M == 2560 ? 1 : std::max(1, pts / s.M);
+        } else {
+            // up to 8 rows per workgroup (measured best of 1/2/4/8 at x2), within the workgroup's
+            // LDS: rows * WP complex + the taps (ntaps reals = ntaps / 2 complex)
+            const int WP = s.hi - s.lo + 1 + s.ntaps - 1;   // staged row: ntaps - 1 leading zeros
+            const int lds_c = g.k2_pts + (g.k2_pts >> 5);
+            s.rows_per_wg = std::max(1, std::min(8, (lds_c - (s.ntaps + 1) / 2) / WP));
+            if (WP * s.rows_per_wg + (s.ntaps + 1) / 2 > lds_c)
+                return bail(fail(RSP_ERR_UNSUPPORTED, "narrow segment window %d samples too long", s.hi - s.lo + 1));
+        }
     }
     // union of needed fast-time windows -> compacted sample list (K1 processes only these)
     std::sort(need.begin(), need.end(), [](const Interval& a, const Interval& b) { return a.lo < b.lo; });
