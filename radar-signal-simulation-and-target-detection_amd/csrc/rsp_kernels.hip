@@ -643,6 +643,24 @@ template <> struct Dbf<double> {
 template <class T, int MB>
 __device__ __forceinline__ void dbf_store(T* Yf, const typename Dbf<T>::Acc (&acc)[MB][Dbf<T>::NACC], int grp, int B,
                                           int NT, int Ppad, int nl, int p, const T (&w)[Dbf<T>::NACC], int sh) {
+    if constexpr (sizeof(T) == 8) {
+        // double: registers i and i + 2 hold Re and Im of the same beam (rows grp + 4 i and
+        // grp + 4 i + 8), so each beam's complex value goes out as one 16-B store.  Two 8-B
+        // stores of the parts at a 16-B lane stride put lanes l and l + 8 on the same banks of
+        // the 32-bank write path (2-way); the 16-B stores of 8 consecutive lanes cover the 32
+        // banks once.
+        const int ip = sh ? p + (p >> K1_SH) : p;
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int b = mb * 8 + ((grp + 4 * i) & 7);
+                if (b < B)
+                    reinterpret_cast<d2*>(Yf)[(b * NT + nl) * Ppad + ip] =
+                        d2{acc[mb][0][i] * w[0], acc[mb][0][i + 2] * w[0]};
+            }
+        return;
+    }
 #pragma unroll
     for (int a = 0; a < Dbf<T>::NACC; ++a) {
         const int pa = p + a;
@@ -1918,19 +1936,24 @@ __global__ __launch_bounds__(RSP_THREADS, RSP_K3_WGS) void k3_cfar(Geometry g, D
         constexpr int BL = floor4(DL), BR = floor4(DR);
         constexpr int NL = (DL + 3 + RR - BL + 3) / 4, NR = (DR + 3 + RR - BR + 3) / 4;
         constexpr int lgT = RTC == 64 ? 4 : 3;                    // log2 threads per row (RT / 4)
-        const int q = threadIdx.x & ((1 << lgT) - 1);
-        const int c = (NOH ? 0 : hR) + 4 * q;                     // first tile column of the group
-        const int r = c0 + c;
         // 16-lane row groups of a wave take rows {0, 2, 1, 3} + 4w: the ds_read_b128 lane groups
         // ({0-3,12-15,20-27}, ... MI355X_MICROARCH.md §LDS) then pair rows 2 apart, 2W = 192
         // floats = 0 mod 64 banks, conflict-free (adjacent rows, W = 96 = 32 mod 64, were 2-way)
         const int rg = threadIdx.x >> lgT;
         // complex double (8 threads per row, 32 B per thread, two ds_read_b128 of 16 lanes from 4
-        // row groups): with the 132-dword row stride, row groups 4a + {0, 1, 2, 3} take rows
-        // 2a + {0, 16, 1, 17}, whose bank offsets {0, 0, 4, 4} (mod 64) put the four lane sets of
-        // every ds_read_b128 on disjoint banks (2-way conflicted with 64-cell rows)
+        // row groups; row stride 34 doubles, so a 16-B slot's bank is (row + 2 q + base / 2) mod
+        // 16 slots): row groups 4a + {0, 1, 2, 3} take rows {0, 1, 8, 9} + 2 (a mod 4) + 16 (a / 4),
+        // and their column groups q are rotated by {0, 4, 4, 0}, so that each ds_read_b128 lane
+        // group holds four rows {0, 1, 8, 9} (+ x) of ONE half of the columns (q < 4 or q >= 4).
+        // Every lane of a group then reads at the same offset (the halo-less prefilter's right
+        // slice is read by q < 4 only, the left one by q >= 4), and rows + 2 q cover the 16 slots
+        // once.  (Rows 2a + {0, 16, 1, 17} with unrotated columns put the two slices in one lane
+        // group: 2-way on a quarter of the slots, 30 % of K3's LDS cycles.)
+        const int q = lgT == 3 ? ((threadIdx.x & 7) ^ (((rg ^ (rg >> 1)) & 1) << 2)) : threadIdx.x & ((1 << lgT) - 1);
+        const int c = (NOH ? 0 : hR) + 4 * q;                     // first tile column of the group
+        const int r = c0 + c;
         const int rgp = lgT == 4 ? (rg & ~3) | ((rg & 1) << 1) | ((rg >> 1) & 1)
-                                 : 2 * (rg >> 2) + ((rg & 1) << 4) + ((rg >> 1) & 1);
+                                 : (rg & 1) + ((rg & 2) << 2) + 2 * ((rg >> 2) & 3) + 16 * (rg >> 4);
 #if RSP_K3_PREFILTER
         // Exact prefilter.  A hit needs CUT > T mean(max of the four slices) >= T mean(left range
         // slice): quot() is the correctly rounded (double) or a monotone (float) quotient and the

@@ -681,12 +681,21 @@ __global__ __launch_bounds__(MU_THREADS, 2) void k_music_cov64(int N, int K, con
         ai[t] = ar[t];
     }
     const int nsteps = (K + 3) >> 2;
+    // the snapshots as one buffer resource: an element past the instance (k >= K or channel >= N)
+    // gets an out-of-range offset and reads 0, so the loads carry no branch -- a branch around
+    // each load made the compiler wait (vmcnt(0)) for it on the spot, and the loads issued two
+    // steps ahead did not overlap the MFMAs of the step between
+    const __amdgpu_buffer_rsrc_t xrs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<double2*>(Xi), (short)0, (int)((unsigned)K * (unsigned)N * 16u), 0x00020000);
     auto load = [&](int s, double (&xr)[4], double (&xi)[4]) {
         const int k = 4 * s + kk, c0 = 4 * r;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            double2 x = make_double2(0.0, 0.0);
-            if (k < K && c0 + i < N) x = Xi[(size_t)k * N + c0 + i];
+            // bit 31 set (past num_records) when k >= K or the channel >= N: arithmetic, not a
+            // select, which the compiler turned into a branch per load
+            const unsigned bad = ((unsigned)(K - 1 - k) | (unsigned)(N - 1 - c0 - i)) & 0x80000000u;
+            const unsigned off = (((unsigned)k * (unsigned)N + (unsigned)(c0 + i)) * 16u) | bad;
+            const double2 x = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(xrs, (int)off, 0, 0));
             xr[i] = x.x;
             xi[i] = x.y;
         }
@@ -707,16 +716,17 @@ __global__ __launch_bounds__(MU_THREADS, 2) void k_music_cov64(int N, int K, con
             }
     };
     double xr0[4], xi0[4], xr1[4], xi1[4];
-    int s = w;
-    if (s < nsteps) load(s, xr0, xi0);
-    if (s + 4 < nsteps) load(s + 4, xr1, xi1);
-    for (; s + 4 < nsteps; s += 8) {
+    // steps s and s + 4 per iteration, each one's loads issued two steps ahead; a step past the
+    // snapshots reads zeros (out-of-range offsets) and adds exact zeros, so the loop has no
+    // data-dependent branch around a load
+    load(w, xr0, xi0);
+    load(w + 4, xr1, xi1);
+    for (int s = w; s < nsteps; s += 8) {
         step(xr0, xi0);
-        if (s + 8 < nsteps) load(s + 8, xr0, xi0);
+        load(s + 8, xr0, xi0);
         step(xr1, xi1);
-        if (s + 12 < nsteps) load(s + 12, xr1, xi1);
+        load(s + 12, xr1, xi1);
     }
-    if (s < nsteps) step(xr0, xi0);
     for (int ww = 0; ww < 4; ++ww) {   // ordered cross-wave sum (deterministic)
         if (w == ww) {
 #pragma unroll
