@@ -468,6 +468,10 @@ int32_t rsp_music_synthesize_device(rsp_music_plan* plan, const rsp_music_scene*
  * averaged over `iters` launches on the plan's stream, in the peaks-only form of a call (the
  * eigenvalues not requested: complex double then finds only the M signal eigenvalues). */
 int32_t rsp_music_profile(rsp_music_plan* plan, const void* d_X, int32_t n_inst, int32_t iters, float* ms_out);
+/* Instances of the last call whose signal subspace came from the block-power fast path (complex
+ * double, peaks-only calls, M <= 4: the iteration converged with a proven 1e-12 subspace bound,
+ * rsp_music.hip me_fast_subspace); the others ran the full tridiagonal eigensolver.  Diagnostic. */
+int32_t rsp_music_fast_count(rsp_music_plan* plan, int32_t* n_fast);
 int32_t rsp_music_device_alloc(rsp_music_plan* plan, int64_t bytes, void** d_ptr);
 int32_t rsp_music_device_free(rsp_music_plan* plan, void* d_ptr);
 int32_t rsp_music_device_download(rsp_music_plan* plan, void* h_dst, const void* d_src, int64_t bytes);

@@ -778,6 +778,10 @@ __global__ __launch_bounds__(MU_THREADS, 2) void k_music_cov64(int N, int K, con
 // ---------------------------------------------------------------------------------------
 #define ME_THREADS 256
 #define ME_SECT 23     // multisection rounds with 4 interior points: 5^23 > 2^53
+#define ME_PW_MIN 3    // block power iterations of the fast path (each with A^2) before the first
+#define ME_PW_MAX 8    // convergence test, and at most (then the full path)
+
+
 #define ME_SECT65 9    // rounds with 64 interior points: 65^9 > 2^53
 // Floor of the squared off-diagonal entries the Sturm count reads (e2[], not ee[]): an exactly
 // zero minor p_r must act as dstebz's q_r = -pivmin, i.e. a sign change after which
@@ -799,7 +803,238 @@ __host__ __device__ constexpr size_t me_lds_bytes(int M, int S) {
            ((size_t)S + 8) * 8 + 8 * 16;
 }
 
+// ---- Fast path of a peaks-only call (the caller reads no eigenvalues, M <= 4): the signal
+// subspace span{q_1..q_M} of R -- all that den(s) = |a - Q_s Q_s^H a|^2 needs (MUSIC_1D.m:31-37)
+// -- by orthogonal (block power) iteration instead of the full tridiagonal eigensolver: steps
+// X <- orth(A^2 X) (CholeskyQR applied twice), M columns, tested for convergence after each step
+// from the ME_PW_MIN-th to the ME_PW_MAX-th.  Accepted only with a proof that
+// span(X) is within 1e-12 (sin of the largest principal angle) of the M leading eigenvectors:
+// with H = X^H A X, E = A X - X H and C the compression of A to span(X)'s complement,
+// ||A||_F^2 = ||H||_F^2 + 2 ||E||_F^2 + ||C||_F^2, so every eigenvalue of A outside the leading
+// M is <= ||C||_F + ||E||_F (Weyl) =: c; if H - mu I is positive definite for mu = c + (1 + 1e12)
+// ||E||_F (a Cholesky test), the gap between span(X)'s Ritz values and the rest exceeds 1e12
+// ||E||_F, and Davis-Kahan bounds the angle by ||E||_F / gap <= 1e-12.  Otherwise (a small gap:
+// slow convergence, or a matrix too degenerate for CholeskyQR) the caller runs the full path.  A
+// is scaled by a power of two (exact) so that the iteration's magnitudes stay near 1 at any
+// scale.  Uniform over the workgroup; lane t holds column i = t >> 2, rows 16 q .. +15 (q = t & 3).
+// Packed S x S Hermitian matrices (pidx): the diagonal (reals) then the upper triangle (re, im).
+template <int S>
+__host__ __device__ constexpr int pidx_d(int c) { return c; }
+template <int S>
+__host__ __device__ constexpr int pidx_o(int c, int d) {   // c < d: re at the index, im at + 1
+    int k = S;
+    for (int cc = 0; cc < S; ++cc)
+        for (int dd = cc + 1; dd < S; ++dd) {
+            if (cc == c && dd == d) return k;
+            k += 2;
+        }
+    return k;
+}
+// Cholesky of a packed S x S Hermitian matrix (in place: L's diagonal, L[d][c] for c < d stored at
+// pidx_o(c, d) as L[d][c]); false unless positive definite
+template <int S>
+__device__ __forceinline__ bool me_chol_p(double (&G)[S * S]) {
+    bool ok = true;
+#pragma unroll
+    for (int c = 0; c < S; ++c) {
+        double d = G[pidx_d<S>(c)];
+#pragma unroll
+        for (int k = 0; k < c; ++k) {
+            const int o = pidx_o<S>(k, c);   // L[c][k]
+            d -= G[o] * G[o] + G[o + 1] * G[o + 1];
+        }
+        ok = ok && d > 0.0 && d < 1e300;
+        const double lcc = sqrt(fmax(d, 1e-300)), il = 1.0 / lcc;
+        G[pidx_d<S>(c)] = lcc;
+#pragma unroll
+        for (int r = c + 1; r < S; ++r) {   // L[r][c] = (G[r][c] - sum_k L[r][k] conj(L[c][k])) / L[c][c]
+            const int o = pidx_o<S>(c, r);  // holds conj-pair G[c][r] = conj(G[r][c]) on entry
+            double xr = G[o], xi = -G[o + 1];
+#pragma unroll
+            for (int k = 0; k < c; ++k) {
+                const int orr = pidx_o<S>(k, r), oc = pidx_o<S>(k, c);   // L[r][k], L[c][k]
+                xr -= G[orr] * G[oc] + G[orr + 1] * G[oc + 1];
+                xi -= G[orr + 1] * G[oc] - G[orr] * G[oc + 1];
+            }
+            G[o] = xr * il;
+            G[o + 1] = xi * il;
+        }
+    }
+    return ok;
+}
+// y <- y L^{-H} for the row vector y (z L^H = y; L packed as me_chol_p leaves it)
+template <int S>
+__device__ __forceinline__ void me_trsm_p(double2 (&y)[S], const double (&L)[S * S]) {
+#pragma unroll
+    for (int d = 0; d < S; ++d) {
+        double2 v = y[d];
+#pragma unroll
+        for (int c = 0; c < d; ++c) {   // (L^H)[c][d] = conj(L[d][c])
+            const int o = pidx_o<S>(c, d);
+            v = zsub(v, zm(y[c], make_double2(L[o], -L[o + 1])));
+        }
+        y[d] = zsc(1.0 / L[pidx_d<S>(d)], v);
+    }
+}
+
 template <int M>
+__device__ bool me_fast_subspace(const double2 (&a)[16], int n, int t, int lane, int w, int i, int q,
+                                 double2* __restrict__ Qb, double2* __restrict__ Yb, double* __restrict__ gp,
+                                 double2* __restrict__ Qs) {
+    constexpr int S = M;
+    constexpr int NV = S * S;
+    const double2 z2 = make_double2(0.0, 0.0);
+    int gb = 0;   // the reduction scratch alternates between two halves (one barrier per sum)
+    // sum over the 64 rows (each quad's lane q == 0, or every lane: all) and the 4 waves
+    auto reduce = [&](double (&v)[NV], bool all) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k] = wsumd(all || q == 0 ? v[k] : 0.0);
+        double* g = gp + gb * 4 * NV;
+        if (lane == 0)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) g[w * NV + k] = v[k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k] = (g[k] + g[NV + k]) + (g[2 * NV + k] + g[3 * NV + k]);
+        gb ^= 1;
+    };
+    // packed X^H Y over the rows (x, y: this quad's row of X and Y)
+    auto herm = [&](const double2 (&x)[S], const double2 (&y)[S], double (&G)[NV]) {
+#pragma unroll
+        for (int c = 0; c < S; ++c) {
+            G[pidx_d<S>(c)] = zmc(x[c], y[c]).x;
+#pragma unroll
+            for (int d = c + 1; d < S; ++d) {
+                const double2 e = zmc(x[c], y[d]);
+                G[pidx_o<S>(c, d)] = e.x;
+                G[pidx_o<S>(c, d) + 1] = e.y;
+            }
+        }
+        reduce(G, false);
+    };
+    // the scale 2^-e with max |a_ij| in [1/2, 1) after it (a power of two: exact), and ||sA A||_F^2
+    double am = 0.0, a2 = 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        am = fmax(am, fmax(fabs(a[u].x), fabs(a[u].y)));
+        a2 = fma(a[u].x, a[u].x, fma(a[u].y, a[u].y, a2));
+    }
+    am = wmaxd(am);
+    if (lane == 0) gp[8 * NV + w] = am;
+    __syncthreads();
+    am = fmax(fmax(gp[8 * NV + 0], gp[8 * NV + 1]), fmax(gp[8 * NV + 2], gp[8 * NV + 3]));
+    if (!(am > 0.0) || !(am < 1e300)) return false;   // uniform
+    const double sA = __builtin_amdgcn_ldexp(1.0, -__builtin_amdgcn_frexp_exp(am));
+    {
+        double v[NV];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k] = 0.0;
+        v[0] = a2 * sA * sA;
+        reduce(v, true);
+        a2 = v[0];
+    }
+    // y = sA A X (A Hermitian: row i of A X = sum_j conj(A(j, i)) X[j], quad i's column)
+    auto matvec = [&](const double2* X, double2 (&y)[S]) {
+#pragma unroll
+        for (int c = 0; c < S; ++c) {
+            double px4[4] = {0.0, 0.0, 0.0, 0.0}, py4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const double2 xj = X[c * ME_VW + ME_PX(16 * q + u)];
+                px4[u & 3] = fma(a[u].x, xj.x, fma(a[u].y, xj.y, px4[u & 3]));
+                py4[u & 3] = fma(a[u].x, xj.y, fma(-a[u].y, xj.x, py4[u & 3]));
+            }
+            const double px = qsumd((px4[0] + px4[1]) + (px4[2] + px4[3]));
+            const double py = qsumd((py4[0] + py4[1]) + (py4[2] + py4[3]));
+            y[c] = make_double2(px * sA, py * sA);
+            __builtin_amdgcn_sched_barrier(0);   // one column's 16 LDS loads in flight at a time (128 VGPRs)
+        }
+    };
+    // start: fixed unit-modulus vectors (deterministic; not orthogonal to an eigenvector in practice)
+    for (int e = t; e < S * 64; e += ME_THREADS) {
+        const int c = e >> 6, j = e & 63;
+        double sn, cs;
+        sincos(0.7 * (double)(j * (2 * c + 1)) + 1.3 * (double)c, &sn, &cs);
+        Qb[c * ME_VW + ME_PX(j)] = j < n ? make_double2(cs, sn) : z2;
+    }
+    __syncthreads();
+    bool ok = true, conv = false;
+    double2 x[S];
+    for (int it = 0; it < ME_PW_MAX && ok && !conv; ++it) {   // uniform
+        {
+            double2 y[S], z[S];
+            matvec(Qb, y);
+            if (q == 0)
+#pragma unroll
+                for (int c = 0; c < S; ++c) Yb[c * ME_VW + ME_PX(i)] = y[c];
+            __syncthreads();
+            matvec(Yb, z);   // sA^2 A^2 X
+#pragma unroll
+            for (int pass = 0; pass < 2; ++pass) {   // CholeskyQR2: orthonormal to rounding
+                double G[NV];
+                herm(z, z, G);
+                ok = me_chol_p<S>(G) && ok;
+                me_trsm_p<S>(z, G);
+            }
+            if (q == 0)
+#pragma unroll
+                for (int c = 0; c < S; ++c) Qb[c * ME_VW + ME_PX(i)] = z[c];
+            __syncthreads();
+#pragma unroll
+            for (int c = 0; c < S; ++c) x[c] = z[c];
+        }
+        if (!ok || it + 1 < ME_PW_MIN) continue;
+        // the proof of convergence (see above): H = X^H A X, E = A X - X H, c bounds the rest
+        double2 y[S];
+        matvec(Qb, y);
+        double H[NV];
+        herm(x, y, H);
+        double h2 = 0.0, e2 = 0.0;
+#pragma unroll
+        for (int c = 0; c < S; ++c) {
+            h2 += H[pidx_d<S>(c)] * H[pidx_d<S>(c)];
+#pragma unroll
+            for (int d = c + 1; d < S; ++d)
+                h2 += 2.0 * (H[pidx_o<S>(c, d)] * H[pidx_o<S>(c, d)] + H[pidx_o<S>(c, d) + 1] * H[pidx_o<S>(c, d) + 1]);
+        }
+#pragma unroll
+        for (int j = 0; j < S; ++j) {   // row i of E, column j
+            double2 e = y[j];
+#pragma unroll
+            for (int k = 0; k < S; ++k) {
+                const double2 hkj = k == j ? make_double2(H[pidx_d<S>(k)], 0.0)
+                                           : (k < j ? make_double2(H[pidx_o<S>(k, j)], H[pidx_o<S>(k, j) + 1])
+                                                    : make_double2(H[pidx_o<S>(j, k)], -H[pidx_o<S>(j, k) + 1]));
+                e = zsub(e, zm(x[k], hkj));
+            }
+            e2 += e.x * e.x + e.y * e.y;
+        }
+        {
+            double v[NV];
+#pragma unroll
+            for (int k = 0; k < NV; ++k) v[k] = 0.0;
+            v[0] = e2;
+            reduce(v, false);
+            e2 = v[0];
+        }
+        // (1e-14 a2: the rounding of the difference, so that cb stays an upper bound)
+        const double en = sqrt(e2), cb = sqrt(fmax(a2 - h2 - 2.0 * e2, 0.0) + 1e-14 * a2);
+        const double mu = cb + en * (1.0 + 1e12);
+#pragma unroll
+        for (int c = 0; c < S; ++c) H[pidx_d<S>(c)] -= mu;
+        conv = me_chol_p<S>(H);   // H - mu I positive definite: the proof holds (uniform)
+    }
+    if (!conv) return false;   // uniform
+    if (q == 0)
+#pragma unroll
+        for (int j = 0; j < M; ++j) Qs[j * 64 + i] = x[j];
+    __syncthreads();
+    return true;
+}
+
+// FAST (peaks-only launches, neig <= 4): try me_fast_subspace first.  A separate instantiation, so
+// that the launches that read every eigenvalue run the full path without the fast path's registers.
+template <int M, bool FAST>
 __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S, int neig, const double2* __restrict__ R,
                                                           const double2* __restrict__ S1T, int Spad,
                                                           double* __restrict__ spec_db, double* __restrict__ eig_out,
@@ -837,6 +1072,17 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
             a[u] = (i < n && j < n) ? Ri[j + MU_NMAX * i] : z2;
         }
     }
+    // ---- 0. peaks-only calls: the signal subspace by block power iteration when it converges
+    //         (me_fast_subspace); otherwise, and whenever every eigenvalue is requested, 1.-3.
+    bool fast = false;
+    if constexpr (FAST && M <= 4) {
+        if (neig <= 4 && M + 1 <= n) {
+            double2* Qb = reinterpret_cast<double2*>(lu);
+            fast = me_fast_subspace<M>(a, n, t, lane, w, i, q, Qb, Qb + (M + 1) * ME_VW,
+                                       reinterpret_cast<double*>(Qb + 2 * (M + 1) * ME_VW), Qs);
+        }
+    }
+    if (!fast) {
     // ---- 1. tridiagonalisation
     for (int k = 0; k < n - 1; ++k) {
         double2* vk = vb + ME_VW * (k & 1);
@@ -928,7 +1174,7 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
         double dl = 0.0;
 #pragma unroll
         for (int u = 0; u < 16; ++u)
-            if (i == n - 1 && 16 * q + u == n - 1) dl = a[u].x;
+            if (u == ((n - 1) & 15) && i == n - 1 && q == ((n - 1) >> 4)) dl = a[u].x;   // u vs a uniform: no per-lane row index
         dl = qsumd(dl);
         if (i == n - 1 && q == 0) dd[n - 1] = dl;
     }
@@ -1180,6 +1426,7 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
         }
         __syncthreads();
     }
+    }   // !fast
     ME_STAMP(4);
     // ---- 4. den(s) = |a(s) - Q_s (Q_s^H a(s))|^2, lane = angle
     for (int s = t; s < S; s += ME_THREADS) {
@@ -1234,7 +1481,9 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
     if (lane == 0) ired[w] = npk;
     __syncthreads();
     int* po = peaks_out + (size_t)blockIdx.x * (MU_MMAX + 1);
-    if (t == 0) po[0] = (ired[0] + ired[1]) + (ired[2] + ired[3]);
+    if (t == 0) {
+        po[0] = (ired[0] + ired[1]) + (ired[2] + ired[3]);
+    }
     __syncthreads();
     for (int rk = 0; rk < M; ++rk) {
         double bv = -1.0e300;
@@ -1266,8 +1515,10 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
         if (t == 0) po[1 + rk] = gs < (1 << 30) ? gs + 1 : 0;
         __syncthreads();
     }
-    if (t == 0)
+    if (t == 0) {
         for (int rk = M; rk < MU_MMAX; ++rk) po[1 + rk] = 0;
+        if (M < MU_MMAX) po[MU_MMAX] = fast ? 1 : 0;   // the slot past the M peaks: which path ran (rsp_music_fast_count)
+    }
     ME_STAMP(6);
 #undef ME_STAMP
 }
@@ -1294,6 +1545,7 @@ struct rsp_music_plan {
     double* d_amp = nullptr;      // [MU_MMAX]
     unsigned long long* d_trace = nullptr;   // RSP_MUSIC_TRACE: [max_batch][8] phase stamps (f32 eig)
     hipEvent_t ev[4] = {};
+    int last_inst = 0;            // instances of the last eig launch (rsp_music_fast_count)
 };
 
 namespace {
@@ -1309,14 +1561,21 @@ namespace {
 template <int MC>
 hipError_t launch_eig64(rsp_music_plan* p, int n_inst, int neig) {
     const size_t lds = me_lds_bytes(MC, p->S);
+    const bool fast = neig <= 4 && MC <= 4;   // peaks-only: the fast-path instantiation
+    const void* kf = fast ? reinterpret_cast<const void*>(k_music_eig64<MC, true>)
+                          : reinterpret_cast<const void*>(k_music_eig64<MC, false>);
     if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_music_eig64<MC>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipError_t e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_music_eig64<MC>, dim3(n_inst), dim3(ME_THREADS), lds, p->stream, p->N, p->S, neig,
-                       (const double2*)p->d_R, (const double2*)p->d_S1T, p->Spad, (double*)p->d_spec,
-                       (double*)p->d_eig, p->d_peaks, p->d_trace);
+    if (fast)
+        hipLaunchKernelGGL((k_music_eig64<MC, true>), dim3(n_inst), dim3(ME_THREADS), lds, p->stream, p->N, p->S, neig,
+                           (const double2*)p->d_R, (const double2*)p->d_S1T, p->Spad, (double*)p->d_spec,
+                           (double*)p->d_eig, p->d_peaks, p->d_trace);
+    else
+        hipLaunchKernelGGL((k_music_eig64<MC, false>), dim3(n_inst), dim3(ME_THREADS), lds, p->stream, p->N, p->S,
+                           neig, (const double2*)p->d_R, (const double2*)p->d_S1T, p->Spad, (double*)p->d_spec,
+                           (double*)p->d_eig, p->d_peaks, p->d_trace);
     return hipGetLastError();
 }
 
@@ -1338,6 +1597,7 @@ int music_run(rsp_music_plan* p, const void* dX, int n_inst, bool timed, float* 
                            (const float2*)dX, (float2*)p->d_R);
     MUCHK(hipGetLastError());
     if (timed) MUCHK(hipEventRecord(p->ev[1], p->stream));
+    p->last_inst = n_inst;
     if (p->f64) {
         switch (p->M) {
 #define MU_EIG64(MC) \
@@ -1623,6 +1883,18 @@ int32_t rsp_music_device_free(rsp_music_plan* p, void* d_ptr) {
     MUCHK(hipSetDevice(p->device));
     MUCHK(hipStreamSynchronize(p->stream));
     MUCHK(hipFree(d_ptr));
+    return RSP_OK;
+}
+
+int32_t rsp_music_fast_count(rsp_music_plan* p, int32_t* n_fast) {
+    if (!p || !n_fast) return rsp_set_error(RSP_ERR_INVALID, "bad argument");
+    *n_fast = 0;
+    if (!p->f64 || p->M >= MU_MMAX || p->last_inst < 1) return RSP_OK;   // only complex double, M <= 4, sets it
+    MUCHK(hipSetDevice(p->device));
+    MUCHK(hipStreamSynchronize(p->stream));
+    std::vector<int> pk((size_t)p->last_inst * (MU_MMAX + 1));
+    MUCHK(hipMemcpy(pk.data(), p->d_peaks, pk.size() * sizeof(int), hipMemcpyDeviceToHost));
+    for (int i = 0; i < p->last_inst; ++i) *n_fast += pk[(size_t)i * (MU_MMAX + 1) + MU_MMAX] == 1;
     return RSP_OK;
 }
 

@@ -196,6 +196,7 @@ PROTOTYPES = {
     'rsp_music_process_device': (ct.c_int32, [_P, _P, ct.c_int32, ct.POINTER(MusicOut)]),
     'rsp_music_synthesize_device': (ct.c_int32, [_P, ct.POINTER(MusicScene), ct.c_int32, ct.c_int32, ct.c_uint64, _P]),
     'rsp_music_profile': (ct.c_int32, [_P, _P, ct.c_int32, ct.c_int32, ct.POINTER(ct.c_float)]),
+    'rsp_music_fast_count': (ct.c_int32, [_P, ct.POINTER(ct.c_int32)]),
     'rsp_music_device_alloc': (ct.c_int32, [_P, ct.c_int64, ct.POINTER(_P)]),
     'rsp_music_device_free': (ct.c_int32, [_P, _P]),
     'rsp_music_device_download': (ct.c_int32, [_P, _P, _P, ct.c_int64]),

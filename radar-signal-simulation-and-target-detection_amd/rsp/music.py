@@ -85,6 +85,23 @@ class MusicPlan:
         _abi.check(self._lib.rsp_music_process(self._h, buf.ctypes.data, dt, n, ct.byref(st)))
         return self._finish(o)
 
+    def peaks(self, X):
+        """rsp_music_process on host snapshots with only the peaks requested (the eigenvalues not
+        read): (peak indices [n, M] 1-based, findpeaks counts [n])."""
+        X = np.asarray(X)
+        if X.ndim == 2:
+            X = X[None]
+        n = X.shape[0]
+        buf = np.ascontiguousarray(np.transpose(X.astype(np.complex128 if self.cdtype == np.complex128 else np.complex64),
+                                                (0, 2, 1)))
+        pk = np.zeros((n, self.M), np.int32)
+        npk = np.zeros(n, np.int32)
+        st = _abi.MusicOut(None, None, pk.ctypes.data_as(ct.POINTER(ct.c_int32)),
+                           npk.ctypes.data_as(ct.POINTER(ct.c_int32)), None)
+        dt = _abi.RSP_C128 if buf.dtype == np.complex128 else _abi.RSP_C64
+        _abi.check(self._lib.rsp_music_process(self._h, buf.ctypes.data, dt, n, ct.byref(st)))
+        return pk, npk
+
     # ---- device-resident path (bench) ------------------------------------------------------
     def device_alloc(self, n_inst):
         p = ct.c_void_p()
@@ -121,6 +138,12 @@ class MusicPlan:
         st = _abi.MusicOut(None, None, peaks.ctypes.data_as(ct.POINTER(ct.c_int32)),
                            n_peaks.ctypes.data_as(ct.POINTER(ct.c_int32)), None)
         _abi.check(self._lib.rsp_music_process_device(self._h, ct.c_void_p(d_X), n_inst, ct.byref(st)))
+
+    def fast_count(self):
+        """Instances of the last call answered by the block-power fast path (rsp_music_fast_count)."""
+        n = ct.c_int32()
+        _abi.check(self._lib.rsp_music_fast_count(self._h, ct.byref(n)))
+        return n.value
 
     def profile(self, d_X, n_inst, iters=20):
         ms = (ct.c_float * 2)()

@@ -132,7 +132,7 @@ def music_case(request):
     prof = plan.profile(d_X, n_inst, iters=2)
     ref = [mu.music_1d(X[i].astype(np.complex128), M, scan, dl) for i in range(n_inst)]
     yield dict(N=N, K=K, M=M, scene=scene, scan=scan, dl=dl, X=X, out=out, ref=ref, plan=plan, prof=prof,
-               n=n_inst, tol=TOL[prec], prec=prec)
+               n=n_inst, tol=TOL[prec], prec=prec, name=name)
     plan.device_free(d_X)
     plan.close()
 
@@ -206,6 +206,60 @@ def test_music_peaks_only_call_equals_full_call(music_case):
         c['plan'].device_free(d_X)
     assert np.array_equal(peaks, c['out']['peaks'])
     assert np.array_equal(npk, c['out']['n_peaks'])
+    if c['prec'] == 'c128' and c['name'] in ('config5', 'music_1d'):
+        # complex double answers these scenes through the block-power fast path (every instance
+        # converges with the proven subspace bound); the full call above ran the full eigensolver
+        assert c['plan'].fast_count() == n
+
+
+@pytest.mark.gpu
+def test_music_fast_path_falls_back_on_a_small_gap():
+    """A covariance whose M-th and (M+1)-th eigenvalues are nearly equal: the block power
+    iteration cannot prove convergence in its fixed steps, so every instance must take the full
+    eigensolver -- and the peaks-only call still equals the full call."""
+    from rsp.music import MusicPlan
+    N, K, M = 16, 64, 2
+    scan = np.linspace(-np.pi / 2, np.pi / 2, 50)
+    rng = np.random.default_rng(7)
+    mags = np.concatenate([[9.0, 1.0 + 1e-3, 1.0], rng.uniform(0.2, 0.5, N - 3)])   # lambda_2 ~ lambda_3
+    Q, _ = np.linalg.qr(rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N)))
+    X = np.zeros((2, N, K), np.complex128)
+    for i in range(2):   # X X^H / K = Q diag(mags) Q^H exactly: X = Q sqrt(K mags) on N snapshots
+        X[i, :, :N] = Q @ np.diag(np.sqrt(mags * K))
+    plan = MusicPlan(N, K, M, scan, 0.5, max_batch=2)
+    try:
+        full = plan.process(X)
+        assert plan.fast_count() == 0   # the full call (every eigenvalue requested)
+        pk, npk = plan.peaks(X)
+        assert plan.fast_count() == 0   # peaks-only: lambda_3 / lambda_2 ~ 1, no proof in 8 powers
+        assert np.array_equal(pk, full['peaks']) and np.array_equal(npk, full['n_peaks'])
+    finally:
+        plan.close()
+    ev = np.sort(full['eig'][0])[::-1][:3]
+    assert np.abs(ev - [9.0, 1.001, 1.0]).max() <= 1e-12 * 9.0
+
+
+@pytest.mark.gpu
+def test_music_fast_path_taken_on_well_separated_signals():
+    """The converse: a large gap (lambda_2 / lambda_3 = 100) converges in the fixed steps, so the
+    peaks-only call takes the fast path for every instance and equals the full call."""
+    from rsp.music import MusicPlan
+    N, K, M = 16, 64, 2
+    scan = np.linspace(-np.pi / 2, np.pi / 2, 50)
+    rng = np.random.default_rng(8)
+    mags = np.concatenate([[900.0, 100.0], rng.uniform(0.5, 1.0, N - 2)])
+    Q, _ = np.linalg.qr(rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N)))
+    X = np.zeros((2, N, K), np.complex128)
+    for i in range(2):
+        X[i, :, :N] = Q @ np.diag(np.sqrt(mags * K))
+    plan = MusicPlan(N, K, M, scan, 0.5, max_batch=2)
+    try:
+        full = plan.process(X)
+        pk, npk = plan.peaks(X)
+        assert plan.fast_count() == 2
+    finally:
+        plan.close()
+    assert np.array_equal(pk, full['peaks']) and np.array_equal(npk, full['n_peaks'])
 
 
 @pytest.mark.gpu
