@@ -38,9 +38,10 @@ def main():
             res[k] = int(round((2 * f[k] + w[k]) * 1024))
     res['_raw'] = {k: {'FETCH_SIZE_KiB': f.get(k), 'WRITE_SIZE_KiB': w.get(k)} for k in sorted(set(f) | set(w))
                    if k.startswith('k')}
+    # PMC_DRIVER: the program the two passes ran (tools/prof_stages.py, or tools/music_prof.py)
     res['_note'] = ('bytes per launch = 2*FETCH_SIZE + WRITE_SIZE (KiB*1024), median over launches of '
-                    'tools/prof_stages.py ' + ' '.join(sys.argv[4:]))
-    if len(sys.argv) > 6:
+                    + os.environ.get('PMC_DRIVER', 'tools/prof_stages.py') + ' ' + ' '.join(sys.argv[4:]))
+    if len(sys.argv) > 6 and 'PMC_DRIVER' not in os.environ:
         res['_frames_per_launch'] = int(sys.argv[6])
     # the code the counters were collected on: bench.py reports this file's traffic for a kernel
     # only while the built kernel still has the same hash (tools/kernel_hashes.py)
