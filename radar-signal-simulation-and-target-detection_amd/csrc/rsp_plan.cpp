@@ -359,7 +359,7 @@ struct Interval { int lo, hi; };
 
 int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga, int gb, int seg_lo,
                       std::vector<cd>& H, std::vector<cd>& twM, std::vector<int>& tw_sizes, std::vector<int>& tw_offs,
-                      const char* name) {
+                      const char* name, double mix_w) {
     std::vector<cd> h(Nfft);
     for (int i = 0; i < Nfft; ++i) h[i] = cd(mf_fft[2 * i], mf_fft[2 * i + 1]);
     fft_d(h, +1);
@@ -389,7 +389,7 @@ int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga,
         const int V = M - Lh + 1;
         if (M == 0 || V < 1) continue;
         const int nb = (nout + V - 1) / V;
-        const double cost = (double)nb * M * (std::log2((double)M) + 2);
+        const double cost = (double)nb * M * (std::log2((double)M) + 2) * (is_pow2(M) ? 1.0 : mix_w);
         if (cost < best * 0.999) { best = cost; bestM = M; }
     }
     if (!bestM) return fail(RSP_ERR_UNSUPPORTED, "%s filter length %d exceeds the 2048-point block", name, Lh);
@@ -882,17 +882,22 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
         for (int j = 0; j < s.ntaps; ++j) taps.push_back(pre->MF_narrow[j]);
         p->segs.push_back(s);
     }
+    // the cost model's weight on the mixed-radix 2560-point block (complex double, where such a
+    // plan runs k2_pc at 3 workgroups per CU)
+#ifndef RSP_K2_MIXW
+#define RSP_K2_MIXW 1.0
+#endif
     if (g2 > 0) {
         SegDesc s{};
         int rc = build_fft_segment(s, pre->MF_medium_fft, pre->N_fft_med, N, g1, g1 + g2, pre->seg_start_medium - 1, H,
-                                   twM, tw_sizes, tw_offs, "medium");
+                                   twM, tw_sizes, tw_offs, "medium", f64 ? RSP_K2_MIXW : 1.0);
         if (rc) return bail(rc);
         p->segs.push_back(s);
     }
     if (g3 > 0) {
         SegDesc s{};
         int rc = build_fft_segment(s, pre->MF_long_fft, pre->N_fft_long, N, g1 + g2, G, pre->seg_start_long - 1, H, twM,
-                                   tw_sizes, tw_offs, "long");
+                                   tw_sizes, tw_offs, "long", f64 ? RSP_K2_MIXW : 1.0);
         if (rc) return bail(rc);
         p->segs.push_back(s);
     }
