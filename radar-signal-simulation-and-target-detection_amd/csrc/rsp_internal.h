@@ -16,6 +16,12 @@
 #ifndef RSP_K2_POINTS
 #define RSP_K2_POINTS 4096   // complex points per pulse-compression workgroup (Geometry::k2_pts)
 #endif
+#ifndef RSP_K2_M1024MIX
+#define RSP_K2_M1024MIX 0    // 3-per-CU K2 plans run 1024-point blocks as 8 x 16 x 8 (1) or 16 x 4 x 16 (0)
+#endif
+#ifndef RSP_K2_MODE3_ALL
+#define RSP_K2_MODE3_ALL 0   // every complex-double plan runs k2_pc at 3 workgroups per CU (A/B builds)
+#endif
 #ifndef RSP_K2_MIXPTS
 #define RSP_K2_MIXPTS 2560   // Geometry::k2_pts of a complex-double plan with a 2560-point block
 #endif

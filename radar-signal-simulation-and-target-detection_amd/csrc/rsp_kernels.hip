@@ -1387,26 +1387,28 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     }
 }
 
-// Mixed-radix overlap-save block M = 16 x R1 x 16 (2560 = 16 x 10 x 16): one block of M = 2560
-// covers x2's long segment (Lh = 700, 1860 gates), which takes two 2048-point blocks in powers of
-// two -- 37.5% fewer points.  One row per workgroup: the radix-16 passes run 160 butterflies
-// (waves 0-2, the fourth wave skips them), the radix-10 passes 256.  The plan is a palindrome,
-// so the inverse FFT runs the same radices, the fused middle pass (forward radix-16 pass, x H,
-// inverse radix-16 pass 0) has the same butterflies on both sides as in k2_fft_job, and the
-// inverse twiddle table equals the forward one (conjugated in load_tw).
-template <class T, int M, int R1, bool EPI>
+// Mixed-radix overlap-save block M = R0 x R1 x R0, a palindrome: the inverse FFT runs the same
+// radices, the fused middle pass (forward last pass, x H, inverse pass 0) has the same
+// butterflies on both sides as in k2_fft_job, and the inverse twiddle table equals the forward
+// one (conjugated in load_tw).  Two plans:
+//  - 2560 = 16 x 10 x 16: one block covers x2's long segment (Lh = 700, 1860 gates), which takes
+//    two 2048-point blocks in powers of two -- 37.5% fewer points.  One row per workgroup: the
+//    radix-16 passes run 160 butterflies (waves 0-2, the fourth wave skips them), the radix-10
+//    passes 256.
+//  - 1024 = 8 x 16 x 8 in workgroups sized for 2048 points (the 3-per-CU plans): two rows, and
+//    the three Ns = 1 / fused / last passes run 2 x 128 radix-8 butterflies on all 256 threads;
+//    as 16 x 4 x 16 those passes ran 2 x 64 radix-16 butterflies on half of them.
+template <class T, int M, int R0, int R1, bool EPI>
 __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConsts& k, const SegDesc& sd, const K2Job& job,
                                                const cx<T>* __restrict__ z, cx<T>* __restrict__ rdm, T* __restrict__ mag,
                                                int row0, int rows_total, cx<T>* L) {
     typedef cx<T> V;
     constexpr int SH = k2_sh<T>();
-    constexpr int R0 = 16;
     static_assert(M == R0 * R1 * R0, "palindromic 3-pass plan");
-    constexpr int rows = RSP_K2_POINTS / M;
-    static_assert(rows >= 1, "block larger than the workgroup");
+    constexpr int rows = M >= 2048 ? 1 : 2048 / M;
     constexpr int rs = M + (M >> SH);
     constexpr bool CMP = RSP_K2_CMP;
-    constexpr int nb0 = M / R0;                                          // radix-16 butterflies per row
+    constexpr int nb0 = M / R0;                                          // radix-R0 butterflies per row
     constexpr int NB0 = (nb0 * rows + K2_THREADS - 1) / K2_THREADS;
     constexpr int NB1 = ((M / R1) * rows + K2_THREADS - 1) / K2_THREADS;
     constexpr int NS1 = R0, NS2 = R0 * R1;                               // Ns of passes 1 and 2
@@ -1420,14 +1422,17 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
     const int a = sd.seg_lo + g0 - Lh1;
     const V* twl = static_cast<const V*>(k.twM) + sd.tw_off;
     const V* __restrict__ H = static_cast<const V*>(k.H);
-    static_assert(rows == 1 && NB0 == 1, "one row per workgroup, one radix-16 butterfly per thread");
+    static_assert(NB0 == 1, "one radix-R0 butterfly per thread");
+    static_assert(rows == 1 || nb0 % 64 == 0, "a row per whole wave (its z window is a scalar resource)");
+    static_assert(!EPI || rows * rs + NTWF <= k2_lds_data(2560, SH) + k2_tw_lds_max(), "fits the 3-per-CU LDS");
     V v0[NB0][R0];
     V hreg[EPI ? 1 : NB0][R0];   // !EPI: the fused pass's H, loaded with the samples
-    // threads nb0.. have no radix-16 butterfly (waves past nb0 skip the loads); the row's samples
-    // are one scalar buffer window (zrow_window), so the loads need no masks
-    if (tid < nb0) {
-        const ZWin zw = zrow_window(g, z, row0, rows_total, off, lo, hi);
-        const int j = tid;
+    // threads past the rows' butterflies (waves past them) skip the loads; a row's samples are one
+    // scalar buffer window (zrow_window), so the loads need no masks
+    const int rl = rows == 1 ? 0 : __builtin_amdgcn_readfirstlane(tid / nb0);
+    const int j = tid - rl * nb0;
+    if (tid < nb0 * rows) {
+        const ZWin zw = zrow_window(g, z, row0 + rl, rows_total, off, lo, hi);
         const int np0 = a + j - lo + off;
         if ((nb0 & (g.NZ - 1)) == 0) {   // uniform
             const unsigned e0 = (unsigned)zw.rel(np0) * (unsigned)sizeof(V), st = (unsigned)(nb0 * P) * (unsigned)sizeof(V);
@@ -1440,7 +1445,7 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
         if constexpr (!EPI) {
             const __amdgpu_buffer_rsrc_t hr = buf_rsrc(H + sd.H_off, (unsigned)(M * sizeof(V)));
 #pragma unroll
-            for (int r = 0; r < R0; ++r)   // fused pass outputs j + r M/16
+            for (int r = 0; r < R0; ++r)   // fused pass outputs j + r M/R0
                 hreg[0][r] = buf_ld<V>(hr, (unsigned)(j + r * nb0) * (unsigned)sizeof(V));
         }
     }
@@ -1448,7 +1453,7 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
     for (int e = threadIdx.x; e < NTWF; e += K2_THREADS) twL[e] = twl[e];
     const V* twF = twL;
     const V* twI = twF;   // palindrome: the reversed plan's table is the forward one
-    constexpr int XZ = RSP_K2_XOR;   // Ns = 1 outputs XOR-swizzled (see sh_store)
+    constexpr int XZ = R0 == 16 ? RSP_K2_XOR : 0;   // Ns = 1 outputs XOR-swizzled (see sh_store)
     shg_store<R0, false, NB0, SH, K2_THREADS, M, 1, XZ>(v0, rs, rows, StoreLds<V>{L}, tid);
     __syncthreads();
     K2_STAMP(1);
@@ -1463,7 +1468,7 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
         for (int t = 0; t < NB0; ++t) {
             Dft<R0, false, V>::run(v[t]);
             if constexpr (EPI) {
-                k2_apply_h<R0, nb0>(v[t], hr, tid);   // fused pass outputs j + r M/16
+                k2_apply_h<R0, nb0>(v[t], hr, j);   // fused pass outputs j + r M/R0
             } else {
 #pragma unroll
                 for (int r = 0; r < R0; ++r) v[t][r] = vmul(v[t][r], hreg[t][r]);
@@ -1476,11 +1481,11 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
     shg_pass<R1, true, NB1, SH, K2_THREADS, M, NS1, CMP, XZ>(L, rs, rows, twI, StoreLds<V>{L});
     K2_STAMP(4);
     const int gend = min(sd.gb, g0 + sd.V);
-    static_assert(NS2 == nb0, "last pass: thread j's outputs are j + r NS2");
     if constexpr (EPI) {
         shg_pass<R0, true, NB0, SH, K2_THREADS, M, NS2, CMP>(L, rs, rows, twI + TW2, StoreLds<V>{L});
         k2_epilogue<T, SH>(L, rs, rows, row0, rows_total, Lh1, g0, gend, rdm, mag, G, g.Gp);
     } else {
+        static_assert(EPI || (rows == 1 && NS2 == nb0), "last pass: thread j's outputs are j + r NS2 of one row");
         V v[NB0][R0];
         shg_load<R0, true, NB0, SH, K2_THREADS, M, NS2, CMP>(L, rs, rows, twI + TW2, v, tid);
         if (rdm)
@@ -1527,7 +1532,7 @@ __global__ __launch_bounds__(K2_THREADS, WGS) void k2_pc(Geometry g, DevConsts k
     K2_TAG((unsigned long long)(sd.type * 16 + sd.logM));
 
     if (sd.type == 1 && sd.logM == 0) {   // mixed-radix block
-        k2_fft_job_mix<T, 2560, 10, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L);
+        k2_fft_job_mix<T, 2560, 16, 10, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L);
     } else if (sd.type == 1) {
         if constexpr (WGS >= 3) {   // workgroups sized for the 2560-point block: 2048 points of 2^k rows
             switch (sd.logM) {
@@ -1535,7 +1540,12 @@ __global__ __launch_bounds__(K2_THREADS, WGS) void k2_pc(Geometry g, DevConsts k
                 case 7: k2_fft_job<T, 7, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
                 case 8: k2_fft_job<T, 8, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
                 case 9: k2_fft_job<T, 9, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-                case 10: k2_fft_job<T, 10, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                case 10:   // 8 x 16 x 8 (the plan builds its twiddles for it, RSP_K2_M1024MIX)
+                    if constexpr (RSP_K2_M1024MIX)
+                        k2_fft_job_mix<T, 1024, 8, 16, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L);
+                    else
+                        k2_fft_job<T, 10, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L);
+                    break;
                 default: k2_fft_job<T, 11, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
             }
         } else {

@@ -130,8 +130,8 @@ void build_pass_twiddles(int m, std::vector<cd>& out, bool rev = false, bool cmp
 
 // Mixed-radix overlap-save block M = 16 x R1 x 16 (k2_fft_job_mix): a palindrome, so the
 // inverse table (reversed radices) is the forward one and only the forward table is stored.
-void build_mix_twiddles(int R1, std::vector<cd>& out, bool cmp) {
-    const int rad[3] = {16, R1, 16};
+void build_mix_twiddles(int R0, int R1, std::vector<cd>& out, bool cmp) {
+    const int rad[3] = {R0, R1, R0};
     int Ns = 1;
     for (int q = 0; q < 3; ++q) {
         const int R = rad[q];
@@ -409,7 +409,7 @@ int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga,
         tw_sizes.push_back(M);
         tw_offs.push_back((int)twM.size());
         if (mix) {
-            build_mix_twiddles(M / 256, twM, RSP_K2_CMP);
+            build_mix_twiddles(16, M / 256, twM, RSP_K2_CMP);
         } else {
             build_pass_twiddles(s.logM, twM, false, RSP_K2_CMP, RSP_K2_PAL);   // forward FFT (compact rows, palindromic plan)
             build_pass_twiddles(s.logM, twM, true, RSP_K2_CMP, RSP_K2_PAL);    // inverse FFT (reversed radices)
@@ -906,7 +906,15 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
     // then holding 2048 / M rows; otherwise RSP_K2_POINTS (4096: 2 per CU in complex double)
     g.k2_pts = RSP_K2_POINTS;
     for (auto& s : p->segs)
-        if (f64 && s.type == 1 && s.M == 2560) g.k2_pts = RSP_K2_MIXPTS;
+        if (f64 && s.type == 1 && (s.M == 2560 || RSP_K2_MODE3_ALL)) g.k2_pts = RSP_K2_MIXPTS;
+    // such a plan's k2_pc runs a 1024-point block as 8 x 16 x 8 (two rows per workgroup, every
+    // thread in the radix-8 passes): its own twiddle tables (k2_fft_job_mix)
+    if (g.k2_pts == RSP_K2_MIXPTS && RSP_K2_M1024MIX)
+        for (auto& s : p->segs)
+            if (s.type == 1 && s.M == 1024) {
+                s.tw_off = (int)twM.size();
+                build_mix_twiddles(8, 16, twM, RSP_K2_CMP);
+            }
     for (auto& s : p->segs) {
         if (s.seg_lo < 0 || s.seg_lo >= N) return bail(fail(RSP_ERR_INVALID, "segment start out of range"));
         if (s.hi >= s.lo) need.push_back({s.lo, s.hi});
