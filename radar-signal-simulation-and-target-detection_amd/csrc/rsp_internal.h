@@ -19,6 +19,9 @@
 #ifndef RSP_K2_M1024MIX
 #define RSP_K2_M1024MIX 0    // 3-per-CU K2 plans run 1024-point blocks as 8 x 16 x 8 (1) or 16 x 4 x 16 (0)
 #endif
+#ifndef RSP_K1_AREL
+#define RSP_K1_AREL 0        // persistent K1 with two MFMA row blocks re-reads the second's operands per sub-tile
+#endif
 #ifndef RSP_K2_MODE3_ALL
 #define RSP_K2_MODE3_ALL 0   // every complex-double plan runs k2_pc at 3 workgroups per CU (A/B builds)
 #endif

@@ -963,9 +963,14 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
     const int lane = threadIdx.x & 63, grp = lane >> 4, col = lane & 15;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: nlv[] and n are scalar
     const T* At = static_cast<const T*>(k.Atab);
+    // the conj(W) operands of the MFMA row blocks held in registers for the kernel's life; with
+    // AREL the second row block's are re-read (L1/L2-resident, 2 x NJ x 64 values) in each
+    // sub-tile's DBF instead (x4: 32 VGPRs fewer across the Stockham passes)
+    constexpr bool AREL = MB == 2 && RSP_K1_AREL;
+    constexpr int MBR = AREL ? 1 : MB;
     T are[MB][NJ], aim[MB][NJ];
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb)
+    for (int mb = 0; mb < MBR; ++mb)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             are[mb][j] = At[((mb * NJ + j) * 2 + 0) * 64 + lane];
@@ -1028,6 +1033,15 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
 #pragma unroll
                 for (int a = 0; a < D::NACC; ++a) acc[mb][a] = typename D::Acc{};
             if (vld[u]) {   // samples past the used ones: zero columns, like k1_dbf_mtd's n = -1
+                if constexpr (AREL) {
+                    int la = lane;
+                    asm volatile("" : "+v"(la));   // opaque: keeps the loads here (not hoisted out of the tile loop)
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) {
+                        are[1][j] = At[((NJ + j) * 2 + 0) * 64 + la];
+                        aim[1][j] = At[((NJ + j) * 2 + 1) * 64 + la];
+                    }
+                }
 #pragma unroll
                 for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
