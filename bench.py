@@ -79,7 +79,9 @@ def parse(argv=None):
     ap.add_argument('--profile-iters', type=int, default=50)
     ap.add_argument('--cpu-frames', type=int, default=0, help='oracle frames for cpu_baseline (0 = auto ~15 s)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--batch', type=int, default=1024, help='MUSIC instances per launch (--config music5)')
+    ap.add_argument('--batch', type=int, default=4096,
+                    help='MUSIC instances per launch (--config music5; 4096: 2.30 vs 1.96-2.14 M instances/s at 1024, '
+                         'profiles/r05w_music_batch.txt)')
     ap.add_argument('--frames-total', type=int, default=0,
                     help='BASELINE config #3 mode: this many distinct frames (e.g. 512), sharded over the ranks, '
                          'each processed once (the default mode times --steps batches over a ring)')
@@ -323,11 +325,19 @@ def pmc_traffic(path, kernels, now=None):
     return None, None, src
 
 
-def music_traffic(prec):
-    """k_music_cov HBM bytes per 1024-instance launch from the PMC passes (profiles/, made by
-    tools/pmc_traffic.py over tools/music_prof.py 1024) and its provenance, or (None, source)."""
+def music_traffic(prec, n_inst):
+    """k_music_cov HBM bytes of one n_inst-instance launch from the PMC passes (profiles/, made by
+    tools/pmc_traffic.py over tools/music_prof.py; the file's launches held _instances_per_launch
+    instances, 1024 when it does not say) and its provenance, or (None, source)."""
     tf = os.path.join(ROOT, 'profiles', 'pmc_traffic_music5%s.json' % ('' if prec == 'c64' else '_c128'))
     tr, _, src = pmc_traffic(tf, ['k_music_cov64', 'k_music_cov'])
+    if tr is not None:
+        try:
+            per = json.load(open(tf)).get('_instances_per_launch', 1024)
+        except (OSError, ValueError):
+            per = 1024
+        src['instances_per_launch_measured'] = per
+        tr = tr * n_inst / float(per)
     return tr, src
 
 
@@ -404,7 +414,7 @@ def main_music(a):
                             'one wave per instance, Householder + bisection + inverse iteration + spectrum in '
                             'single') + '; latency-bound (neither HBM nor MFMA), see DESIGN.md'}]
         dom = max(stages, key=lambda st: st['ms_per_launch'])
-        mtraffic = music_traffic(a.precision)
+        mtraffic = music_traffic(a.precision, I)
         eig_tf = stages[1]['ref_eig_equiv_TFLOPs']
         out = {'metric': 'MUSIC_1D DOA instances/sec, 64ch x 1024 snapshots (BASELINE config #5)',
                'value': I * a.steps * world / el, 'unit': 'instances/s', 'n_gpus': world, 'steps': a.steps,

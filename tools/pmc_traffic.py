@@ -43,6 +43,8 @@ def main():
                     + os.environ.get('PMC_DRIVER', 'tools/prof_stages.py') + ' ' + ' '.join(sys.argv[4:]))
     if len(sys.argv) > 6 and 'PMC_DRIVER' not in os.environ:
         res['_frames_per_launch'] = int(sys.argv[6])
+    if 'music_prof' in os.environ.get('PMC_DRIVER', '') and len(sys.argv) > 4:
+        res['_instances_per_launch'] = int(sys.argv[4])
     # the code the counters were collected on: bench.py reports this file's traffic for a kernel
     # only while the built kernel still has the same hash (tools/kernel_hashes.py)
     kh = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
