@@ -325,12 +325,12 @@ def pmc_traffic(path, kernels, now=None):
     return None, None, src
 
 
-def music_traffic(prec, n_inst):
+def music_traffic(prec, n_inst, path=None, now=None):
     """k_music_cov HBM bytes of one n_inst-instance launch from the PMC passes (profiles/, made by
     tools/pmc_traffic.py over tools/music_prof.py; the file's launches held _instances_per_launch
     instances, 1024 when it does not say) and its provenance, or (None, source)."""
-    tf = os.path.join(ROOT, 'profiles', 'pmc_traffic_music5%s.json' % ('' if prec == 'c64' else '_c128'))
-    tr, _, src = pmc_traffic(tf, ['k_music_cov64', 'k_music_cov'])
+    tf = path or os.path.join(ROOT, 'profiles', 'pmc_traffic_music5%s.json' % ('' if prec == 'c64' else '_c128'))
+    tr, _, src = pmc_traffic(tf, ['k_music_cov64', 'k_music_cov'], now=now)
     if tr is not None:
         try:
             per = json.load(open(tf)).get('_instances_per_launch', 1024)

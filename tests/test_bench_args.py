@@ -119,3 +119,19 @@ def test_pmc_traffic_staleness(tmp_path):
     tr, _, src = bench.pmc_traffic(str(f), ['k2_pc'], now={'k2_pc': 'aaaa'})          # no hashes recorded
     assert tr is None and 'no kernel hash' in src['stale_reason']
     assert bench.pmc_traffic(str(tmp_path / 'missing.json'), ['k2_pc']) == (None, None, None)
+
+
+def test_music_traffic_scales_with_the_launch(tmp_path):
+    """config #5's roofline traffic is the PMC file's bytes per launch scaled from the instances
+    that launch held (_instances_per_launch, 1024 when absent) to the bench's --batch."""
+    import json
+    f = tmp_path / 'pmc_music.json'
+    f.write_text(json.dumps({'k_music_cov64': 4000, '_instances_per_launch': 4096,
+                             '_kernel_hashes': {'k_music_cov64': 'aaaa'}}))
+    tr, src = bench.music_traffic('c128', 1024, path=str(f), now={'k_music_cov64': 'aaaa'})
+    assert tr == 1000 and src['instances_per_launch_measured'] == 4096
+    f.write_text(json.dumps({'k_music_cov64': 1000, '_kernel_hashes': {'k_music_cov64': 'aaaa'}}))
+    tr, _ = bench.music_traffic('c128', 4096, path=str(f), now={'k_music_cov64': 'aaaa'})
+    assert tr == 4000
+    tr, src = bench.music_traffic('c128', 4096, path=str(f), now={'k_music_cov64': 'bbbb'})
+    assert tr is None and not src['fresh']
