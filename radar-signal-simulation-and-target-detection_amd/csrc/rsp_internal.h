@@ -22,6 +22,9 @@
 #ifndef RSP_K1_AREL
 #define RSP_K1_AREL 0        // persistent K1 with two MFMA row blocks re-reads the second's operands per sub-tile
 #endif
+#ifndef RSP_K3_BUFLD
+#define RSP_K3_BUFLD 1       // complex-single k3_cfar's tile loads through buffer resources (branch-free)
+#endif
 #ifndef RSP_K2_MODE3_ALL
 #define RSP_K2_MODE3_ALL 0   // every complex-double plan runs k2_pc at 3 workgroups per CU (A/B builds)
 #endif

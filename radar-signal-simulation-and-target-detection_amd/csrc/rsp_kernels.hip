@@ -1862,10 +1862,27 @@ __global__ __launch_bounds__(RSP_THREADS, RSP_K3_WGS) void k3_cfar(Geometry g, D
         const T* pa = MA + (size_t)(vt0 + rr) * Gp + r;
         const T* pb = MB + (size_t)(vt0 + rr) * Gp + r;
         U* sd = reinterpret_cast<U*>(S + rr * WC) + u;
+        // RSP_K3_BUFLD: the two maps as buffer resources, a unit outside the tile gets an
+        // out-of-range offset (bit 31) and reads 0 -- no branch around a load, so the 2 K3_VEC
+        // loads of a sweep are in flight together
+        const unsigned mbytes = (unsigned)((size_t)P * Gp * sizeof(T));
+        const __amdgpu_buffer_rsrc_t ra = buf_rsrc(MA, mbytes), rbm = buf_rsrc(MB, mbytes);
+        const unsigned base = colok ? (unsigned)(((size_t)(vt0 + rr) * Gp + r) * sizeof(T)) : RSP_OOB;
+        const unsigned rowb = (unsigned)Gp * (unsigned)sizeof(T);
         for (int vb = 0; vb < nv; vb += K3_VEC * NTR) {
             U xa[K3_VEC], xb[K3_VEC];
 #pragma unroll
             for (int q = 0; q < K3_VEC; ++q) {
+                if constexpr (RSP_K3_BUFLD && sizeof(T) == 4) {   // complex double: 35.0 vs 36.0 us, kept off
+                    const unsigned bad = (unsigned)(nv - 1 - (vb + rr + q * NTR)) & 0x80000000u;
+                    const unsigned off = (base + (unsigned)(vb + q * NTR) * rowb) | bad;
+                    xa[q] = __builtin_bit_cast(U, __builtin_amdgcn_raw_buffer_load_b128(ra, (int)off, 0, 0));
+                    xb[q] = __builtin_bit_cast(U, __builtin_amdgcn_raw_buffer_load_b128(rbm, (int)off, 0, 0));
+#pragma unroll
+                    for (int e = 1; e < EPU; ++e)   // the row pad past G (Gp > G) is not written by K2
+                        if (r + e >= G) { xa[q][e] = 0; xb[q][e] = 0; }
+                    continue;
+                }
                 xa[q] = U{};
                 xb[q] = xa[q];
                 if (colok && vb + rr + q * NTR < nv) {
