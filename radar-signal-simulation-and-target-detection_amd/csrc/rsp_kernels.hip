@@ -141,9 +141,20 @@ __device__ unsigned long long* rsp_k2_trace;
 extern "C" int rsp_debug_set_k2_trace(unsigned long long* p) {
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(rsp_k2_trace), &p, sizeof(p));
 }
+// persistent K1: workgroup x, loop iteration it < 64 writes [(x 64 + it) 4 + i] (tools/ab/k1_phases.py)
+__device__ unsigned long long* rsp_k1_trace;
+#define K1_STAMP(it, i)                                                                                 \
+    do {                                                                                                \
+        if (rsp_k1_trace && threadIdx.x == 0 && (it) < 64)                                              \
+            rsp_k1_trace[((size_t)blockIdx.x * 64 + (it)) * 4 + (i)] = wall_clock64();                 \
+    } while (0)
+extern "C" int rsp_debug_set_k1_trace(unsigned long long* p) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(rsp_k1_trace), &p, sizeof(p));
+}
 #else
 #define K2_STAMP(i) ((void)0)
 #define K2_TAG(v) ((void)0)
+#define K1_STAMP(it, i) ((void)0)
 #endif
 
 // ---- radix-R DFT kernels in registers -------------------------------------------------
@@ -1065,8 +1076,10 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
     if (EARLY && !EARLY2 && TT + (int)gridDim.x < total) issue(TT + gridDim.x);
     __syncthreads();
     int cur = 0;
-    for (; TT < total; TT += gridDim.x) {
+    int it = 0;   // diagnostic builds: the phase stamps' iteration index
+    for (; TT < total; TT += gridDim.x, ++it) {
         const int Tn = TT + gridDim.x;
+        K1_STAMP(it, 0);
         if (!EARLY && Tn < total) issue(Tn);   // next tile's loads fly during this tile's FFT + z stores
         const int f = __builtin_amdgcn_readfirstlane(TT / g.ntiles), tile = TT - f * g.ntiles;
         if (tile == 0 && threadIdx.x == 0 && fp.count[f]) *fp.count[f] = 0;   // K3's detection counter
@@ -1081,11 +1094,14 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
         else
             fft_passes<LGP, k1p_pts<T>(), K1_SH, K1_THREADS, false>(Y + cur * bufsz, Ppad, B * NT, twl,
                                                                      StoreLds<V>{Y + cur * bufsz}, sz);
+        K1_STAMP(it, 1);
         if (Tn < total) {
             dbf(Y + (cur ^ 1) * bufsz, EARLY2 && Tn + (int)gridDim.x < total ? Tn + (int)gridDim.x : -1);
             if (EARLY && !EARLY2 && Tn + (int)gridDim.x < total) issue(Tn + gridDim.x);
         }
+        K1_STAMP(it, 2);
         __syncthreads();
+        K1_STAMP(it, 3);
         cur ^= 1;
     }
 }
