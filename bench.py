@@ -98,6 +98,9 @@ def parse(argv=None):
                          'a secondary line, not the headline')
     ap.add_argument('--stage-timing', action='store_true',
                     help='HIP events around every kernel in the timed region (diagnostic: overlapped durations)')
+    ap.add_argument('--per-call', action='store_true',
+                    help='latency mode: --steps synchronous rsp_process_targets calls, one frame each, timed one by '
+                         'one like the v8 frame loop\'s tic/toc (v8:162,177,191-194); not the headline')
     return ap.parse_args(argv)
 
 
@@ -189,6 +192,9 @@ def validate_args(a):
                 'complex RD map, so the line would claim map bytes that were never stored')
     if a.want_rdm and a.config == 'music5':
         return '--want-rdm applies to the radar chain, not --config music5'
+    if a.per_call and (a.config == 'music5' or a.e2e or a.want_rdm or a.frames_total or a.gpus != 1):
+        return ('--per-call times single synchronous frames of the radar chain on one GPU: it takes none of '
+                '--config music5, --e2e, --want-rdm, --frames-total, --gpus N')
     return None
 
 
@@ -246,6 +252,22 @@ def cpu_baseline(cfg, cfar, clus, W, ang, k, targets, budget_s=15.0, nframes=0, 
             'sample': '%d frames of the same %s cube, median of per-frame times (%.3f s/frame); oracle = '
                       'numpy/scipy complex128 restatement of fsf S5-S11, CFAR vectorised '
                       '(the MATLAB scalar CFAR loop fsf:192-213 would be slower)' % (len(times), name, med)}
+
+
+def k3_map_bytes(P, G, B, cfar, real_bytes, rt=None):
+    """Magnitude-map bytes K3 reads per frame (its stage bytes in rsp_profile_stages): with the
+    reference's CFAR window (refCells 5, guardCells 10) the halo-less tiles hold only the
+    P - 2 (refV + guardV) Doppler rows under test, over the tiled range columns (the first cell
+    under test rounded down to 4, ceil-ish tiles of rt cells clipped to G); other windows read
+    whole maps.  Restates k3_map_bytes / k3_ntiles of rsp_internal.h."""
+    rt = rt if rt is not None else (64 if real_bytes == 4 else 32)
+    rR, gR, rV, gV = cfar['refCells_R'], cfar['guardCells_R'], cfar['refCells_V'], cfar['guardCells_V']
+    if (rR, rV, gR, gV) == (5, 5, 10, 10) and rt in (32, 64):
+        rc0 = rR + gR
+        ntiles = (G - rc0 - (rc0 & ~3) + rt - 1) // rt
+        c0, c1 = rc0 & ~3, min(G, (rc0 & ~3) + ntiles * rt)
+        return B * max(P - 2 * (rV + gV), 0) * max(c1 - c0, 0) * real_bytes
+    return B * P * G * real_bytes
 
 
 MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense peak
@@ -450,6 +472,92 @@ def main_music(a):
         print(json.dumps(out))
 
 
+def main_per_call(a):
+    """Latency of the literal drop-in: `final_targets = fun_process_single_frame(targets, ...)` once
+    per frame (fsf:13), as the v8 frame loop calls it and times it with tic/toc (v8:162,177,191-194).
+    Each step is ONE synchronous rsp_process_targets call through the C ABI, exactly what the MEX
+    gateway's rsp_mex('frame', ...) makes: on-device S4/S4.1 synthesis of the frame from the target
+    list, S5-S9 on the device, S10/S11 on the host, the final targets copied out.  The targets
+    evolve per frame (v8:170-173).  value = calls / s over the --steps timed calls."""
+    import ctypes as ct
+    from rsp import config as C, _abi
+    from rsp.precompute import precompute
+    from rsp.plan import Plan
+    cfg, cfar, clus, W, ang, k = C.named_config(a.config)
+    pre = precompute(cfg, W, ang, k, C.V8_FIR)
+    plan = Plan(cfg, cfar, clus, pre, device=0, frames_per_launch=1, precision=a.precision)
+    sz = plan.sizes
+    targets = scene(cfg)
+    cap = 4096
+    tbuf = (_abi.Target * cap)()
+    o = _abi.FrameOut()
+    o.dets, o.dets_cap, o.targets, o.targets_cap = None, 0, ct.cast(tbuf, ct.POINTER(_abi.Target)), cap
+    lib = _abi.lib()
+    seqs = []
+    tg = targets
+    for i in range(a.warmup + a.steps):
+        seqs.append(Plan._targets_in(tg))
+        tg = C.evolve_targets(tg, cfg)
+    ntg = len(targets)
+
+    def call(i):
+        _abi.check(lib.rsp_process_targets(plan.h, seqs[i], ntg, i + 1, 20250101, 1.0, ct.byref(o)))
+
+    for i in range(max(a.warmup, 3)):
+        call(i % len(seqs))
+    times = []
+    n_targets = 0
+    t_all = time.perf_counter()
+    for i in range(a.warmup, a.warmup + a.steps):
+        t0 = time.perf_counter()
+        call(i)
+        times.append(time.perf_counter() - t0)
+        n_targets += o.n_targets
+    el = time.perf_counter() - t_all
+    ms = np.array(times) * 1e3
+    # the device stages of one frame in isolation (HIP events, F = 1), for the roofline object
+    d_cube = plan.device_alloc(plan.cube_bytes)
+    plan.synthesize_device(d_cube, targets, frame_idx=1)
+    plan.sync()
+    prof = plan.profile_stages([d_cube], iters=a.profile_iters)
+    plan.device_free(d_cube)
+    stages = [{'stage': pr['stage'], 'ms_per_launch': pr['ms'], 'frames_per_launch': pr['frames'],
+               'alg_bytes_per_launch': pr['bytes'], 'achieved_GBps': pr['bytes'] / (pr['ms'] * 1e-3) / 1e9}
+              for pr in prof]
+    dom = max(stages, key=lambda s: s['ms_per_launch'])
+    cells = sz.B * sz.G * sz.P
+    cfg_no = {'x2': '2', 'x4': '4', 'plumbing': '1'}.get(a.config, '-')
+    out = {'metric': 'per-call latency of rsp_process_targets (one synchronous fun_process_single_frame frame), '
+                     '%dch×%dbeam×%dsamp×%dpulse' % (sz.C, sz.B, sz.N, sz.P),
+           'value': a.steps / el, 'unit': 'frames/s', 'n_gpus': 1, 'steps': a.steps, 'warmup': a.warmup,
+           'ms_per_step': el / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+           'dtype': 'fp64 (complex128)' if a.precision == 'c128' else 'fp32 (complex64)',
+           'data': 'synthetic (device S4 synthesis + Philox noise of the v8_2 targets inside every call)',
+           'per_call_ms': {'median': float(np.median(ms)), 'mean': float(ms.mean()), 'min': float(ms.min()),
+                           'p10': float(np.percentile(ms, 10)), 'p90': float(np.percentile(ms, 90)),
+                           'max': float(ms.max())},
+           'cells_per_s': a.steps / el * cells,
+           'config': {'workload': 'BASELINE config #%s: %s C=%d B=%d N=%d P=%d G=%d, synchronous calls' % (
+               cfg_no, a.config, sz.C, sz.B, sz.N, sz.P, sz.G), 'frames_per_call': 1,
+               'used_samples': sz.used_samples, 'targets_reported': n_targets,
+               'call': 'rsp_process_targets(plan, targets, nt, frame_idx, seed, 1.0, out) -- the C call of '
+                       'rsp_mex(\'frame\', ...) (matlab/rsp_mex.c)'},
+           'roofline': {'bound': 'hbm', 'kernel': dom['stage'], 'achieved': dom['achieved_GBps'],
+                        'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': dom['achieved_GBps'] / HBM_PEAK_GBS,
+                        'traffic': None, 'kernel_ms': dom['ms_per_launch'],
+                        'alg_bytes_per_launch': dom['alg_bytes_per_launch'], 'frames_per_launch': 1,
+                        'timing': '%d isolated one-frame launches per stage, HIP events on the kernel stream'
+                                  % a.profile_iters, 'stages': stages,
+                        'device_ms_per_frame': sum(s['ms_per_launch'] for s in stages)}}
+    if not a.no_cpu_baseline:
+        out['cpu_baseline'] = cpu_baseline(cfg, cfar, clus, W, ang, k, targets, nframes=a.cpu_frames, name=a.config)
+    else:
+        out['cpu_baseline'] = None
+    plan.close()
+    print(json.dumps(out))
+    return 0
+
+
 def main():
     a = parse()
     bad = validate_args(a)
@@ -468,7 +576,9 @@ def main():
         return spawn_ranks(a.gpus, sys.argv[1:])
     if a.config == 'music5':
         return main_music(a)
-    rank = int(os.environ.get('RANK', 0))
+    if a.per_call:
+        return main_per_call(a)
+    rank =int(os.environ.get('RANK', 0))
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', 0))
     dist = None

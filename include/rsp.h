@@ -446,7 +446,9 @@ typedef struct rsp_music_scene {
 typedef struct rsp_music_out {
     double* spectrum_db;      /* [n_scan x I] P_MUSIC_dB (MUSIC_1D.m:41)                      */
     double* eigenvalues;      /* [N x I] descending (MUSIC_1D.m:30-31); when NULL, complex double
-                                 finds only the M signal eigenvalues the spectrum needs        */
+                                 finds only the M signal eigenvalues the spectrum needs, and
+                                 when spectrum_db is NULL too, only the signal subspace (the
+                                 block-power fast path, rsp_music_fast_count)                  */
     int32_t* peak_idx;        /* [M x I] 1-based scan indices of the M largest peaks (:43-47), 0 = none */
     int32_t* n_peaks;         /* [I] number of findpeaks peaks                                 */
     double* covariance;       /* complex [N x N x I] R (MUSIC_1D.m:28), column-major           */
@@ -468,8 +470,18 @@ int32_t rsp_music_synthesize_device(rsp_music_plan* plan, const rsp_music_scene*
  * averaged over `iters` launches on the plan's stream, in the peaks-only form of a call (the
  * eigenvalues not requested: complex double then finds only the M signal eigenvalues). */
 int32_t rsp_music_profile(rsp_music_plan* plan, const void* d_X, int32_t n_inst, int32_t iters, float* ms_out);
+/* The same timing for the form of call `what` names: RSP_MUSIC_PEAKS (= rsp_music_profile: only
+ * peak_idx / n_peaks read; the block-power fast path may stand in for the eigensolver),
+ * RSP_MUSIC_SPECTRUM (spectrum_db read too: the full eigensolver, M signal eigenvalues) or
+ * RSP_MUSIC_EIGENVALUES (eigenvalues read: the full eigensolver, all N eigenvalues -- the
+ * 3-output rsp_mex('music') call and music_1d_calllib.m, MUSIC_1D.m:29-33). */
+#define RSP_MUSIC_PEAKS 0
+#define RSP_MUSIC_SPECTRUM 1
+#define RSP_MUSIC_EIGENVALUES 2
+int32_t rsp_music_profile_ex(rsp_music_plan* plan, const void* d_X, int32_t n_inst, int32_t iters, int32_t what,
+                             float* ms_out);
 /* Instances of the last call whose signal subspace came from the block-power fast path (complex
- * double, peaks-only calls, M <= 4: the iteration converged with a proven 1e-12 subspace bound,
+ * double, calls that read neither eigenvalues nor spectrum_db, M <= 4: the iteration converged with a proven 1e-12 subspace bound,
  * rsp_music.hip me_fast_subspace); the others ran the full tridiagonal eigensolver.  Diagnostic. */
 int32_t rsp_music_fast_count(rsp_music_plan* plan, int32_t* n_fast);
 int32_t rsp_music_device_alloc(rsp_music_plan* plan, int64_t bytes, void** d_ptr);

@@ -122,6 +122,10 @@ struct Geometry {
     int NZ, nzc;     // z layout: NZ compacted samples per (row, chunk) slab, nzc chunks per row
     int twPp_elems;  // per-pass twiddles of the P-point FFT
     int pow2P, logP;
+    // non-power-of-two P = rqR * rqQ (rqR = 2 or 4, rqQ odd >= 3): K1's factored slow-time DFT
+    // (k1_dft_rq); rqQ = 0: the direct O(P^2) DFT.  twq_elems = complex entries of its
+    // frequency-set twiddle table (DevConsts::twQ)
+    int rqR, rqQ, twq_elems;
     int nseg, njobs, nwg_k2;
     // complex points of LDS rows per pulse-compression workgroup: RSP_K2_POINTS, or 2560 in a
     // complex-double plan with a 2560-point block (3 workgroups per CU: 53.5 KB of LDS each);
@@ -159,6 +163,21 @@ __host__ __device__ inline int k3_ntiles(const Geometry& g) {
     return (g.G - rc0 - (rc0 & ~3) + g.cfar_RT - 1) / g.cfar_RT;
 }
 
+// Magnitude-map bytes K3 reads from HBM per frame (the K3 stage's algorithmic bytes): on the
+// fast path the halo-less tiles hold only the Doppler rows under test, P - 2 (refV + guardV), over
+// the tiled range columns (first cell under test rounded down to 4, k3_ntiles * cfar_RT cells,
+// clipped to G); each beam's map is read by two pairs, the second read an L2 hit (XCD-aware
+// order).  The general path reads whole maps.  bench.py / tests/test_bench_args.py restate it.
+__host__ __device__ inline long long k3_map_bytes(const Geometry& g, int real_bytes) {
+    if (RSP_K3_NOHALO && k3_fast_params(g)) {
+        const int hV = g.refV + g.guardV, c0 = (g.refR + g.guardR) & ~3;
+        const int rows = g.P - 2 * hV > 0 ? g.P - 2 * hV : 0;
+        const int c1 = c0 + k3_ntiles(g) * g.cfar_RT < g.G ? c0 + k3_ntiles(g) * g.cfar_RT : g.G;
+        return (long long)g.B * rows * (c1 > c0 ? c1 - c0 : 0) * real_bytes;
+    }
+    return (long long)g.B * g.P * g.G * real_bytes;
+}
+
 // Per-frame device buffers of one launch.  Element types follow Geometry::prec: complex
 // values are (re, im) pairs of float or double, maps are float or double.
 struct FramePtrs {
@@ -178,6 +197,7 @@ struct DevConsts {
     const void* twP;         // W_P^i table (direct DFT path), complex
     const void* twPp;        // per-pass Stockham twiddles of the P-point FFT, complex
     const void* twD;         // persistent K1's in-place FFT: [i][n2] = W_P^(n2 2^i), i < 4, n2 < P/16, complex
+    const void* twQ;         // factored DFT (P = R Q): [fset][n - 1][r] = (cos, sin)(2 pi k n / Q), k = RQ_RK fset + r
     const void* taps;        // narrow FIR taps, real
     const void* H;           // overlap-save spectra, 1/M scaled, complex
     const void* twM;         // per-pass Stockham twiddles of each overlap-save block size, complex
@@ -195,6 +215,9 @@ struct SynthTarget {          // per-target constants of S4 (fsf:51-73), host-co
     double fd_prt;            // doppler_freq * prt   (phase per pulse / 2pi)
     double dphi;              // channel phase step (rad)
 };
+
+// Frequencies per wave-uniform set of the factored slow-time DFT's Q-point stage (k1_dft_rq)
+#define RQ_RK 6
 
 // Launchers (rsp_kernels.hip).  `mode` bits for K1: 1 = apply DBF, 2 = apply MTD.
 hipError_t launch_k1(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int mode, hipStream_t s);

@@ -651,9 +651,12 @@ template <> struct Dbf<double> {
 
 // D of one sub-tile (sample nl, pulses p .. p + PPL*... of this lane) x window -> padded LDS
 // columns [b * NT + nl][Ppad] (Re / Im parts as two scalar stores).
+// plim: pulses >= plim (the last sub-tile's lanes past P when P is not a multiple of 16) are not
+// stored.
 template <class T, int MB>
 __device__ __forceinline__ void dbf_store(T* Yf, const typename Dbf<T>::Acc (&acc)[MB][Dbf<T>::NACC], int grp, int B,
-                                          int NT, int Ppad, int nl, int p, const T (&w)[Dbf<T>::NACC], int sh) {
+                                          int NT, int Ppad, int nl, int p, const T (&w)[Dbf<T>::NACC], int sh,
+                                          int plim) {
     if constexpr (sizeof(T) == 8) {
         // double: registers i and i + 2 hold Re and Im of the same beam (rows grp + 4 i and
         // grp + 4 i + 8), so each beam's complex value goes out as one 16-B store.  Two 8-B
@@ -666,7 +669,7 @@ __device__ __forceinline__ void dbf_store(T* Yf, const typename Dbf<T>::Acc (&ac
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 const int b = mb * 8 + ((grp + 4 * i) & 7);
-                if (b < B)
+                if (b < B && p < plim)
                     reinterpret_cast<d2*>(Yf)[(b * NT + nl) * Ppad + ip] =
                         d2{acc[mb][0][i] * w[0], acc[mb][0][i + 2] * w[0]};
             }
@@ -682,7 +685,7 @@ __device__ __forceinline__ void dbf_store(T* Yf, const typename Dbf<T>::Acc (&ac
             for (int i = 0; i < 4; ++i) {   // D row m: beam mb*8 + (m & 7), part m >> 3
                 const int m = Dbf<T>::row(grp, i);
                 const int b = mb * 8 + (m & 7);
-                if (b < B) Yf[2 * ((b * NT + nl) * Ppad + ip) + (m >> 3)] = acc[mb][a][i] * w[a];
+                if (b < B && pa < plim) Yf[2 * ((b * NT + nl) * Ppad + ip) + (m >> 3)] = acc[mb][a][i] * w[a];
             }
     }
 }
@@ -782,11 +785,125 @@ __device__ __forceinline__ void k1_fft(int lgp, V* Y, int Ppad, int ncols, const
     }
 }
 
+// ---- factored slow-time DFT for P = R Q (R = 2 or 4, Q odd >= 3; the reference frame's
+// P = 332 = 4 x 83, v8:57), decimation in frequency:
+//   X[R k1 + k2] = sum_{n1 < Q} W_Q^(n1 k1) y_k2[n1],  y_k2[n1] = W_P^(n1 k2) sum_{n2 < R} x[n1 + Q n2] W_R^(n2 k2)
+// Pass 1 (thread per column and n1 <= (Q - 1) / 2): the radix-R DFTs of x[n1 + Q n2] and of its
+// mirror x[Q - n1 + Q n2], their twiddles, and the fold of the Q-point stage
+//   s_k2[n] = y_k2[n] + y_k2[Q - n] -> slot n + Q k2,   d_k2[n] = y_k2[n] - y_k2[Q - n] -> slot Q - n + Q k2
+// in place (a thread writes exactly the slots it read).  Pass 2: with theta = 2 pi k1 n / Q,
+//   A = y[0] + sum_{n=1}^{(Q-1)/2} s_n cos(theta),  Bv = sum_n d_n sin(theta),
+//   X[R k1 + k2] = A - i Bv,   X[R (Q - k1) + k2] = A + i Bv          (k1 = 0 .. (Q - 1) / 2)
+// -- 4 real FMAs per (k1, n) for two outputs, a quarter of the direct sum.  One lane per
+// subsequence (column, k2), a wave-uniform set of RQ_RK frequencies per wave: the (cos, sin)
+// pair of a step is the same for every lane (an LDS broadcast read), the lane's s_n and d_n two
+// 16-B reads shared by its RQ_RK frequencies.  twq = [fset][n - 1][r] (twQ, in LDS), twp =
+// W_P^i, i < P (in LDS); st.put(col, o, x) stores output bin o of column col.
+template <int R, int NTHR, class V, class St>
+__device__ __forceinline__ void k1_dft_rq(V* buf, int rs, int ncols, int Q, const V* twq, const V* twp, const St& st) {
+    const int Qh = (Q - 1) >> 1, KH = Qh + 1;
+    {   // ---- pass 1
+        const int items = ncols * KH;
+        for (int it = threadIdx.x; it < items; it += NTHR) {
+            const int c = it / KH, n1 = it - c * KH;
+            V* col = buf + c * rs;
+            V u[R];
+#pragma unroll
+            for (int n2 = 0; n2 < R; ++n2) u[n2] = col[n1 + Q * n2];
+            Dft<R, false, V>::run(u);
+            if (n1 == 0) {   // W_P^0 = 1; y[0] is its own mirror
+#pragma unroll
+                for (int k2 = 0; k2 < R; ++k2) col[Q * k2] = u[k2];
+                continue;
+            }
+            V v[R];
+            const int m = Q - n1;
+#pragma unroll
+            for (int n2 = 0; n2 < R; ++n2) v[n2] = col[m + Q * n2];
+            Dft<R, false, V>::run(v);
+            col[n1] = u[0] + v[0];
+            col[m] = u[0] - v[0];
+#pragma unroll
+            for (int k2 = 1; k2 < R; ++k2) {   // n1 k2, m k2 < Q R = P: direct table entries
+                const V a = vmul(u[k2], twp[n1 * k2]), b = vmul(v[k2], twp[m * k2]);
+                col[n1 + Q * k2] = a + b;
+                col[m + Q * k2] = a - b;
+            }
+        }
+    }
+    __syncthreads();
+    {   // ---- pass 2
+        const int NS = ncols * R, nfs = (KH + RQ_RK - 1) / RQ_RK, ngrp = (NS + 63) >> 6;
+        const int lane = threadIdx.x & 63;
+        const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        for (int item = wv; item < ngrp * nfs; item += NTHR / 64) {   // wave-uniform
+            const int grp = item / nfs, fs = item - grp * nfs;
+            const int sub = grp * 64 + lane;
+            const int sc = min(sub, NS - 1);   // idle lanes read a real column, store nothing
+            const int c = sc / R, k2 = sc - c * R;
+            const V* col = buf + c * rs + Q * k2;   // s_n = col[n], d_n = col[Q - n]
+            const V* tw = twq + fs * Qh * RQ_RK;
+            V A[RQ_RK], Bv[RQ_RK];
+            const V y0 = col[0];
+#pragma unroll
+            for (int r = 0; r < RQ_RK; ++r) {
+                A[r] = y0;
+                Bv[r] = V{};
+            }
+#pragma unroll 2
+            for (int n = 1; n <= Qh; ++n) {
+                const V sv = col[n], dv = col[Q - n];
+                const V* t = tw + (n - 1) * RQ_RK;
+#pragma unroll
+                for (int r = 0; r < RQ_RK; ++r) {
+                    const V cs = t[r];   // (cos, sin)(2 pi k1 n / Q): the same address in every lane
+                    A[r] += cs.x * sv;
+                    Bv[r] += cs.y * dv;
+                }
+            }
+            if (sub < NS) {
+#pragma unroll
+                for (int r = 0; r < RQ_RK; ++r) {
+                    const int k1 = fs * RQ_RK + r;
+                    if (k1 < KH) {
+                        st.put(c, R * k1 + k2, V{A[r].x + Bv[r].y, A[r].y - Bv[r].x});   // A - i Bv
+                        if (k1 > 0) st.put(c, R * (Q - k1) + k2, V{A[r].x - Bv[r].y, A[r].y + Bv[r].x});
+                    }
+                }
+            }
+        }
+    }
+}
+
+// z store of the factored DFT's outputs: column col = b NT + nl, bin o -> Doppler cell
+// v = (o + P/2) mod P (fftshift, fsf:135), compacted sample tile NT + nl.
+template <class V>
+struct StoreZq {
+    __amdgpu_buffer_rsrc_t z; int lgNT, nzc, tile, P, half, lgNZ;
+    __device__ __forceinline__ void put(int col, int o, V x) const {
+        const int b = col >> lgNT, nl = col & ((1 << lgNT) - 1);
+        int v = o + half;
+        v = v >= P ? v - P : v;
+        const int np = (tile << lgNT) + nl;
+        buf_st<RSP_Z_AUX>(z, (unsigned)((((b * nzc + (np >> lgNZ)) * P + v) << lgNZ) + (np & ((1 << lgNZ) - 1))) *
+                                 (unsigned)sizeof(V), x);
+    }
+};
+
+template <class V, class St>
+__device__ __forceinline__ void k1_dft_rq_r(int R, V* buf, int rs, int ncols, int Q, const V* twq, const V* twp,
+                                            const St& st) {
+    if (R == 2) k1_dft_rq<2, K1_THREADS>(buf, rs, ncols, Q, twq, twp, st);
+    else k1_dft_rq<4, K1_THREADS>(buf, rs, ncols, Q, twq, twp, st);
+}
+
 // BMAX = beams rounded up (4/8/16), CP = channels rounded up (8/16/32).  conj(W) enters as the
 // per-lane MFMA A operands (Atab, zero for padded beams/channels), so the DBF has no
 // data-dependent branches.  mode 3 = DBF + MTD; mode 0 = transpose only (stage-2 path: the
-// input channels are the beams).  Non-power-of-two P takes a direct DFT (O(P^2) per column).
-template <class T, int BMAX, int CP>
+// input channels are the beams).  Non-power-of-two P = R Q takes the factored DFT (k1_dft_rq),
+// any other the direct DFT (O(P^2) per column).
+// RQ: the instantiation that runs the factored DFT (its registers stay out of the others).
+template <class T, int BMAX, int CP, bool RQ>
 __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConsts k, FramePtrs fp, int mode) {
     typedef cx<T> V;
     typedef Dbf<T> D;
@@ -796,6 +913,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
     if (tile == 0 && threadIdx.x == 0 && fp.count[f]) *fp.count[f] = 0;   // K3's detection counter
     V* twl = Y + B * NT * Ppad;
     const bool fft = (mode & 2) && g.pow2P;
+    const bool rq = RQ && (mode & 2);   // factored DFT: twl = twQ | W_P^i
     const int sh = fft ? K1_SH : 0;
     // P = 64, 128 run the in-place k1_fft_dif (as the persistent K1: the same bits), the other
     // powers of two the Stockham passes
@@ -868,7 +986,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
                 T w[D::NACC];
 #pragma unroll
                 for (int a = 0; a < D::NACC; ++a) w[a] = (mode & 2) ? win[p + a] : (T)1;
-                dbf_store<T, MB>(Yf, acc, grp, B, NT, Ppad, nlv[u], p, w, sh);
+                dbf_store<T, MB>(Yf, acc, grp, B, NT, Ppad, nlv[u], p, w, sh, P);
             }
         }
     } else {
@@ -898,6 +1016,12 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
         }
         for (int i = threadIdx.x + TWPRE * K1_THREADS; i < ntw; i += K1_THREADS) twl[i] = twPp[i];
     }
+    if (RQ && rq) {
+        const V* __restrict__ twQ = static_cast<const V*>(k.twQ);
+        const V* __restrict__ twP = static_cast<const V*>(k.twP);
+        for (int i = threadIdx.x; i < g.twq_elems; i += K1_THREADS) twl[i] = twQ[i];
+        for (int i = threadIdx.x; i < P; i += K1_THREADS) twl[g.twq_elems + i] = twP[i];
+    }
     __syncthreads();
     V* __restrict__ z = static_cast<V*>(fp.z[f]);
     const int zslab = P * NT;   // contiguous [P][NT] slab per (b, tile)
@@ -916,6 +1040,9 @@ __global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConst
         // and stores the [P][NT] slabs from registers
         const StoreZ<V> sz{buf_rsrc(z, (unsigned)(B * g.nzc * P * g.NZ * sizeof(V))), lgNT, g.nzc, tile, P, half, ilog2(g.NZ)};
         k1_fft(g.logP, Y, Ppad, B * NT, twl, sz);
+    } else if (RQ && rq) {
+        const StoreZq<V> sz{buf_rsrc(z, (unsigned)(B * g.nzc * P * g.NZ * sizeof(V))), lgNT, g.nzc, tile, P, half, ilog2(g.NZ)};
+        k1_dft_rq_r(g.rqR, Y, Ppad, B * NT, g.rqQ, twl, twl + g.twq_elems, sz);
     } else {
         // non power-of-two P: direct DFT straight to global (O(P^2) per column)
         const V* __restrict__ twP = static_cast<const V*>(k.twP);
@@ -1059,7 +1186,7 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
                     for (int j = 0; j < NJ; ++j) D::mma(acc[mb], are[mb][j], aim[mb][j], xv[u][j]);
             }
             if (Tnext >= 0) issue_u(Tnext, u);
-            dbf_store<T, MB>(Yf, acc, grp, B, NT, Ppad, nlv[u], pv[u], wv_[u], K1_SH);
+            dbf_store<T, MB>(Yf, acc, grp, B, NT, Ppad, nlv[u], pv[u], wv_[u], K1_SH, P);
         }
     };
     const int lgNT = ilog2(NT), half = P >> 1;
@@ -1103,6 +1230,117 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
         __syncthreads();
         K1_STAMP(it, 3);
         cur ^= 1;
+    }
+}
+
+// K1 for the factored slow-time DFT (P = R Q, k1_dft_rq; the reference frame's P = 332),
+// persistent: one 512-thread workgroup per CU walks the flattened (frame, tile) list of the launch
+// with ONE tile buffer -- the tile and the DFT's tables fill the LDS (reference frame: 13 beams x
+// 332 pulses x 16 B + 33 KB of tables).  Per tile: the DBF consumes the cube loads already in
+// registers, the next tile's loads go out at once (non-temporal), and they land while pass 1 and
+// pass 2 run; pass 2 stores z.  Same arithmetic per element as k1_dbf_mtd (mode 3, factored DFT):
+// bit-identical outputs.  TPW sub-tiles per wave cover a tile in one load round (k1q_tpw); the
+// last sub-tile of a column may run past P (lanes with p >= P load the next row's samples or
+// zeros past the cube and store nothing).
+template <class T, int BMAX, int CP, int TPW>
+__global__ __launch_bounds__(K1_THREADS, 1) void k1q_dbf_mtd(Geometry g, DevConsts k, FramePtrs fp, int nf) {
+    typedef cx<T> V;
+    typedef Dbf<T> D;
+    V* Y = reinterpret_cast<V*>(rsp_lds);   // tile [B][NT][Ppad] | twQ | W_P^i
+    const int B = g.B, C = g.C, P = g.P, NT = g.NT, Ppad = g.Ppad;
+    V* twq = Y + B * NT * Ppad;
+    V* twp = twq + g.twq_elems;
+    const int total = nf * g.ntiles;
+    int TT = blockIdx.x;
+    if (TT >= total) return;
+    {
+        const V* __restrict__ tq = static_cast<const V*>(k.twQ);
+        const V* __restrict__ tp = static_cast<const V*>(k.twP);
+        for (int i = threadIdx.x; i < g.twq_elems; i += K1_THREADS) twq[i] = tq[i];
+        for (int i = threadIdx.x; i < P; i += K1_THREADS) twp[i] = tp[i];
+    }
+    constexpr int NJ = CP / 4, MB = BMAX <= 8 ? 1 : 2;
+    constexpr int PT = 16 * D::PPL;
+    const int lane = threadIdx.x & 63, grp = lane >> 4, col = lane & 15;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const T* At = static_cast<const T*>(k.Atab);
+    T are[MB][NJ], aim[MB][NJ];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            are[mb][j] = At[((mb * NJ + j) * 2 + 0) * 64 + lane];
+            aim[mb][j] = At[((mb * NJ + j) * 2 + 1) * 64 + lane];
+        }
+    const int ptiles = (P + PT - 1) / PT, ntp = NT * ptiles;
+    const T* __restrict__ win = static_cast<const T*>(k.win);
+    int nlv[TPW], pv[TPW];
+    T wv_[TPW][D::NACC];
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) {
+        const int t = wv * TPW + u;
+        const int nl = t / ptiles;
+        pv[u] = (t - nl * ptiles) * PT + D::PPL * col;
+        nlv[u] = t < ntp ? nl : -1;   // wave-uniform
+#pragma unroll
+        for (int a = 0; a < D::NACC; ++a) wv_[u][a] = (nlv[u] >= 0 && pv[u] + a < P) ? win[pv[u] + a] : (T)0;
+    }
+    const size_t NPc = (size_t)g.cpitch;
+    unsigned loff[TPW][NJ];
+#pragma unroll
+    for (int u = 0; u < TPW; ++u)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+            loff[u][j] = (unsigned)(((size_t)min(4 * j + grp, C - 1) * NPc + pv[u]) * sizeof(V));
+    const unsigned cube_bytes = (unsigned)((size_t)C * NPc * sizeof(V));
+    typename D::Ld xv[TPW][NJ];
+    bool vld[TPW];
+    auto issue = [&](int Tn) {   // cube loads of tile Tn (fsf:93 operands) into xv
+        const int f = __builtin_amdgcn_readfirstlane(Tn / g.ntiles), tile = Tn - f * g.ntiles;
+        const __amdgpu_buffer_rsrc_t xr = buf_rsrc(fp.in[f], cube_bytes);
+#pragma unroll
+        for (int u = 0; u < TPW; ++u) {
+            const int np = tile * NT + nlv[u];
+            vld[u] = nlv[u] >= 0 && np < g.nU;
+            if (vld[u]) {
+                const int soff = used_sample(g, np) * P * (int)sizeof(V);
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)   // non-temporal: the cube is read exactly once
+                    xv[u][j] = D::bits(__builtin_amdgcn_raw_buffer_load_b128(xr, (int)loff[u][j], soff, 2));
+            }
+        }
+    };
+    const int lgNT = ilog2(NT), half = P >> 1;
+    issue(TT);
+    for (; TT < total; TT += gridDim.x) {
+        const int Tn = TT + gridDim.x;
+        {   // MFMA DBF + window of xv into Y
+            T* Yf = reinterpret_cast<T*>(Y);
+#pragma unroll
+            for (int u = 0; u < TPW; ++u) {
+                if (nlv[u] < 0) continue;
+                typename D::Acc acc[MB][D::NACC];
+#pragma unroll
+                for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+                    for (int a = 0; a < D::NACC; ++a) acc[mb][a] = typename D::Acc{};
+                if (vld[u]) {   // samples past the used ones: zero columns
+#pragma unroll
+                    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j) D::mma(acc[mb], are[mb][j], aim[mb][j], xv[u][j]);
+                }
+                dbf_store<T, MB>(Yf, acc, grp, B, NT, Ppad, nlv[u], pv[u], wv_[u], 0, P);
+            }
+        }
+        if (Tn < total) issue(Tn);   // the next tile's loads fly during this tile's DFT
+        const int f = __builtin_amdgcn_readfirstlane(TT / g.ntiles), tile = TT - f * g.ntiles;
+        if (tile == 0 && threadIdx.x == 0 && fp.count[f]) *fp.count[f] = 0;   // K3's detection counter
+        __syncthreads();   // the tile (and, the first time, the tables) in LDS
+        V* __restrict__ z = static_cast<V*>(fp.z[f]);
+        const StoreZq<V> sz{buf_rsrc(z, (unsigned)(B * g.nzc * P * g.NZ * sizeof(V))), lgNT, g.nzc, tile, P, half, ilog2(g.NZ)};
+        k1_dft_rq_r(g.rqR, Y, Ppad, B * NT, g.rqQ, twq, twp, sz);
+        __syncthreads();   // pass 2's reads of Y before the next DBF writes it
     }
 }
 
@@ -2359,6 +2597,19 @@ static int k1p_tpw(const Geometry& g) {
     return need <= k1_tpw(g) ? k1_tpw(g) : (need <= 2 * k1_tpw(g) ? 2 * k1_tpw(g) : 0);
 }
 
+// sub-tiles per wave of the factored-DFT K1 (one load round per tile): TPW or 2 TPW, else 0
+static int k1q_tpw(const Geometry& g) {
+    const int pt = g.prec == RSP_PREC_F64 ? 16 : 32;
+    const int need = (g.NT * ((g.P + pt - 1) / pt) + (K1_THREADS / 64) - 1) / (K1_THREADS / 64);
+    return need <= k1_tpw(g) ? k1_tpw(g) : (need <= 2 * k1_tpw(g) ? 2 * k1_tpw(g) : 0);
+}
+static size_t k1q_lds(const Geometry& g) {
+    return ((size_t)g.B * g.NT * g.Ppad + g.twq_elems + g.P) * cplx_bytes(g);
+}
+static bool k1q_fits(const Geometry& g) {
+    return !g.pow2P && g.rqQ > 0 && k1q_tpw(g) > 0 && k1q_lds(g) <= 160 * 1024 && g.ncu > 0 && !g.k1_tiled;
+}
+
 bool k1_persistent_fits(const Geometry& g) {
     const int pts = g.prec == RSP_PREC_F64 ? 8 : 16;   // FFT points per thread (k1p_pts)
     return g.pow2P && g.logP >= 6 && g.logP <= 8 && k1p_tpw(g) > 0 && k1p_lds(g) <= 160 * 1024 &&
@@ -2389,10 +2640,34 @@ static hipError_t launch_k1_t(const Geometry& g, const DevConsts& k, const Frame
         }
 #undef K1P_LAUNCH
     }
-    const size_t lds = ((size_t)g.B * g.NT * g.Ppad + g.P) * sizeof(cx<T>);
-    hipError_t e = allow_lds(k1_dbf_mtd<T, BMAX, CP>, lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k1_dbf_mtd<T, BMAX, CP>), dim3(g.ntiles, nf), dim3(K1_THREADS), lds, s, g, k, fp, mode);
+    // the persistent factored-DFT K1 for C <= 16 when one load round of at most 16 16-B cube loads
+    // per lane covers a tile (register budget: no scratch); otherwise the tiled kernel
+    if constexpr (CP <= 16) {
+        constexpr int NJ = CP / 4, MB = BMAX <= 8 ? 1 : 2, TPW = (16 / NJ) / MB > 0 ? (16 / NJ) / MB : 1;
+        if (mode == 3 && k1q_fits(g) && k1q_tpw(g) * NJ <= 16) {
+            const size_t ldsq = k1q_lds(g);
+            const int grid = std::min(g.ncu, nf * g.ntiles);
+            hipError_t e;
+            if (k1q_tpw(g) == TPW) {
+                if ((e = allow_lds(k1q_dbf_mtd<T, BMAX, CP, TPW>, ldsq)) != hipSuccess) return e;
+                hipLaunchKernelGGL((k1q_dbf_mtd<T, BMAX, CP, TPW>), dim3(grid), dim3(K1_THREADS), ldsq, s, g, k, fp, nf);
+            } else if constexpr (2 * TPW * NJ <= 16) {
+                if ((e = allow_lds(k1q_dbf_mtd<T, BMAX, CP, 2 * TPW>, ldsq)) != hipSuccess) return e;
+                hipLaunchKernelGGL((k1q_dbf_mtd<T, BMAX, CP, 2 * TPW>), dim3(grid), dim3(K1_THREADS), ldsq, s, g, k, fp, nf);
+            }
+            return hipGetLastError();
+        }
+    }
+    const bool rq = (mode & 2) && !g.pow2P && g.rqQ > 0;
+    const size_t lds = ((size_t)g.B * g.NT * g.Ppad + g.P + (rq ? g.twq_elems : 0)) * sizeof(cx<T>);
+    hipError_t e;
+    if (rq) {
+        if ((e = allow_lds(k1_dbf_mtd<T, BMAX, CP, true>, lds)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k1_dbf_mtd<T, BMAX, CP, true>), dim3(g.ntiles, nf), dim3(K1_THREADS), lds, s, g, k, fp, mode);
+    } else {
+        if ((e = allow_lds(k1_dbf_mtd<T, BMAX, CP, false>, lds)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k1_dbf_mtd<T, BMAX, CP, false>), dim3(g.ntiles, nf), dim3(K1_THREADS), lds, s, g, k, fp, mode);
+    }
     return hipGetLastError();
 }
 

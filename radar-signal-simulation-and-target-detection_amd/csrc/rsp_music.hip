@@ -912,10 +912,7 @@ __device__ bool me_fast_subspace(const double2 (&a)[16], int n, int t, int lane,
     // the scale 2^-e with max |a_ij| in [1/2, 1) after it (a power of two: exact), and ||sA A||_F^2
     double am = 0.0, a2 = 0.0;
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        am = fmax(am, fmax(fabs(a[u].x), fabs(a[u].y)));
-        a2 = fma(a[u].x, a[u].x, fma(a[u].y, a[u].y, a2));
-    }
+    for (int u = 0; u < 16; ++u) am = fmax(am, fmax(fabs(a[u].x), fabs(a[u].y)));
     am = wmaxd(am);
     if (lane == 0) gp[8 * NV + w] = am;
     __syncthreads();
@@ -926,7 +923,14 @@ __device__ bool me_fast_subspace(const double2 (&a)[16], int n, int t, int lane,
         double v[NV];
 #pragma unroll
         for (int k = 0; k < NV; ++k) v[k] = 0.0;
-        v[0] = a2 * sA * sA;
+        // squares of the scaled entries (|sA a| in [0, 1)): summed unscaled, entries below ~1e-154
+        // would underflow and leave ||C|| assumed 0 in the bound below
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const double xr = a[u].x * sA, xi = a[u].y * sA;
+            a2 = fma(xr, xr, fma(xi, xi, a2));
+        }
+        v[0] = a2;
         reduce(v, true);
         a2 = v[0];
     }
@@ -1555,10 +1559,19 @@ namespace {
                                  __FILE__, __LINE__);                                                  \
     } while (0)
 
+// What a launch's caller reads (music_run): only the peak indices (the block-power fast path may
+// replace the eigen-decomposition), also the pseudo-spectrum (full path: the spectrum is then the
+// eigensolver's to rounding), or also all N eigenvalues (full path, every eigenvalue).
+enum MusicWant { MU_WANT_PEAKS = 0, MU_WANT_SPECTRUM = 1, MU_WANT_EIGS = 2 };
+
 template <int MC>
-hipError_t launch_eig64(rsp_music_plan* p, int n_inst, int neig) {
+hipError_t launch_eig64(rsp_music_plan* p, int n_inst, int want) {
     const size_t lds = me_lds_bytes(MC, p->S);
-    const bool fast = neig <= 4 && MC <= 4;   // peaks-only: the fast-path instantiation
+    // neig: eigenvalues the kernel finds (all N when the caller reads them, else the M signal ones)
+    const int neig = want == MU_WANT_EIGS ? p->N : p->M;
+    // the fast-path instantiation only for peaks-only calls: a call that reads eigenvalues or the
+    // spectrum never takes it, whatever N and M are (an N <= 4 plan asks for neig = N <= 4 too)
+    const bool fast = want == MU_WANT_PEAKS && MC <= 4;
     const void* kf = fast ? reinterpret_cast<const void*>(k_music_eig64<MC, true>)
                           : reinterpret_cast<const void*>(k_music_eig64<MC, false>);
     if (lds > 64 * 1024) {
@@ -1576,9 +1589,10 @@ hipError_t launch_eig64(rsp_music_plan* p, int n_inst, int neig) {
     return hipGetLastError();
 }
 
-// all_eig: every eigenvalue is computed (the caller reads them); otherwise only the M signal
-// eigenvalues the vectors and the spectrum need (complex double)
-int music_run(rsp_music_plan* p, const void* dX, int n_inst, bool timed, float* ms, bool all_eig) {
+// want (MusicWant): MU_WANT_EIGS computes every eigenvalue (the caller reads them); otherwise only
+// the M signal eigenvalues the vectors and the spectrum need (complex double), and MU_WANT_PEAKS
+// allows the fast path
+int music_run(rsp_music_plan* p, const void* dX, int n_inst, bool timed, float* ms, int want) {
     if (n_inst < 1 || n_inst > p->max_batch)
         return rsp_set_error(RSP_ERR_INVALID, "n_inst %d outside 1..max_batch %d", n_inst, p->max_batch);
     MUCHK(hipSetDevice(p->device));
@@ -1598,7 +1612,7 @@ int music_run(rsp_music_plan* p, const void* dX, int n_inst, bool timed, float* 
     if (p->f64) {
         switch (p->M) {
 #define MU_EIG64(MC) \
-    case MC: MUCHK(launch_eig64<MC>(p, n_inst, all_eig ? p->N : p->M)); break;
+    case MC: MUCHK(launch_eig64<MC>(p, n_inst, want)); break;
             MU_EIG64(1) MU_EIG64(2) MU_EIG64(3) MU_EIG64(4) MU_EIG64(5) MU_EIG64(6) MU_EIG64(7) MU_EIG64(8)
 #undef MU_EIG64
         }
@@ -1803,7 +1817,9 @@ int32_t rsp_music_synthesize_device(rsp_music_plan* p, const rsp_music_scene* sc
 
 int32_t rsp_music_process_device(rsp_music_plan* p, const void* d_X, int32_t n_inst, rsp_music_out* out) {
     if (!p || !d_X) return rsp_set_error(RSP_ERR_INVALID, "null argument");
-    int rc = music_run(p, d_X, n_inst, false, nullptr, out && out->eigenvalues);
+    const int want = !out ? MU_WANT_PEAKS
+                          : out->eigenvalues ? MU_WANT_EIGS : out->spectrum_db ? MU_WANT_SPECTRUM : MU_WANT_PEAKS;
+    int rc = music_run(p, d_X, n_inst, false, nullptr, want);
     if (rc) return rc;
     if (!out) {
         MUCHK(hipStreamSynchronize(p->stream));
@@ -1841,11 +1857,20 @@ int32_t rsp_music_process(rsp_music_plan* p, const void* X, int32_t dtype, int32
 }
 
 int32_t rsp_music_profile(rsp_music_plan* p, const void* d_X, int32_t n_inst, int32_t iters, float* ms_out) {
+    return rsp_music_profile_ex(p, d_X, n_inst, iters, RSP_MUSIC_PEAKS, ms_out);
+}
+
+int32_t rsp_music_profile_ex(rsp_music_plan* p, const void* d_X, int32_t n_inst, int32_t iters, int32_t what,
+                             float* ms_out) {
     if (!p || !d_X || !ms_out || iters < 1) return rsp_set_error(RSP_ERR_INVALID, "bad argument");
+    if (what != RSP_MUSIC_PEAKS && what != RSP_MUSIC_SPECTRUM && what != RSP_MUSIC_EIGENVALUES)
+        return rsp_set_error(RSP_ERR_INVALID, "unknown profile form %d", what);
+    const int want = what == RSP_MUSIC_EIGENVALUES ? MU_WANT_EIGS
+                   : what == RSP_MUSIC_SPECTRUM ? MU_WANT_SPECTRUM : MU_WANT_PEAKS;
     double acc[2] = {0.0, 0.0};
     for (int it = 0; it < iters; ++it) {
         float ms[2];
-        int rc = music_run(p, d_X, n_inst, true, ms, false);   // as the bench's step (peaks only)
+        int rc = music_run(p, d_X, n_inst, true, ms, want);
         if (rc) return rc;
         acc[0] += ms[0];
         acc[1] += ms[1];

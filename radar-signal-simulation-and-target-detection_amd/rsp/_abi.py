@@ -80,6 +80,8 @@ class PlanOptions(ct.Structure):
                 ('flags', ct.c_int32)]
 
 
+RSP_MUSIC_PEAKS, RSP_MUSIC_SPECTRUM, RSP_MUSIC_EIGENVALUES = 0, 1, 2   # rsp_music_profile_ex
+
 RSP_MAT_CHAR, RSP_MAT_DOUBLE, RSP_MAT_SINGLE = 4, 6, 7
 RSP_MAT_OUT_F64, RSP_MAT_OUT_F32, RSP_MAT_OUT_CHAR = 1, 2, 3
 RSP_MAT_MAXDIMS = 8
@@ -196,6 +198,7 @@ PROTOTYPES = {
     'rsp_music_process_device': (ct.c_int32, [_P, _P, ct.c_int32, ct.POINTER(MusicOut)]),
     'rsp_music_synthesize_device': (ct.c_int32, [_P, ct.POINTER(MusicScene), ct.c_int32, ct.c_int32, ct.c_uint64, _P]),
     'rsp_music_profile': (ct.c_int32, [_P, _P, ct.c_int32, ct.c_int32, ct.POINTER(ct.c_float)]),
+    'rsp_music_profile_ex': (ct.c_int32, [_P, _P, ct.c_int32, ct.c_int32, ct.c_int32, ct.POINTER(ct.c_float)]),
     'rsp_music_fast_count': (ct.c_int32, [_P, ct.POINTER(ct.c_int32)]),
     'rsp_music_device_alloc': (ct.c_int32, [_P, ct.c_int64, ct.POINTER(_P)]),
     'rsp_music_device_free': (ct.c_int32, [_P, _P]),

@@ -48,13 +48,15 @@ class MusicPlan:
             pass
 
     # ---- outputs -------------------------------------------------------------------------
-    def _out(self, n, want_cov):
-        o = {'spectrum_db': np.zeros((n, self.S), np.float64), 'eig': np.zeros((n, self.N), np.float64),
-             'peaks': np.zeros((n, self.M), np.int32), 'n_peaks': np.zeros(n, np.int32)}
+    def _out(self, n, want_cov, want_eig=True):
+        o = {'spectrum_db': np.zeros((n, self.S), np.float64), 'peaks': np.zeros((n, self.M), np.int32),
+             'n_peaks': np.zeros(n, np.int32)}
+        if want_eig:
+            o['eig'] = np.zeros((n, self.N), np.float64)
         if want_cov:
             o['R'] = np.zeros((n, self.N, self.N, 2), np.float64)   # per instance: [b][a] = R(a, b)
         st = _abi.MusicOut(o['spectrum_db'].ctypes.data_as(_abi._dp),
-                           o['eig'].ctypes.data_as(_abi._dp),
+                           o['eig'].ctypes.data_as(_abi._dp) if want_eig else None,
                            o['peaks'].ctypes.data_as(ct.POINTER(ct.c_int32)),
                            o['n_peaks'].ctypes.data_as(ct.POINTER(ct.c_int32)),
                            o['R'].ctypes.data_as(_abi._dp) if want_cov else None)
@@ -68,8 +70,10 @@ class MusicPlan:
         o['angles_deg'] = np.where(pk > 0, self.scan_rad[np.maximum(pk - 1, 0)] * 180.0 / np.pi, np.nan)
         return o
 
-    def process(self, X, want_cov=False):
-        """X: complex [n, N, K] (or [N, K]) host snapshots -> dict of per-instance outputs."""
+    def process(self, X, want_cov=False, want_eig=True):
+        """X: complex [n, N, K] (or [N, K]) host snapshots -> dict of per-instance outputs.
+        ``want_eig=False``: the eigenvalues are not read (no 'eig' key), so complex double finds
+        only the M signal eigenvalues (the spectrum is still the full eigensolver's)."""
         X = np.asarray(X)
         if X.ndim == 2:
             X = X[None]
@@ -81,7 +85,7 @@ class MusicPlan:
             buf, dt = np.ascontiguousarray(np.transpose(X, (0, 2, 1))), _abi.RSP_C64
         else:
             buf, dt = np.ascontiguousarray(np.transpose(X.astype(np.complex128), (0, 2, 1))), _abi.RSP_C128
-        o, st = self._out(n, want_cov)
+        o, st = self._out(n, want_cov, want_eig)
         _abi.check(self._lib.rsp_music_process(self._h, buf.ctypes.data, dt, n, ct.byref(st)))
         return self._finish(o)
 
@@ -145,9 +149,13 @@ class MusicPlan:
         _abi.check(self._lib.rsp_music_fast_count(self._h, ct.byref(n)))
         return n.value
 
-    def profile(self, d_X, n_inst, iters=20):
+    def profile(self, d_X, n_inst, iters=20, what='peaks'):
+        """HIP-event times of the two stages for the form of call ``what``: 'peaks' (the bench's
+        step), 'spectrum' (spectrum_db read) or 'eigenvalues' (all N eigenvalues read)."""
+        forms = {'peaks': _abi.RSP_MUSIC_PEAKS, 'spectrum': _abi.RSP_MUSIC_SPECTRUM,
+                 'eigenvalues': _abi.RSP_MUSIC_EIGENVALUES}
         ms = (ct.c_float * 2)()
-        _abi.check(self._lib.rsp_music_profile(self._h, ct.c_void_p(d_X), n_inst, iters, ms))
+        _abi.check(self._lib.rsp_music_profile_ex(self._h, ct.c_void_p(d_X), n_inst, iters, forms[what], ms))
         return {'cov_ms': ms[0], 'eig_ms': ms[1]}
 
 

@@ -123,3 +123,60 @@ def test_bench_rank_census_two_ranks():
         assert [x['rank'] for x in c['ranks']] == [0, 1]
         assert [x['device'] for x in c['ranks']] == [0, 1]
         assert c['distinct_devices'] == 2
+
+
+CONFIG3_FRAMES, CONFIG3_WORLD = 512, 8
+
+
+def _config3_results(frames):
+    """Deterministic stand-in final_targets per frame id (0..3 targets; frames with none keep
+    their NaN marker row): what each rank's plan returns for its frames, without the chain."""
+    out = []
+    for f in frames:
+        n = (f * 7) % 4
+        out.append({'frame_idx': f, 'final_targets': [
+            {'Range': 1000.0 + 3.5 * f + j, 'Velocity': 0.25 * (f % 17) - j, 'Angle': 0.01 * f + j,
+             'Power': 1.0 / (f + j)} for j in range(n)]})
+    return out
+
+
+def _config3_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from rsp.dist import gather_rows, shard_frames as shard, _pack
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        mine = shard(CONFIG3_FRAMES, rank, world)
+        counts, bufs = gather_rows(_pack(_config3_results(mine)), rank, world)
+        rows = np.concatenate([b[:c] for c, b in zip(counts, bufs)])
+        q.put((rank, len(mine), counts, rows))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_config3_split_eight_ranks_equals_single_process():
+    """BASELINE config #3's actual split rehearsed as 8 processes (gloo, CPU): 512 frame ids
+    sharded by shard_frames (64 per rank, v8:164-190 frames are independent), each rank's packed
+    (frame_idx, Range, Velocity, Angle, Power) rows all-gathered through gather_rows -- the code
+    bench.py runs over RCCL.  Every rank must hold the one-process rows of frames 1..512, in frame
+    order, bit for bit."""
+    world = CONFIG3_WORLD
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_config3_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = dict((r, (n, c, rows)) for r, n, c, rows in (q.get(timeout=300) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from rsp.dist import _pack
+    want = _pack(_config3_results(list(range(1, CONFIG3_FRAMES + 1))))
+    assert [outs[r][0] for r in range(world)] == [CONFIG3_FRAMES // world] * world
+    for r in range(world):
+        n, counts, rows = outs[r]
+        assert sum(counts) == want.shape[0]
+        assert np.array_equal(rows, want, equal_nan=True)
+    f = want[:, 0]
+    assert np.all(np.diff(f) >= 0) and set(f.astype(int)) == set(range(1, CONFIG3_FRAMES + 1))

@@ -2,7 +2,8 @@
 
 Configurations: small (P=64), x2 (BASELINE #2, P=128), p256 (P=256), x4 (BASELINE #4:
 32C x 16B x 8192N x 256P, two MFMA row blocks, 5-block long segment, 32-cell K3 tiles) and
-reference (the v8 frame 16C x 13B x 5819N x 332P: direct-DFT K1, B=13 in BMAX=16), each
+reference (the v8 frame 16C x 13B x 5819N x 332P: the factored 4 x 83 slow-time DFT K1, B=13
+in BMAX=16), each
 through the complex-double plan (the default, MATLAB's arithmetic) and through the
 complex-single plan (the reference frame's device-synthesised cube rounded to complex64).
 
@@ -296,17 +297,24 @@ def test_profile_stages_reports_three_kernels():
     plan.close()
     assert [x['stage'] for x in st] == ['k1_dbf_mtd', 'k2_pc', 'k3_cfar']
     assert all(x['ms'] > 0 and x['bytes'] > 0 for x in st)
+    # K3's stage bytes = the rows under test of every beam's magnitude map (k3_map_bytes), the
+    # formula tests/test_bench_args.py checks against the PMC-measured traffic
+    import bench
+    sc = s['cfg']['Sig_Config']
+    G = sum(sc['point_prt_segments'])
+    assert st[2]['bytes'] == st[2]['frames'] * bench.k3_map_bytes(sc['prtNum'], G, sc['beam_num'], s['cfar'], 8)
 
 
 @pytest.mark.parametrize('prec', ['c128', 'c64'])
-@pytest.mark.parametrize('name', ['small', 'x2', 'p256'])
+@pytest.mark.parametrize('name', ['small', 'x2', 'p256', 'reference'])
 def test_persistent_k1_bit_identical_to_tiled_k1(name, prec):
-    """The persistent software-pipelined K1 (k1p_dbf_mtd, default) and the one-tile-per-workgroup
-    K1 (RSP_PLAN_K1_TILED) do the same operations in the same order: identical RDM bits and
+    """The persistent software-pipelined K1 (k1p_dbf_mtd for power-of-two P; k1q_dbf_mtd for the
+    factored DFT of the reference frame's P = 332) and the one-tile-per-workgroup K1
+    (RSP_PLAN_K1_TILED) do the same operations in the same order: identical RDM bits and
     detections, on the synchronous path and through the 8-frame queue."""
     s = scenario(name)
     tg = targets_for(name)
-    cube = noisy_cube(s, tg, dtype=np.complex128 if prec == 'c128' else np.complex64)
+    cube = _input_cube(name, s, tg).astype(np.complex128 if prec == 'c128' else np.complex64)
     outs, queued = [], []
     for tiled in (False, True):
         plan = Plan(s['cfg'], s['cfar'], s['clus'], s['pre_p'], frames_per_launch=8, precision=prec, k1_tiled=tiled)

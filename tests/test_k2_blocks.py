@@ -7,7 +7,8 @@ segment exercises only M = 1024 there.  These configurations keep x2's long segm
 1860 gates: one 2560-point block) and shorten or lengthen the medium pulse and gate count
 (fun_process_single_frame.m:115-116 with N_fft / MF_medium_fft from
 main_simulate_echoes_with_array_v8.m:104-123), so that the medium segment takes M = 128, 256, 512
-and 2048 (16, 8, 4 and 1 rows per workgroup).  The device RD map must match the complex128 oracle to
+and 2048 (16, 8, 4 and 1 rows per workgroup); 'narrow2700' widens the narrow segment past what a
+2560-point workgroup stages.  The device RD map must match the complex128 oracle to
 1e-12 of its maximum (complex double) and the CFAR detection lists must be identical; in complex
 single (2-per-CU workgroups, the same block sizes) the maps within 2e-5.
 """
@@ -30,6 +31,10 @@ CFGS = {
     'med256': ((0.16e-6, 2e-6, 28e-6), (228, 200, 1860), 4096, 256),
     'med512': ((0.16e-6, 4e-6, 28e-6), (228, 400, 1860), 4096, 512),
     'med2048': ((0.16e-6, 8e-6, 28e-6), (228, 1800, 1860), 8192, 2048),
+    # a 2700-gate narrow segment: its direct-FIR rows (~2.7 k samples) do not fit a 2560-point
+    # workgroup, so the plan falls back to 2-per-CU workgroups (RSP_K2_POINTS) that still run the
+    # long segment's 2560-point block (this used to fail plan creation)
+    'narrow2700': ((0.16e-6, 8e-6, 28e-6), (2700, 723, 1860), 8192, 1024),
 }
 
 

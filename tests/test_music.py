@@ -305,3 +305,71 @@ def test_music_scale_invariance(music_case, scale):
         assert o['n_peaks'][i] == c['out']['n_peaks'][i]
         live = c['out']['spectrum_db'][i] > -60.0
         assert np.abs(o['spectrum_db'][i][live] - c['out']['spectrum_db'][i][live]).max() <= 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('N,M', [(4, 2), (3, 2), (4, 3)])
+def test_music_small_n_full_call_returns_every_eigenvalue(N, M):
+    """with N <= 4 a call that reads the eigenvalues asks for neig = N <= 4, which
+    must not select the peaks-only fast path (it writes no eigenvalue when it converges).  The
+    output array starts at zero, so an unwritten eigenvalue fails the comparison with LAPACK's
+    eigvalsh of the same covariance; the spectrum and peaks are the oracle's too."""
+    from rsp.music import MusicPlan
+    K, n = 64, 3
+    scan = np.linspace(-np.pi / 2, np.pi / 2, 60)
+    rng = np.random.default_rng(100 * N + M)
+    X = rng.standard_normal((n, N, K)) + 1j * rng.standard_normal((n, N, K))
+    X[:, :, :4] *= 5.0
+    plan = MusicPlan(N, K, M, scan, 0.5, max_batch=n)
+    try:
+        o = plan.process(X)
+        assert plan.fast_count() == 0
+        pk, npk = plan.peaks(X)   # the peaks-only call may take the fast path; same answer
+    finally:
+        plan.close()
+    for i in range(n):
+        R = X[i] @ X[i].conj().T / K
+        want = np.sort(np.linalg.eigvalsh(R))[::-1]
+        assert np.abs(o['eig'][i] - want).max() <= 1e-11 * want.max(), (o['eig'][i], want)
+        ref = mu.music_1d(X[i], M, scan, 0.5)
+        live = ref['spectrum_db'] > -60.0
+        assert np.abs(o['spectrum_db'][i][live] - ref['spectrum_db'][live]).max() <= 1e-7
+        # the device pads the M peak slots with 0 when findpeaks finds fewer (N = 4, M = 3 here)
+        have = [int(p) for p in o['peaks'][i] if p > 0]
+        assert have == [int(p) for p in ref['peaks']] == [int(p) for p in pk[i] if p > 0]
+        assert list(o['peaks'][i]) == list(pk[i])
+        assert o['n_peaks'][i] == ref['n_peaks'] == npk[i]
+
+
+@pytest.mark.gpu
+def test_music_spectrum_call_without_eigenvalues(music_case):
+    """a call that reads spectrum_db but not the eigenvalues (rsp_mex('music')
+    with two outputs) runs the full eigensolver for the M signal eigenvalues -- never the fast path,
+    whose subspace is bounded only to 1e-12 -- so its spectrum holds the oracle tolerance."""
+    c = music_case
+    o = c['plan'].process(c['X'][:4], want_eig=False)
+    assert 'eig' not in o
+    if c['prec'] == 'c128':
+        assert c['plan'].fast_count() == 0
+    for i in range(4):
+        ref = c['ref'][i]['spectrum_db']
+        live = ref > -60.0
+        assert np.abs(o['spectrum_db'][i][live] - ref[live]).max() <= c['tol']['db']
+        assert list(o['peaks'][i]) == list(c['out']['peaks'][i])
+        assert o['n_peaks'][i] == c['out']['n_peaks'][i]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('scale', [1e-80, 1e-60, 1e40])
+def test_music_peaks_only_scale_invariance(music_case, scale):
+    """The peaks-only call (fast path) at scaled snapshots: ADVICE r5 (low) -- the fast path's
+    ||A||_F^2 is summed from the scaled entries, so R ~ 1e-160 (X ~ 1e-80) no longer underflows the
+    squares and the Davis-Kahan bound keeps its ||C|| term.  Peaks and counts are the unscaled ones."""
+    c = music_case
+    if c['prec'] != 'c128':
+        pytest.skip('complex single cannot hold R at these scales')
+    pk, npk = c['plan'].peaks(c['X'][:2] * scale)
+    assert np.array_equal(pk, c['out']['peaks'][:2])
+    assert np.array_equal(npk, c['out']['n_peaks'][:2])
+    if c['name'] in ('config5', 'music_1d'):
+        assert c['plan'].fast_count() == 2
