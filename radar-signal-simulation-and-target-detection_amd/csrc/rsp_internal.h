@@ -3,60 +3,15 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#ifndef RSP_MAX_F
 #define RSP_MAX_F 8          // frames batched per launch
-#endif
 #define RSP_LANES 4          // max streams of the throughput queue (batches in flight)
-#ifndef RSP_NLANES
 #define RSP_NLANES 3         // streams the throughput queue uses (<= RSP_LANES)
-#endif
-#ifndef RSP_Z_LINE
-#define RSP_Z_LINE 0   // bytes of one row's z chunk (0: NT samples, the K1 tile width)
-#endif
-#ifndef RSP_K2_POINTS
 #define RSP_K2_POINTS 4096   // complex points per pulse-compression workgroup (Geometry::k2_pts)
-#endif
-#ifndef RSP_K2_M1024MIX
-#define RSP_K2_M1024MIX 0    // 3-per-CU K2 plans run 1024-point blocks as 8 x 16 x 8 (1) or 16 x 4 x 16 (0)
-#endif
-#ifndef RSP_K1_AREL
-#define RSP_K1_AREL 0        // persistent K1 with two MFMA row blocks re-reads the second's operands per sub-tile
-#endif
-#ifndef RSP_K3_BUFLD
-#define RSP_K3_BUFLD 1       // complex-single k3_cfar's tile loads through buffer resources (branch-free)
-#endif
-#ifndef RSP_K2_MODE3_ALL
-#define RSP_K2_MODE3_ALL 0   // every complex-double plan runs k2_pc at 3 workgroups per CU (A/B builds)
-#endif
-#ifndef RSP_K2_MIXPTS
 #define RSP_K2_MIXPTS 2560   // Geometry::k2_pts of a complex-double plan with a 2560-point block
-#endif
 #define K2_THREADS 256       // threads per pulse-compression workgroup (16 points each)
 #define RSP_THREADS 256
-// Compile-time kernel choices (defaults = the shipped library; other values only for A/B
-// timing builds, `make ab`): overlap-save radix plan palindromic (1) or standard (0); compact
-// (1) or full (0) twiddle rows; LDS pad shift of complex-double overlap-save rows.
-#ifndef RSP_K2_PAL
-#define RSP_K2_PAL 1
-#endif
-#ifndef RSP_K2_CMP
-#define RSP_K2_CMP 1
-#endif
-// 2560-point mixed-radix overlap-save blocks (1) or powers of two only (0)
-#ifndef RSP_K2_MIX
-#define RSP_K2_MIX 1
-#endif
-// pulse-compression workgroups dispatched with the jobs interleaved (1) or job after job (0)
-#ifndef RSP_K2_ORDER
-#define RSP_K2_ORDER 1
-#endif
-// Ns = 1 pass outputs of the overlap-save blocks XOR-swizzled (1) or padded like the others (0)
-#ifndef RSP_K2_XOR
-#define RSP_K2_XOR 1
-#endif
-#ifndef RSP_K2_SH64
-#define RSP_K2_SH64 5
-#endif
+// The kernel variants measured and not kept (profiles/EXPERIMENTS.md) were removed in round 6;
+// the library has one code path per configuration and no compile-time A/B switches.
 
 // Arithmetic of a plan: every device buffer, table and operation of the chain is in one of
 // these.  PREC_F64 is MATLAB's complex double (the reference's arithmetic, fsf:47,92,101,131);
@@ -152,9 +107,6 @@ struct Geometry {
 __host__ __device__ inline bool k3_fast_params(const Geometry& g) {
     return g.refR == 5 && g.refV == 5 && g.guardR == 10 && g.guardV == 10 && (g.cfar_RT == 32 || g.cfar_RT == 64);
 }
-#ifndef RSP_K3_NOHALO
-#define RSP_K3_NOHALO 1   // fast-path K3 tiles without the right range halo and the Doppler halo rows
-#endif
 
 // K3 tiles: range cells from the first cell under test rounded down to 4, cfar_RT per tile
 // (k3_cfar, launch_k3, rsp_profile_stages).
@@ -169,7 +121,7 @@ __host__ __device__ inline int k3_ntiles(const Geometry& g) {
 // clipped to G); each beam's map is read by two pairs, the second read an L2 hit (XCD-aware
 // order).  The general path reads whole maps.  bench.py / tests/test_bench_args.py restate it.
 __host__ __device__ inline long long k3_map_bytes(const Geometry& g, int real_bytes) {
-    if (RSP_K3_NOHALO && k3_fast_params(g)) {
+    if (k3_fast_params(g)) {
         const int hV = g.refV + g.guardV, c0 = (g.refR + g.guardR) & ~3;
         const int rows = g.P - 2 * hV > 0 ? g.P - 2 * hV : 0;
         const int c1 = c0 + k3_ntiles(g) * g.cfar_RT < g.G ? c0 + k3_ntiles(g) * g.cfar_RT : g.G;
@@ -201,7 +153,7 @@ struct DevConsts {
     const void* taps;        // narrow FIR taps, real
     const void* H;           // overlap-save spectra, 1/M scaled, complex
     const void* twM;         // per-pass Stockham twiddles of each overlap-save block size, complex
-    const int* k2order;      // pulse-compression workgroup dispatch order (RSP_K2_ORDER): job kinds interleaved
+    const int* k2order;      // pulse-compression workgroup dispatch order: job kinds interleaved
     const double* range_axis;
     const double* velocity_axis;
     const double* beam_angles;

@@ -111,12 +111,8 @@ __device__ __forceinline__ void buf_st1(__amdgpu_buffer_rsrc_t r, unsigned off, 
 // Non-temporal z and RDM stores: z (50 MB per frame, read back by K2 after the whole launch) and
 // the RDM (never re-read on the device) only evict lines from L2 and the Infinity Cache
 // (interleaved A/B: K1 -5.5 %, k2_pc -1.2 %).
-#ifndef RSP_Z_AUX
 #define RSP_Z_AUX 2     // K1's z stores
-#endif
-#ifndef RSP_RDM_AUX
 #define RSP_RDM_AUX 2   // K2's RDM stores
-#endif
 
 // Diagnostic builds (-DRSP_DEBUG_KNOBS) only: K2 phase stamps.  Workgroup (f, x) of a k2_pc
 // launch writes s_memrealtime (100 MHz) at its phase boundaries into rsp_k2_trace[(f G + x) 8 +
@@ -850,16 +846,45 @@ __device__ __forceinline__ void k1_dft_rq(V* buf, int rs, int ncols, int Q, cons
                 A[r] = y0;
                 Bv[r] = V{};
             }
-#pragma unroll 2
-            for (int n = 1; n <= Qh; ++n) {
-                const V sv = col[n], dv = col[Q - n];
-                const V* t = tw + (n - 1) * RQ_RK;
+            // software-pipelined: step n + 1's operands are read while step n computes, so one LDS
+            // latency is exposed per step instead of one per (cos, sin) pair.  The reads past the
+            // last step (s_(Qh+1), d_Qh, the next table row) stay inside the LDS tile / tables and
+            // are never used.  Pointer steps keep every address a base plus an immediate offset.
+            // Two register sets alternate: the reads of the step after next go out before this
+            // step's FMAs (the scheduling barriers keep that order), so a read has a whole step of
+            // FMAs to land.  Steps are taken in pairs; the second step of the last pair exists only
+            // when Qh is even (uniform).
+            const V* ps = col + 1;
+            const V* pd = col + Q - 1;
+            const V* pt = tw;
+            V s0 = ps[0], d0 = pd[0], t0[RQ_RK];
+#pragma unroll
+            for (int r = 0; r < RQ_RK; ++r) t0[r] = pt[r];   // (cos, sin): the same address in every lane
+            auto fma_step = [&](const V& sv, const V& dv, const V (&tc)[RQ_RK]) {
 #pragma unroll
                 for (int r = 0; r < RQ_RK; ++r) {
-                    const V cs = t[r];   // (cos, sin)(2 pi k1 n / Q): the same address in every lane
-                    A[r] += cs.x * sv;
-                    Bv[r] += cs.y * dv;
+                    A[r] += tc[r].x * sv;
+                    Bv[r] += tc[r].y * dv;
                 }
+            };
+            for (int n = 1; n <= Qh; n += 2) {
+                const V s1 = ps[1], d1 = pd[-1];
+                V t1[RQ_RK];
+#pragma unroll
+                for (int r = 0; r < RQ_RK; ++r) t1[r] = pt[RQ_RK + r];
+                __builtin_amdgcn_sched_barrier(0);
+                fma_step(s0, d0, t0);
+                __builtin_amdgcn_sched_barrier(0);
+                ps += 2;
+                pd -= 2;
+                pt += 2 * RQ_RK;
+                s0 = ps[0];
+                d0 = pd[0];
+#pragma unroll
+                for (int r = 0; r < RQ_RK; ++r) t0[r] = pt[r];
+                __builtin_amdgcn_sched_barrier(0);
+                if (n + 1 <= Qh) fma_step(s1, d1, t1);
+                __builtin_amdgcn_sched_barrier(0);
             }
             if (sub < NS) {
 #pragma unroll
@@ -885,8 +910,11 @@ struct StoreZq {
         int v = o + half;
         v = v >= P ? v - P : v;
         const int np = (tile << lgNT) + nl;
-        buf_st<RSP_Z_AUX>(z, (unsigned)((((b * nzc + (np >> lgNZ)) * P + v) << lgNZ) + (np & ((1 << lgNZ) - 1))) *
-                                 (unsigned)sizeof(V), x);
+        // default cache policy, not non-temporal: one store instruction writes 4 consecutive bins
+        // (64 B) of each column and the next one of the wave the other half of the 128-B line,
+        // which then merge in L2 (non-temporal partial lines went to HBM unmerged: 1.8x the bytes)
+        buf_st<0>(z, (unsigned)((((b * nzc + (np >> lgNZ)) * P + v) << lgNZ) + (np & ((1 << lgNZ) - 1))) *
+                         (unsigned)sizeof(V), x);
     }
 };
 
@@ -1101,14 +1129,10 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
     const int lane = threadIdx.x & 63, grp = lane >> 4, col = lane & 15;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: nlv[] and n are scalar
     const T* At = static_cast<const T*>(k.Atab);
-    // the conj(W) operands of the MFMA row blocks held in registers for the kernel's life; with
-    // AREL the second row block's are re-read (L1/L2-resident, 2 x NJ x 64 values) in each
-    // sub-tile's DBF instead (x4: 32 VGPRs fewer across the Stockham passes)
-    constexpr bool AREL = MB == 2 && RSP_K1_AREL;
-    constexpr int MBR = AREL ? 1 : MB;
+    // the conj(W) operands of the MFMA row blocks held in registers for the kernel's life
     T are[MB][NJ], aim[MB][NJ];
 #pragma unroll
-    for (int mb = 0; mb < MBR; ++mb)
+    for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             are[mb][j] = At[((mb * NJ + j) * 2 + 0) * 64 + lane];
@@ -1171,15 +1195,6 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
 #pragma unroll
                 for (int a = 0; a < D::NACC; ++a) acc[mb][a] = typename D::Acc{};
             if (vld[u]) {   // samples past the used ones: zero columns, like k1_dbf_mtd's n = -1
-                if constexpr (AREL) {
-                    int la = lane;
-                    asm volatile("" : "+v"(la));   // opaque: keeps the loads here (not hoisted out of the tile loop)
-#pragma unroll
-                    for (int j = 0; j < NJ; ++j) {
-                        are[1][j] = At[((NJ + j) * 2 + 0) * 64 + la];
-                        aim[1][j] = At[((NJ + j) * 2 + 1) * 64 + la];
-                    }
-                }
 #pragma unroll
                 for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
@@ -1246,58 +1261,54 @@ template <class T, int BMAX, int CP, int TPW>
 __global__ __launch_bounds__(K1_THREADS, 1) void k1q_dbf_mtd(Geometry g, DevConsts k, FramePtrs fp, int nf) {
     typedef cx<T> V;
     typedef Dbf<T> D;
-    V* Y = reinterpret_cast<V*>(rsp_lds);   // tile [B][NT][Ppad] | twQ | W_P^i
+    // LDS: tile [B][NT][Ppad] | twQ | W_P^i | the DBF's MFMA A operands (Atab) -- read from LDS
+    // per sub-tile rather than held in registers, which pass 2 needs for its operands in flight
+    constexpr int NJ = CP / 4, MB = BMAX <= 8 ? 1 : 2;
+    V* Y = reinterpret_cast<V*>(rsp_lds);
     const int B = g.B, C = g.C, P = g.P, NT = g.NT, Ppad = g.Ppad;
     V* twq = Y + B * NT * Ppad;
     V* twp = twq + g.twq_elems;
+    T* Al = reinterpret_cast<T*>(twp + P);   // [MB][NJ][Re, Im][64]
     const int total = nf * g.ntiles;
     int TT = blockIdx.x;
     if (TT >= total) return;
     {
         const V* __restrict__ tq = static_cast<const V*>(k.twQ);
         const V* __restrict__ tp = static_cast<const V*>(k.twP);
+        const T* __restrict__ At = static_cast<const T*>(k.Atab);
         for (int i = threadIdx.x; i < g.twq_elems; i += K1_THREADS) twq[i] = tq[i];
         for (int i = threadIdx.x; i < P; i += K1_THREADS) twp[i] = tp[i];
+        for (int i = threadIdx.x; i < MB * NJ * 2 * 64; i += K1_THREADS) Al[i] = At[i];
     }
-    constexpr int NJ = CP / 4, MB = BMAX <= 8 ? 1 : 2;
+    __syncthreads();   // the first DBF reads Atab entries other waves wrote
     constexpr int PT = 16 * D::PPL;
     const int lane = threadIdx.x & 63, grp = lane >> 4, col = lane & 15;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const T* At = static_cast<const T*>(k.Atab);
-    T are[MB][NJ], aim[MB][NJ];
-#pragma unroll
-    for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            are[mb][j] = At[((mb * NJ + j) * 2 + 0) * 64 + lane];
-            aim[mb][j] = At[((mb * NJ + j) * 2 + 1) * 64 + lane];
-        }
     const int ptiles = (P + PT - 1) / PT, ntp = NT * ptiles;
     const T* __restrict__ win = static_cast<const T*>(k.win);
     int nlv[TPW], pv[TPW];
     T wv_[TPW][D::NACC];
 #pragma unroll
     for (int u = 0; u < TPW; ++u) {
-        const int t = wv * TPW + u;
+        // round-robin over the waves: a tile's ntp sub-tiles (21 at the reference frame) split
+        // 3/3/3/3/3/2/2/2 rather than 4/4/4/4/4/1, so that the waves sharing a SIMD (w, w + 4)
+        // carry 6 + 5 + 5 + 5 of the MFMA work instead of 8 + 5 + 4 + 4
+        const int t = u * (K1_THREADS / 64) + wv;
         const int nl = t / ptiles;
         pv[u] = (t - nl * ptiles) * PT + D::PPL * col;
         nlv[u] = t < ntp ? nl : -1;   // wave-uniform
 #pragma unroll
         for (int a = 0; a < D::NACC; ++a) wv_[u][a] = (nlv[u] >= 0 && pv[u] + a < P) ? win[pv[u] + a] : (T)0;
     }
-    const size_t NPc = (size_t)g.cpitch;
-    unsigned loff[TPW][NJ];
-#pragma unroll
-    for (int u = 0; u < TPW; ++u)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-            loff[u][j] = (unsigned)(((size_t)min(4 * j + grp, C - 1) * NPc + pv[u]) * sizeof(V));
-    const unsigned cube_bytes = (unsigned)((size_t)C * NPc * sizeof(V));
+    const unsigned NPc = (unsigned)g.cpitch;
+    const unsigned cube_bytes = (unsigned)((size_t)C * g.cpitch * sizeof(V));
     typename D::Ld xv[TPW][NJ];
     bool vld[TPW];
     auto issue = [&](int Tn) {   // cube loads of tile Tn (fsf:93 operands) into xv
         const int f = __builtin_amdgcn_readfirstlane(Tn / g.ntiles), tile = Tn - f * g.ntiles;
         const __amdgpu_buffer_rsrc_t xr = buf_rsrc(fp.in[f], cube_bytes);
+        int gq = grp;
+        asm volatile("" : "+v"(gq));   // the lane offsets are formed here, not kept live across the DFT
 #pragma unroll
         for (int u = 0; u < TPW; ++u) {
             const int np = tile * NT + nlv[u];
@@ -1305,8 +1316,10 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1q_dbf_mtd(Geometry g, DevCons
             if (vld[u]) {
                 const int soff = used_sample(g, np) * P * (int)sizeof(V);
 #pragma unroll
-                for (int j = 0; j < NJ; ++j)   // non-temporal: the cube is read exactly once
-                    xv[u][j] = D::bits(__builtin_amdgcn_raw_buffer_load_b128(xr, (int)loff[u][j], soff, 2));
+                for (int j = 0; j < NJ; ++j) {   // non-temporal: the cube is read exactly once
+                    const unsigned lo = ((unsigned)min(4 * j + gq, C - 1) * NPc + (unsigned)pv[u]) * (unsigned)sizeof(V);
+                    xv[u][j] = D::bits(__builtin_amdgcn_raw_buffer_load_b128(xr, (int)lo, soff, 2));
+                }
             }
         }
     };
@@ -1328,7 +1341,9 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1q_dbf_mtd(Geometry g, DevCons
 #pragma unroll
                     for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
-                        for (int j = 0; j < NJ; ++j) D::mma(acc[mb], are[mb][j], aim[mb][j], xv[u][j]);
+                        for (int j = 0; j < NJ; ++j)
+                            D::mma(acc[mb], Al[((mb * NJ + j) * 2 + 0) * 64 + lane], Al[((mb * NJ + j) * 2 + 1) * 64 + lane],
+                                   xv[u][j]);
                 }
                 dbf_store<T, MB>(Yf, acc, grp, B, NT, Ppad, nlv[u], pv[u], wv_[u], 0, P);
             }
@@ -1427,7 +1442,7 @@ __device__ __forceinline__ ZWin zrow_window(const Geometry& g, const V* z, int r
 // ds_read_b128 of a pass conflict-free (a pad per 16 would shift lanes 20-27 of a lane group
 // onto lane 12's bank), and the stride-16 stores of the two radix-16 Ns = 1 passes 2-way
 // (tools/ab/lds_conflicts64.py)
-template <class T> constexpr int k2_sh() { return sizeof(T) == 4 ? 5 : RSP_K2_SH64; }
+template <class T> constexpr int k2_sh() { return 5; }
 // LDS complex slots of a workgroup's rows: pts points (Geometry::k2_pts) + their pads
 __host__ __device__ constexpr int k2_lds_data(int pts, int sh) { return pts + (pts >> sh); }
 
@@ -1437,16 +1452,16 @@ __host__ __device__ constexpr int k2_lds_data(int pts, int sh) { return pts + (p
 // conjugation happens in load_tw), so one copy serves both.
 constexpr bool k2_tw_sym(int LGM) {
     for (int q = 0; q < n_passes(LGM); ++q)
-        if (rad_bits_p(LGM, q, false, RSP_K2_PAL) != rad_bits_p(LGM, n_passes(LGM) - 1 - q, false, RSP_K2_PAL))
+        if (rad_bits_p(LGM, q, false, true) != rad_bits_p(LGM, n_passes(LGM) - 1 - q, false, true))
             return false;
     return true;
 }
 constexpr int k2_tw_lds(int LGM) {
-    return tw_total(LGM, false, RSP_K2_CMP, RSP_K2_PAL) +
-           (k2_tw_sym(LGM) ? 0 : tw_total(LGM, true, RSP_K2_CMP, RSP_K2_PAL));
+    return tw_total(LGM, false, true, true) +
+           (k2_tw_sym(LGM) ? 0 : tw_total(LGM, true, true, true));
 }
 constexpr int k2_tw_lds_max() {
-    int m = 16 * tw_row(10, RSP_K2_CMP) + 160 * tw_row(16, RSP_K2_CMP);   // k2_fft_job_mix<2560>
+    int m = 16 * tw_row(10, true) + 160 * tw_row(16, true);   // k2_fft_job_mix<2560>
     for (int lg = 6; lg <= 11; ++lg) m = k2_tw_lds(lg) > m ? k2_tw_lds(lg) : m;
     return m;
 }
@@ -1514,7 +1529,7 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     constexpr int rs = M + (M >> SH);
     constexpr int NP = n_passes(LGM);
     static_assert(NP >= 2, "overlap-save block needs >= 2 FFT passes");
-    constexpr bool PAL = RSP_K2_PAL, CMP = RSP_K2_CMP;
+    constexpr bool PAL = true, CMP = true;
     constexpr int RB0 = rad_bits_p(LGM, 0, false, PAL), R0 = 1 << RB0, NB0 = 16 / R0, nb0 = M / R0;
     constexpr int RBL = rad_bits_p(LGM, NP - 1, false, PAL), RL = 1 << RBL, NBL = 16 / RL;   // last forward pass
     const int P = g.P, G = g.G;
@@ -1595,7 +1610,7 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     const V* twI = k2_tw_sym(LGM) ? twL : twL + NTWF;
     // forward pass 0 (Ns = 1, no twiddles) straight from the loaded samples
     // the Ns = 1 passes' outputs XOR-swizzled (sh_store) when a middle pass reads them (3 passes)
-    constexpr int XZ = (NP == 3 && R0 == 16 && RL == 16 && RSP_K2_XOR) ? 1 : 0;
+    constexpr int XZ = (NP == 3 && R0 == 16 && RL == 16 && 1) ? 1 : 0;
     sh_store<R0, false, NB0, SH, K2_THREADS, LGM, 0, XZ>(v0, rs, rows, StoreLds<V>{L});
     __syncthreads();
     K2_STAMP(1);
@@ -1675,7 +1690,7 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
     static_assert(M == R0 * R1 * R0, "palindromic 3-pass plan");
     constexpr int rows = M >= 2048 ? 1 : 2048 / M;
     constexpr int rs = M + (M >> SH);
-    constexpr bool CMP = RSP_K2_CMP;
+    constexpr bool CMP = true;
     constexpr int nb0 = M / R0;                                          // radix-R0 butterflies per row
     constexpr int NB0 = (nb0 * rows + K2_THREADS - 1) / K2_THREADS;
     constexpr int NB1 = ((M / R1) * rows + K2_THREADS - 1) / K2_THREADS;
@@ -1721,7 +1736,7 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
     for (int e = threadIdx.x; e < NTWF; e += K2_THREADS) twL[e] = twl[e];
     const V* twF = twL;
     const V* twI = twF;   // palindrome: the reversed plan's table is the forward one
-    constexpr int XZ = R0 == 16 ? RSP_K2_XOR : 0;   // Ns = 1 outputs XOR-swizzled (see sh_store)
+    constexpr int XZ = R0 == 16 ? 1 : 0;   // Ns = 1 outputs XOR-swizzled (see sh_store)
     shg_store<R0, false, NB0, SH, K2_THREADS, M, 1, XZ>(v0, rs, rows, StoreLds<V>{L}, tid);
     __syncthreads();
     K2_STAMP(1);
@@ -1771,19 +1786,13 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
 // k2_epilogue): without them the last pass peaks at 188 VGPRs.  WGS = 2 (4096-point workgroups,
 // 76 KB of LDS) keeps H in registers from the start and stores the gates from the last pass,
 // which measured faster at that occupancy (x2 at 2 per CU: 225 vs 248 us per 8 frames).
-#ifndef RSP_K2_EPI3
-#define RSP_K2_EPI3 1
-#endif
-#ifndef RSP_K2_EPI2
-#define RSP_K2_EPI2 0
-#endif
 template <class T, int WGS>
 __global__ __launch_bounds__(K2_THREADS, WGS) void k2_pc(Geometry g, DevConsts k, FramePtrs fp, int rows_total) {
-    constexpr bool EPI = WGS >= 3 ? RSP_K2_EPI3 : RSP_K2_EPI2;
+    constexpr bool EPI = WGS >= 3;
     typedef cx<T> V;
     V* L = reinterpret_cast<V*>(rsp_lds);   // overlap-save rows | narrow: staged rows + taps
     const int f = blockIdx.y;
-    const int wg = RSP_K2_ORDER ? k.k2order[blockIdx.x] : blockIdx.x;
+    const int wg = k.k2order[blockIdx.x];   // the plan's dispatch order (job kinds interleaved)
     int ji = 0;
     while (ji + 1 < g.njobs && wg >= g.jobs[ji + 1].wg_begin) ++ji;
     const K2Job job = g.jobs[ji];
@@ -1808,12 +1817,7 @@ __global__ __launch_bounds__(K2_THREADS, WGS) void k2_pc(Geometry g, DevConsts k
                 case 7: k2_fft_job<T, 7, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
                 case 8: k2_fft_job<T, 8, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
                 case 9: k2_fft_job<T, 9, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-                case 10:   // 8 x 16 x 8 (the plan builds its twiddles for it, RSP_K2_M1024MIX)
-                    if constexpr (RSP_K2_M1024MIX)
-                        k2_fft_job_mix<T, 1024, 8, 16, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L);
-                    else
-                        k2_fft_job<T, 10, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L);
-                    break;
+                case 10: k2_fft_job<T, 10, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
                 default: k2_fft_job<T, 11, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
             }
         } else {
@@ -2022,15 +2026,8 @@ __device__ __forceinline__ void s9_estimate(const S9Consts& k, SF sval, int P, i
 
 #define K3_QCAP 1024
 
-#ifndef K3_VEC
-#define K3_VEC 8   // 16-B loads per beam per thread in flight (halo-less 98-row tiles: 8 -> 120 rows per sweep; 12 measured 43.7 vs 36.8 us)
-#endif
-#ifndef RSP_K3_WGS
+#define K3_VEC 8       // 16-B loads per beam per thread in flight (halo-less 98-row tiles: 8 -> 120 rows per sweep)
 #define RSP_K3_WGS 3   // k3_cfar workgroups per CU the register budget is sized for
-#endif
-#ifndef RSP_K3_PREFILTER
-#define RSP_K3_PREFILTER 1   // exact left-slice prefilter before the full GOCA test (0: A/B builds)
-#endif
 
 constexpr int floor4(int x) { return x >= 0 ? (x & ~3) : -((-x + 3) & ~3); }
 
@@ -2062,11 +2059,10 @@ __global__ __launch_bounds__(RSP_THREADS, RSP_K3_WGS) void k3_cfar(Geometry g, D
     constexpr int HRC = ((RR + GR > 2 ? RR + GR : 2) + 3) & ~3;   // = g.cfar_hR (rsp_plan.cpp)
     // = g.cfar_W; complex double rows get 2 extra cells (stride 132 dwords = 4 mod 64 banks), see
     // the row-group order of the CFAR loop
-    // NOH (RSP_K3_NOHALO, fast path): the tile holds the band's own cells only, no halo; the
+    // NOH (the fast path): the tile holds the band's own cells only, no halo; the
     // prefilter takes whichever range slice lies inside the tile, survivors and S9 read the rest
     // from the maps
-    constexpr bool NOH = FAST && RSP_K3_NOHALO;
-    static_assert(!NOH || RSP_K3_PREFILTER, "halo-less K3 tiles need the prefilter path");
+    constexpr bool NOH = FAST;
     constexpr int WC = ((RTC + (NOH ? 0 : 2) * HRC + 3) & ~3) + (sizeof(T) == 8 ? 2 : 0);
     // XCD-aware order (bijective swizzle, cdna_hip_programming.md T1): the workgroups that
     // share an XCD take consecutive (tile, pair) ids with pairs fastest, so beam b's tile --
@@ -2116,7 +2112,7 @@ __global__ __launch_bounds__(RSP_THREADS, RSP_K3_WGS) void k3_cfar(Geometry g, D
         const T* pa = MA + (size_t)(vt0 + rr) * Gp + r;
         const T* pb = MB + (size_t)(vt0 + rr) * Gp + r;
         U* sd = reinterpret_cast<U*>(S + rr * WC) + u;
-        // RSP_K3_BUFLD: the two maps as buffer resources, a unit outside the tile gets an
+        // complex single: the two maps as buffer resources, a unit outside the tile gets an
         // out-of-range offset (bit 31) and reads 0 -- no branch around a load, so the 2 K3_VEC
         // loads of a sweep are in flight together
         const unsigned mbytes = (unsigned)((size_t)P * Gp * sizeof(T));
@@ -2127,7 +2123,7 @@ __global__ __launch_bounds__(RSP_THREADS, RSP_K3_WGS) void k3_cfar(Geometry g, D
             U xa[K3_VEC], xb[K3_VEC];
 #pragma unroll
             for (int q = 0; q < K3_VEC; ++q) {
-                if constexpr (RSP_K3_BUFLD && sizeof(T) == 4) {   // complex double: 35.0 vs 36.0 us, kept off
+                if constexpr (sizeof(T) == 4) {   // complex double: plain loads (35.0 vs 36.0 us)
                     const unsigned bad = (unsigned)(nv - 1 - (vb + rr + q * NTR)) & 0x80000000u;
                     const unsigned off = (base + (unsigned)(vb + q * NTR) * rowb) | bad;
                     xa[q] = __builtin_bit_cast(U, __builtin_amdgcn_raw_buffer_load_b128(ra, (int)off, 0, 0));
@@ -2249,7 +2245,6 @@ __global__ __launch_bounds__(RSP_THREADS, RSP_K3_WGS) void k3_cfar(Geometry g, D
         const int r = c0 + c;
         const int rgp = lgT == 4 ? (rg & ~3) | ((rg & 1) << 1) | ((rg >> 1) & 1)
                                  : (rg & 1) + ((rg & 2) << 2) + 2 * ((rg >> 2) & 3) + 16 * (rg >> 4);
-#if RSP_K3_PREFILTER
         // Exact prefilter.  A hit needs CUT > T mean(max of the four slices) >= T mean(left range
         // slice): quot() is the correctly rounded (double) or a monotone (float) quotient and the
         // product with T > 0 rounds monotonically, so a cell with CUT <= T quot(lr) cannot be a
@@ -2317,7 +2312,6 @@ __global__ __launch_bounds__(RSP_THREADS, RSP_K3_WGS) void k3_cfar(Geometry g, D
                 }
             }
         } else
-#endif
 #pragma unroll 1
         for (int v = v0 + rgp; v < v1; v += RSP_THREADS >> lgT) {
             const T* row = Sv + v * WC + c;
@@ -2597,14 +2591,14 @@ static int k1p_tpw(const Geometry& g) {
     return need <= k1_tpw(g) ? k1_tpw(g) : (need <= 2 * k1_tpw(g) ? 2 * k1_tpw(g) : 0);
 }
 
-// sub-tiles per wave of the factored-DFT K1 (one load round per tile): TPW or 2 TPW, else 0
+// sub-tiles per wave of the factored-DFT K1 (one load round per tile): ceil(sub-tiles / 8) <= 4
 static int k1q_tpw(const Geometry& g) {
     const int pt = g.prec == RSP_PREC_F64 ? 16 : 32;
     const int need = (g.NT * ((g.P + pt - 1) / pt) + (K1_THREADS / 64) - 1) / (K1_THREADS / 64);
-    return need <= k1_tpw(g) ? k1_tpw(g) : (need <= 2 * k1_tpw(g) ? 2 * k1_tpw(g) : 0);
+    return need <= 4 ? need : 0;
 }
-static size_t k1q_lds(const Geometry& g) {
-    return ((size_t)g.B * g.NT * g.Ppad + g.twq_elems + g.P) * cplx_bytes(g);
+static size_t k1q_lds(const Geometry& g) {   // tile | twQ | W_P^i | Atab (MB x NJ x 2 x 64 <= 1024 reals: CP <= 16)
+    return ((size_t)g.B * g.NT * g.Ppad + g.twq_elems + g.P) * cplx_bytes(g) + (size_t)1024 * (cplx_bytes(g) / 2);
 }
 static bool k1q_fits(const Geometry& g) {
     return !g.pow2P && g.rqQ > 0 && k1q_tpw(g) > 0 && k1q_lds(g) <= 160 * 1024 && g.ncu > 0 && !g.k1_tiled;
@@ -2643,18 +2637,23 @@ static hipError_t launch_k1_t(const Geometry& g, const DevConsts& k, const Frame
     // the persistent factored-DFT K1 for C <= 16 when one load round of at most 16 16-B cube loads
     // per lane covers a tile (register budget: no scratch); otherwise the tiled kernel
     if constexpr (CP <= 16) {
-        constexpr int NJ = CP / 4, MB = BMAX <= 8 ? 1 : 2, TPW = (16 / NJ) / MB > 0 ? (16 / NJ) / MB : 1;
+        constexpr int NJ = CP / 4;
         if (mode == 3 && k1q_fits(g) && k1q_tpw(g) * NJ <= 16) {
             const size_t ldsq = k1q_lds(g);
             const int grid = std::min(g.ncu, nf * g.ntiles);
             hipError_t e;
-            if (k1q_tpw(g) == TPW) {
-                if ((e = allow_lds(k1q_dbf_mtd<T, BMAX, CP, TPW>, ldsq)) != hipSuccess) return e;
-                hipLaunchKernelGGL((k1q_dbf_mtd<T, BMAX, CP, TPW>), dim3(grid), dim3(K1_THREADS), ldsq, s, g, k, fp, nf);
-            } else if constexpr (2 * TPW * NJ <= 16) {
-                if ((e = allow_lds(k1q_dbf_mtd<T, BMAX, CP, 2 * TPW>, ldsq)) != hipSuccess) return e;
-                hipLaunchKernelGGL((k1q_dbf_mtd<T, BMAX, CP, 2 * TPW>), dim3(grid), dim3(K1_THREADS), ldsq, s, g, k, fp, nf);
+#define K1Q_LAUNCH(TW)                                                                                            \
+    do {                                                                                                          \
+        if ((e = allow_lds(k1q_dbf_mtd<T, BMAX, CP, TW>, ldsq)) != hipSuccess) return e;                           \
+        hipLaunchKernelGGL((k1q_dbf_mtd<T, BMAX, CP, TW>), dim3(grid), dim3(K1_THREADS), ldsq, s, g, k, fp, nf); \
+    } while (0)
+            switch (k1q_tpw(g)) {
+                case 1: K1Q_LAUNCH(1); break;
+                case 2: K1Q_LAUNCH(2); break;
+                case 3: K1Q_LAUNCH(3); break;
+                default: if constexpr (NJ <= 4) K1Q_LAUNCH(4); break;
             }
+#undef K1Q_LAUNCH
             return hipGetLastError();
         }
     }
@@ -2710,24 +2709,16 @@ static hipError_t launch_k2_p(const Geometry& g, const DevConsts& k, const Frame
 
 // Streaming copy (rsp_hbm_copy_probe): CU16 x 16 B per lane, all loads in flight before the
 // stores, one chunk per workgroup.
-#ifndef RSP_COPY_U
-#define RSP_COPY_U 4
-#endif
-#ifndef RSP_COPY_NT
-#define RSP_COPY_NT 1   // non-temporal both ways: 6.2-6.5 TB/s at 0.25-1 GiB vs 5.7-5.9 plain (A/B)
-#endif
+#define RSP_COPY_U 4    // 16-B loads per lane in flight; non-temporal both ways (6.2-6.5 TB/s at 0.25-1 GiB, 5.7-5.9 plain)
 __global__ __launch_bounds__(256) void k_stream_copy(const u32x4* __restrict__ in, u32x4* __restrict__ out, size_t n16) {
     const size_t base = (size_t)blockIdx.x * (256 * RSP_COPY_U) + threadIdx.x;
     u32x4 v[RSP_COPY_U];
 #pragma unroll
     for (int u = 0; u < RSP_COPY_U; ++u)
-        if (base + u * 256 < n16) v[u] = RSP_COPY_NT ? __builtin_nontemporal_load(in + base + u * 256) : in[base + u * 256];
+        if (base + u * 256 < n16) v[u] = __builtin_nontemporal_load(in + base + u * 256);
 #pragma unroll
     for (int u = 0; u < RSP_COPY_U; ++u)
-        if (base + u * 256 < n16) {
-            if (RSP_COPY_NT) __builtin_nontemporal_store(v[u], out + base + u * 256);
-            else out[base + u * 256] = v[u];
-        }
+        if (base + u * 256 < n16) __builtin_nontemporal_store(v[u], out + base + u * 256);
 }
 
 hipError_t launch_stream_copy(const void* in, void* out, size_t n16, int, hipStream_t s) {

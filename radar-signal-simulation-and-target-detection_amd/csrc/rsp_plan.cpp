@@ -397,7 +397,7 @@ struct Interval { int lo, hi; };
 
 int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga, int gb, int seg_lo,
                       std::vector<cd>& H, std::vector<cd>& twM, std::vector<int>& tw_sizes, std::vector<int>& tw_offs,
-                      const char* name, double mix_w) {
+                      const char* name) {
     std::vector<cd> h(Nfft);
     for (int i = 0; i < Nfft; ++i) h[i] = cd(mf_fft[2 * i], mf_fft[2 * i + 1]);
     fft_d(h, +1);
@@ -417,17 +417,17 @@ int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga,
     s.lo = std::max(seg_lo, seg_lo + ga - (Lh - 1));
     s.hi = std::min(seg_lo + Ls - 1, seg_lo + gb - 1);
     // overlap-save block size M = 2^k <= 2048 (so that a workgroup owns >= 2 adjacent rows:
-    // 128 B contiguous loads of z) or the mixed-radix 2560 = 16 x 10 x 16 (one row per workgroup,
-    // RSP_K2_MIX); cost model blocks * M * (log2 M + 2)
+    // 128 B contiguous loads of z) or the mixed-radix 2560 = 16 x 10 x 16 (one row per
+    // workgroup); cost model blocks * M * (log2 M + 2)
     const int nout = gb - ga;
     double best = 1e300;
     int bestM = 0;
-    const int cand[] = {64, 128, 256, 512, 1024, 2048, RSP_K2_MIX ? 2560 : 0};
+    const int cand[] = {64, 128, 256, 512, 1024, 2048, 2560};
     for (int M : cand) {
         const int V = M - Lh + 1;
-        if (M == 0 || V < 1) continue;
+        if (V < 1) continue;
         const int nb = (nout + V - 1) / V;
-        const double cost = (double)nb * M * (std::log2((double)M) + 2) * (is_pow2(M) ? 1.0 : mix_w);
+        const double cost = (double)nb * M * (std::log2((double)M) + 2);
         if (cost < best * 0.999) { best = cost; bestM = M; }
     }
     if (!bestM) return fail(RSP_ERR_UNSUPPORTED, "%s filter length %d exceeds the 2048-point block", name, Lh);
@@ -447,10 +447,10 @@ int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga,
         tw_sizes.push_back(M);
         tw_offs.push_back((int)twM.size());
         if (mix) {
-            build_mix_twiddles(16, M / 256, twM, RSP_K2_CMP);
+            build_mix_twiddles(16, M / 256, twM, true);
         } else {
-            build_pass_twiddles(s.logM, twM, false, RSP_K2_CMP, RSP_K2_PAL);   // forward FFT (compact rows, palindromic plan)
-            build_pass_twiddles(s.logM, twM, true, RSP_K2_CMP, RSP_K2_PAL);    // inverse FFT (reversed radices)
+            build_pass_twiddles(s.logM, twM, false, true, true);   // forward FFT (compact rows, palindromic plan)
+            build_pass_twiddles(s.logM, twM, true, true, true);    // inverse FFT (reversed radices)
         }
         ti = (int)tw_sizes.size() - 1;
     }
@@ -527,12 +527,8 @@ FramePtrs lane_ptrs(const rsp_plan* p, const Lane& L, const void* const* in, int
 
 // Enqueue K1 -> K2 -> K3 for nf frames on lane L, plus the async detection read-back.
 // smap (optional, one frame): K3 also writes rdm_for_cfar_all there.
-#ifndef RSP_K3_TILE_KB
 #define RSP_K3_TILE_KB 48   // KB of S per K3 tile (48: 2 Doppler bands at P = 128, 3 workgroups per CU)
-#endif
-#ifndef RSP_K3_RT_C128
-#define RSP_K3_RT_C128 32   // K3 tile width in range cells, complex double (32 or 64)
-#endif
+#define RSP_K3_RT_C128 32   // K3 tile width in range cells, complex double
 // A lane's buffers are reused only after harvest has waited for the lane's previous batch.
 int launch_batch(rsp_plan* p, Lane& L, const void* const* in, const int* ids, int nf, void* smap = nullptr,
                  const int* slots = nullptr, void* const* rdm = nullptr) {
@@ -920,22 +916,17 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
         for (int j = 0; j < s.ntaps; ++j) taps.push_back(pre->MF_narrow[j]);
         p->segs.push_back(s);
     }
-    // the cost model's weight on the mixed-radix 2560-point block (complex double, where such a
-    // plan runs k2_pc at 3 workgroups per CU)
-#ifndef RSP_K2_MIXW
-#define RSP_K2_MIXW 1.0
-#endif
     if (g2 > 0) {
         SegDesc s{};
         int rc = build_fft_segment(s, pre->MF_medium_fft, pre->N_fft_med, N, g1, g1 + g2, pre->seg_start_medium - 1, H,
-                                   twM, tw_sizes, tw_offs, "medium", f64 ? RSP_K2_MIXW : 1.0);
+                                   twM, tw_sizes, tw_offs, "medium");
         if (rc) return bail(rc);
         p->segs.push_back(s);
     }
     if (g3 > 0) {
         SegDesc s{};
         int rc = build_fft_segment(s, pre->MF_long_fft, pre->N_fft_long, N, g1 + g2, G, pre->seg_start_long - 1, H, twM,
-                                   tw_sizes, tw_offs, "long", f64 ? RSP_K2_MIXW : 1.0);
+                                   tw_sizes, tw_offs, "long");
         if (rc) return bail(rc);
         p->segs.push_back(s);
     }
@@ -944,15 +935,7 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
     // then holding 2048 / M rows; otherwise RSP_K2_POINTS (4096: 2 per CU in complex double)
     g.k2_pts = RSP_K2_POINTS;
     for (auto& s : p->segs)
-        if (f64 && s.type == 1 && (s.M == 2560 || RSP_K2_MODE3_ALL)) g.k2_pts = RSP_K2_MIXPTS;
-    // such a plan's k2_pc runs a 1024-point block as 8 x 16 x 8 (two rows per workgroup, every
-    // thread in the radix-8 passes): its own twiddle tables (k2_fft_job_mix)
-    if (g.k2_pts == RSP_K2_MIXPTS && RSP_K2_M1024MIX)
-        for (auto& s : p->segs)
-            if (s.type == 1 && s.M == 1024) {
-                s.tw_off = (int)twM.size();
-                build_mix_twiddles(8, 16, twM, RSP_K2_CMP);
-            }
+        if (f64 && s.type == 1 && s.M == 2560) g.k2_pts = RSP_K2_MIXPTS;
     // the narrow (direct-FIR) segment stages whole rows in the workgroup's LDS: when its window
     // does not fit a 2560-point workgroup the plan falls back to RSP_K2_POINTS workgroups (2 per
     // CU; k2_pc runs the 2560-point block in either sizing)
@@ -1022,8 +1005,8 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
     if ((size_t)B * g.NT * g.Ppad * esz + tab_bytes > 160 * 1024 || (g.pow2P && B * g.NT * P > 8192))
         return bail(fail(RSP_ERR_UNSUPPORTED, "B*P too large for the slow-time FFT tile"));
     g.ntiles = (g.nU + g.NT - 1) / g.NT;
-    // z chunks: NT samples (one K1 tile) per row slab, or RSP_Z_LINE bytes (A/B builds)
-    g.NZ = std::max(g.NT, RSP_Z_LINE / (int)esz);
+    // z chunks: NT samples (one K1 tile) per row slab
+    g.NZ = g.NT;
     g.nzc = (g.nU + g.NZ - 1) / g.NZ;
     if ((int)U.size() > RSP_MAX_IVL) return bail(fail(RSP_ERR_UNSUPPORTED, "too many sample intervals"));
     g.nivl = (int)U.size();
@@ -1062,10 +1045,10 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
     // splits the rows into bands, each with the rV + gV window rows on either side
     g.cfar_RT = p->rsz == 4 ? 64 : RSP_K3_RT_C128;
     // LDS row stride, 16-B aligned; complex double + 2 cells (bank spread, k3_cfar)
-    // k3_cfar's compile-time path (the reference's 5/5/10/10) with RSP_K3_NOHALO holds only the
+    // k3_cfar's compile-time path (the reference's 5/5/10/10) holds only the
     // band's own cells (its prefilter reads whichever range slice lies in the tile; the rare
     // survivors and S9 read the windows from the magnitude maps)
-    const bool k3_nohalo = RSP_K3_NOHALO && k3_fast_params(g);
+    const bool k3_nohalo = k3_fast_params(g);
     const int hx = k3_nohalo ? 0 : 2;
     g.cfar_W = ((g.cfar_RT + hx * g.cfar_hR + 3) & ~3) + (p->rsz == 8 ? 2 : 0);
     {

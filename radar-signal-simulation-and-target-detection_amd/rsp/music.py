@@ -143,6 +143,14 @@ class MusicPlan:
                            n_peaks.ctypes.data_as(ct.POINTER(ct.c_int32)), None)
         _abi.check(self._lib.rsp_music_process_device(self._h, ct.c_void_p(d_X), n_inst, ct.byref(st)))
 
+    def eig_device(self, d_X, n_inst, eig, peaks, n_peaks):
+        """Device run returning all N eigenvalues (descending, MUSIC_1D.m:29-33) and the peak indices
+        into caller arrays: the form of the 3-output rsp_mex('music') / music_1d_calllib.m call,
+        which always runs the full eigensolver (bench.py --want-eig)."""
+        st = _abi.MusicOut(None, eig.ctypes.data_as(_abi._dp), peaks.ctypes.data_as(ct.POINTER(ct.c_int32)),
+                           n_peaks.ctypes.data_as(ct.POINTER(ct.c_int32)), None)
+        _abi.check(self._lib.rsp_music_process_device(self._h, ct.c_void_p(d_X), n_inst, ct.byref(st)))
+
     def fast_count(self):
         """Instances of the last call answered by the block-power fast path (rsp_music_fast_count)."""
         n = ct.c_int32()

@@ -1,4 +1,4 @@
-"""K3's exact CFAR prefilter (rsp_kernels.hip, RSP_K3_PREFILTER) under low thresholds.
+"""K3's exact CFAR prefilter (rsp_kernels.hip, k3_cfar) under low thresholds.
 
 K3 rejects a cell when CUT <= T mean(left range slice) and runs the full GOCA test
 (fsf:192-213) only on the survivors.  At the reference's T_CFAR = 8 almost no noise cell
