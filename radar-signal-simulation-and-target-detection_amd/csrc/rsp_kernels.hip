@@ -932,7 +932,7 @@ __device__ __forceinline__ void k1_dft_rq_r(int R, V* buf, int rs, int ncols, in
 // any other the direct DFT (O(P^2) per column).
 // RQ: the instantiation that runs the factored DFT (its registers stay out of the others).
 template <class T, int BMAX, int CP, bool RQ>
-__global__ __launch_bounds__(K1_THREADS, 4) void k1_dbf_mtd(Geometry g, DevConsts k, FramePtrs fp, int mode) {
+__global__ __launch_bounds__(K1_THREADS, 2) void k1_dbf_mtd(Geometry g, DevConsts k, FramePtrs fp, int mode) {
     typedef cx<T> V;
     typedef Dbf<T> D;
     V* Y = reinterpret_cast<V*>(rsp_lds);   // [B][NT][Ppad] | twiddles
@@ -1129,15 +1129,25 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
     const int lane = threadIdx.x & 63, grp = lane >> 4, col = lane & 15;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: nlv[] and n are scalar
     const T* At = static_cast<const T*>(k.Atab);
-    // the conj(W) operands of the MFMA row blocks held in registers for the kernel's life
+    // the conj(W) operands of the MFMA row blocks: held in registers for the kernel's life with
+    // one row block (<= 8 beams); with two (16 beams: x4's 32 channels are 64 VGPRs of them) read
+    // from LDS (after the twiddles, k1p_lds) in each sub-tile's DBF, which keeps the kernel
+    // within 256 VGPRs without scratch
+    constexpr bool ALDS = MB == 2;
+    T* Al = reinterpret_cast<T*>(twl + P);
     T are[MB][NJ], aim[MB][NJ];
+    if constexpr (ALDS) {
+        for (int i = threadIdx.x; i < MB * NJ * 2 * 64; i += K1_THREADS) Al[i] = At[i];
+    } else {
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb)
+        for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            are[mb][j] = At[((mb * NJ + j) * 2 + 0) * 64 + lane];
-            aim[mb][j] = At[((mb * NJ + j) * 2 + 1) * 64 + lane];
-        }
+            for (int j = 0; j < NJ; ++j) {
+                are[mb][j] = At[((mb * NJ + j) * 2 + 0) * 64 + lane];
+                aim[mb][j] = At[((mb * NJ + j) * 2 + 1) * 64 + lane];
+            }
+    }
+    __syncthreads();   // the first DBF reads LDS entries (Atab) other waves wrote
     // this lane's sub-tiles are the same for every tile: (sample nl, pulses p ..) and their
     // window values (k1_persistent_fits guarantees one round: NT * ptiles <= waves * TPWX)
     const int ptiles = P / PT, ntp = NT * ptiles;
@@ -1198,7 +1208,13 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
 #pragma unroll
                 for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
-                    for (int j = 0; j < NJ; ++j) D::mma(acc[mb], are[mb][j], aim[mb][j], xv[u][j]);
+                    for (int j = 0; j < NJ; ++j) {
+                        if constexpr (ALDS)
+                            D::mma(acc[mb], Al[((mb * NJ + j) * 2 + 0) * 64 + lane], Al[((mb * NJ + j) * 2 + 1) * 64 + lane],
+                                   xv[u][j]);
+                        else
+                            D::mma(acc[mb], are[mb][j], aim[mb][j], xv[u][j]);
+                    }
             }
             if (Tnext >= 0) issue_u(Tnext, u);
             dbf_store<T, MB>(Yf, acc, grp, B, NT, Ppad, nlv[u], pv[u], wv_[u], K1_SH, P);
@@ -2582,7 +2598,12 @@ static int k1_tpw(const Geometry& g) {
     const int nj = cp / 4, mb = bmax <= 8 ? 1 : 2;
     return (16 / nj) / mb > 0 ? (16 / nj) / mb : 1;
 }
-static size_t k1p_lds(const Geometry& g) { return ((size_t)2 * g.B * g.NT * g.Ppad + g.P) * cplx_bytes(g); }
+// tile buffers x 2 | FFT twiddles (<= P) | two MFMA row blocks' Atab when B > 8 (k1p_dbf_mtd ALDS)
+static size_t k1p_lds(const Geometry& g) {
+    const int cp = g.C <= 8 ? 8 : (g.C <= 16 ? 16 : 32);
+    return ((size_t)2 * g.B * g.NT * g.Ppad + g.P) * cplx_bytes(g) +
+           (g.B > 8 ? (size_t)2 * (cp / 4) * 2 * 64 * (cplx_bytes(g) / 2) : 0);
+}
 
 // sub-tiles per wave of the persistent K1 (one load round per tile): TPW, or 2 TPW
 static int k1p_tpw(const Geometry& g) {
@@ -2626,11 +2647,17 @@ static hipError_t launch_k1_t(const Geometry& g, const DevConsts& k, const Frame
         hipLaunchKernelGGL((k1p_dbf_mtd<T, BMAX, CP, LGP, TW>), dim3(grid), dim3(K1_THREADS), ldsp, s, g, k, fp, nf); \
         return hipGetLastError();                                                                                \
     } while (0)
-        switch (g.logP) {
-            case 6: if (twice) K1P_LAUNCH(6, 2 * TPW); else K1P_LAUNCH(6, TPW);
-            case 7: if (twice) K1P_LAUNCH(7, 2 * TPW); else K1P_LAUNCH(7, TPW);
-            case 8: if (twice) K1P_LAUNCH(8, 2 * TPW); else K1P_LAUNCH(8, TPW);
-            default: break;
+        // 2 TPW sub-tiles per wave only where their loads stay within 16 16-B registers per lane
+        // and 4 sub-tiles (x4: 2 x 8 channels); otherwise (no instantiation: it would spill) the
+        // tiled kernel below
+        constexpr bool TWICE_OK = 2 * TPW * NJ <= 16 && 2 * TPW <= 4;
+        if (!twice || TWICE_OK) {
+            switch (g.logP) {
+                case 6: if constexpr (TWICE_OK) { if (twice) K1P_LAUNCH(6, 2 * TPW); } K1P_LAUNCH(6, TPW);
+                case 7: if constexpr (TWICE_OK) { if (twice) K1P_LAUNCH(7, 2 * TPW); } K1P_LAUNCH(7, TPW);
+                case 8: if constexpr (TWICE_OK) { if (twice) K1P_LAUNCH(8, 2 * TPW); } K1P_LAUNCH(8, TPW);
+                default: break;
+            }
         }
 #undef K1P_LAUNCH
     }

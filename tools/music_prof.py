@@ -20,13 +20,14 @@ from rsp.music import MusicPlan, music_1d_scene  # noqa: E402
 n_inst = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 prec = sys.argv[3] if len(sys.argv) > 3 else 'c128'
+what = sys.argv[4] if len(sys.argv) > 4 else 'peaks'   # form of call timed: peaks | spectrum | eigenvalues
 N, K, M = 64, 1024, 3
 scene, scan, dl = music_1d_scene()
 plan = MusicPlan(N, K, M, scan, dl, max_batch=n_inst, precision=prec)
 d_X = plan.device_alloc(n_inst)
 plan.synthesize_device(d_X, scene, n_inst, inst0=0, seed=20250101)
 plan.process_device(d_X, n_inst, fetch=False)
-pr = plan.profile(d_X, n_inst, iters=iters)
+pr = plan.profile(d_X, n_inst, iters=iters, what=what)
 flops = 8.0 * N * (N + 1) / 2 * K * n_inst
 bytes_ = (16.0 if prec == 'c128' else 8.0) * N * K * n_inst
 pr.update(n_inst=n_inst, precision=prec, cov_tflops=flops / (pr['cov_ms'] * 1e-3) / 1e12,
