@@ -1341,8 +1341,10 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1q_dbf_mtd(Geometry g, DevCons
     };
     const int lgNT = ilog2(NT), half = P >> 1;
     issue(TT);
-    for (; TT < total; TT += gridDim.x) {
+    int it = 0;   // diagnostic builds: the phase stamps' iteration index
+    for (; TT < total; TT += gridDim.x, ++it) {
         const int Tn = TT + gridDim.x;
+        K1_STAMP(it, 0);
         {   // MFMA DBF + window of xv into Y
             T* Yf = reinterpret_cast<T*>(Y);
 #pragma unroll
@@ -1365,12 +1367,15 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1q_dbf_mtd(Geometry g, DevCons
             }
         }
         if (Tn < total) issue(Tn);   // the next tile's loads fly during this tile's DFT
+        K1_STAMP(it, 1);
         const int f = __builtin_amdgcn_readfirstlane(TT / g.ntiles), tile = TT - f * g.ntiles;
         if (tile == 0 && threadIdx.x == 0 && fp.count[f]) *fp.count[f] = 0;   // K3's detection counter
         __syncthreads();   // the tile (and, the first time, the tables) in LDS
+        K1_STAMP(it, 2);
         V* __restrict__ z = static_cast<V*>(fp.z[f]);
         const StoreZq<V> sz{buf_rsrc(z, (unsigned)(B * g.nzc * P * g.NZ * sizeof(V))), lgNT, g.nzc, tile, P, half, ilog2(g.NZ)};
         k1_dft_rq_r(g.rqR, Y, Ppad, B * NT, g.rqQ, twq, twp, sz);
+        K1_STAMP(it, 3);
         __syncthreads();   // pass 2's reads of Y before the next DBF writes it
     }
 }

@@ -54,8 +54,12 @@ def main():
         r = raw[w][used[w]]
         if len(r) > 1:
             nxt.extend(((r[1:, 0] - r[:-1, 0]) / 100.0).tolist())
-    print('per tile (wave 0, us): FFT + z stores %.2f | DBF of the next tile (load wait, MFMA, LDS) + next issue %.2f | '
-          'barrier %.2f | top to top %.2f' % (ph[:, 0].mean(), ph[:, 1].mean(), ph[:, 2].mean(), np.mean(nxt)))
+    if plan.sizes.P & (plan.sizes.P - 1):   # k1q_dbf_mtd (factored DFT): stamps at DBF | barrier | DFT
+        print('per tile (wave 0, us): DBF (load wait, MFMA, LDS) + next issue %.2f | barrier %.2f | pass 1 + pass 2 '
+              '(+ z stores) %.2f | top to top %.2f' % (ph[:, 0].mean(), ph[:, 1].mean(), ph[:, 2].mean(), np.mean(nxt)))
+    else:
+        print('per tile (wave 0, us): FFT + z stores %.2f | DBF of the next tile (load wait, MFMA, LDS) + next issue %.2f | '
+              'barrier %.2f | top to top %.2f' % (ph[:, 0].mean(), ph[:, 1].mean(), ph[:, 2].mean(), np.mean(nxt)))
     for q in (10, 50, 90):
         print('  p%d: %.2f %.2f %.2f' % (q, np.percentile(ph[:, 0], q), np.percentile(ph[:, 1], q), np.percentile(ph[:, 2], q)))
     t0 = raw[used][:, 0].min()
