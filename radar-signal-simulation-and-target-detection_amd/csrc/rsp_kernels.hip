@@ -1625,10 +1625,14 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
         }
     }
     constexpr int NTWF = tw_total(LGM, false, CMP, PAL);
+    // twiddles staged in LDS next to the rows; a 4096-point block's (1 088 entries) do not fit the
+    // 2-per-CU workgroup's LDS and are read from L1/L2 instead
+    constexpr bool TW_LDS = LGM <= 11;
     V* twL = L + k2_lds_data(g.k2_pts, SH);
-    for (int e = tid; e < k2_tw_lds(LGM); e += K2_THREADS) twL[e] = twl[e];   // visible after the pass-0 barrier
-    const V* twF = twL;
-    const V* twI = k2_tw_sym(LGM) ? twL : twL + NTWF;
+    if constexpr (TW_LDS)
+        for (int e = tid; e < k2_tw_lds(LGM); e += K2_THREADS) twL[e] = twl[e];   // visible after the pass-0 barrier
+    const V* twF = TW_LDS ? twL : twl;
+    const V* twI = k2_tw_sym(LGM) ? twF : twF + NTWF;
     // forward pass 0 (Ns = 1, no twiddles) straight from the loaded samples
     // the Ns = 1 passes' outputs XOR-swizzled (sh_store) when a middle pass reads them (3 passes)
     constexpr int XZ = (NP == 3 && R0 == 16 && RL == 16 && 1) ? 1 : 0;
@@ -1848,7 +1852,8 @@ __global__ __launch_bounds__(K2_THREADS, WGS) void k2_pc(Geometry g, DevConsts k
                 case 8: k2_fft_job<T, 8, RSP_K2_POINTS, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
                 case 9: k2_fft_job<T, 9, RSP_K2_POINTS, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
                 case 10: k2_fft_job<T, 10, RSP_K2_POINTS, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-                default: k2_fft_job<T, 11, RSP_K2_POINTS, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                case 11: k2_fft_job<T, 11, RSP_K2_POINTS, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                default: k2_fft_job<T, 12, RSP_K2_POINTS, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
             }
         }
     } else {

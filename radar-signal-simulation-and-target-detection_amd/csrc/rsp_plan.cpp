@@ -417,12 +417,13 @@ int build_fft_segment(SegDesc& s, const double* mf_fft, int Nfft, int N, int ga,
     s.lo = std::max(seg_lo, seg_lo + ga - (Lh - 1));
     s.hi = std::min(seg_lo + Ls - 1, seg_lo + gb - 1);
     // overlap-save block size M = 2^k <= 2048 (so that a workgroup owns >= 2 adjacent rows:
-    // 128 B contiguous loads of z) or the mixed-radix 2560 = 16 x 10 x 16 (one row per
-    // workgroup); cost model blocks * M * (log2 M + 2)
+    // 128 B contiguous loads of z), the mixed-radix 2560 = 16 x 10 x 16 (one row per workgroup)
+    // or 4096 = 16 x 16 x 16 (one row per 4096-point workgroup: x4's 5 956-gate long segment in
+    // 2 blocks instead of 5 x 2048); cost model blocks * M * (log2 M + 2)
     const int nout = gb - ga;
     double best = 1e300;
     int bestM = 0;
-    const int cand[] = {64, 128, 256, 512, 1024, 2048, 2560};
+    const int cand[] = {64, 128, 256, 512, 1024, 2048, 2560, 4096};
     for (int M : cand) {
         const int V = M - Lh + 1;
         if (V < 1) continue;
@@ -936,6 +937,8 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
     g.k2_pts = RSP_K2_POINTS;
     for (auto& s : p->segs)
         if (f64 && s.type == 1 && s.M == 2560) g.k2_pts = RSP_K2_MIXPTS;
+    for (auto& s : p->segs)   // a 4096-point block needs the 4096-point workgroups (2 per CU)
+        if (s.type == 1 && s.M == 4096) g.k2_pts = RSP_K2_POINTS;
     // the narrow (direct-FIR) segment stages whole rows in the workgroup's LDS: when its window
     // does not fit a 2560-point workgroup the plan falls back to RSP_K2_POINTS workgroups (2 per
     // CU; k2_pc runs the 2560-point block in either sizing)

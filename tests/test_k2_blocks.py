@@ -65,7 +65,7 @@ def _block(mf, ga, gb):
     a = np.abs(h)
     Lh = int(np.nonzero(a > 1e-10 * a.max())[0].max()) + 1
     best, bm = 1e300, 0
-    for M in (64, 128, 256, 512, 1024, 2048, 2560):
+    for M in (64, 128, 256, 512, 1024, 2048, 2560, 4096):
         V = M - Lh + 1
         if V < 1:
             continue
