@@ -211,6 +211,11 @@ int32_t rsp_process_targets(rsp_plan* plan, const rsp_target_in* targets, int32_
  * PNC layout, device pointer with cube_elems entries).  Synchronous. */
 int32_t rsp_synthesize_device(rsp_plan* plan, const rsp_target_in* targets, int32_t n_targets,
                               int32_t frame_idx, uint64_t seed, double p_noise, void* d_cube);
+/* Device time of that synthesis (its two kernels: per-target phasor tables, then the cube),
+ * averaged over `iters` back-to-back launches into d_cube, by HIP events on the plan's stream.
+ * *bytes_out (may be NULL) = the cube bytes one synthesis writes, C x N x P elements. */
+int32_t rsp_profile_synthesis(rsp_plan* plan, const rsp_target_in* targets, int32_t n_targets, int32_t iters,
+                              void* d_cube, float* ms_out, int64_t* bytes_out);
 
 /* ---- device-resident queue (throughput path) ----
  * rsp_enqueue_device: process a PNC cube (the plan's precision) already resident in

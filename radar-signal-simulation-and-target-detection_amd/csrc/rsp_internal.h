@@ -167,6 +167,10 @@ struct SynthTarget {          // per-target constants of S4 (fsf:51-73), host-co
     double fd_prt;            // doppler_freq * prt   (phase per pulse / 2pi)
     double dphi;              // channel phase step (rad)
 };
+#define RSP_MAX_SYNTH_TARGETS 64
+struct SynthTargets {         // by value in the kernel arguments (2 KiB): no upload, no sync
+    SynthTarget t[RSP_MAX_SYNTH_TARGETS];
+};
 
 // Frequencies per wave-uniform set of the factored slow-time DFT's Q-point stage (k1_dft_rq)
 #define RQ_RK 6
@@ -177,7 +181,8 @@ hipError_t launch_stream_copy(const void* in, void* out, size_t n16, int ncu, hi
 hipError_t launch_k2(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int rows, hipStream_t s);
 hipError_t launch_k3(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, hipStream_t s);
 hipError_t launch_mtd_cols(const Geometry& g, const DevConsts& k, const void* pc, void* rdm, hipStream_t s);
-hipError_t launch_synth(const Geometry& g, const double* tx, const SynthTarget* tg, int nt, int frame_idx,
+// S4 + S4.1: tab holds RSP_MAX_SYNTH_TARGETS x (P + C) complex doubles (the per-target phasors)
+hipError_t launch_synth(const Geometry& g, const double* tx, const SynthTargets& tg, int nt, void* tab, int frame_idx,
                         uint64_t seed, double noise_scale, void* cube, hipStream_t s);
 // Queue read-back: count record + the detections of nf frames (device stride dcap + 1 records) into
 // mapped pinned host memory (stride hcap + 1), only the records that exist.

@@ -2524,46 +2524,90 @@ __global__ __launch_bounds__(RSP_THREADS, 2) void k_mtd_cols(Geometry g, DevCons
 // ======================================================================================
 // S4 + S4.1 on the device: echo synthesis + Philox noise (fsf:45-88)
 // ======================================================================================
+// The per-target phasors of S4, once per (target, pulse) and (target, channel) instead of once per
+// sample: tab[t][j] = e^{i 2 pi fd_prt j} for j < P (doppler_phase_shift, fsf:58), then
+// e^{i c dphi} for c < C (the channel phasor, fsf:71-72) -- the same sincos arguments, so the
+// cube is what the per-sample evaluation gave.
+__global__ __launch_bounds__(RSP_THREADS) void k_synth_tab(Geometry g, SynthTargets tg, int nt, d2* __restrict__ tab) {
+    const int per = g.P + g.C;
+    const int i = blockIdx.x * RSP_THREADS + threadIdx.x;
+    if (i >= nt * per) return;
+    const int t = i / per, j = i - t * per;
+    double s, c;
+    if (j < g.P)
+        sincos(2.0 * M_PI * tg.t[t].fd_prt * j, &s, &c);
+    else
+        sincos((double)(j - g.P) * tg.t[t].dphi, &s, &c);
+    tab[i] = d2{c, s};
+}
+
+// S4 + S4.1 on the device, laid out so that everything shared is loaded once: a wave owns one
+// fast-time strip of SYNTH_NS samples n of one channel c (both wave-uniform, so the tx_pulse
+// samples and the channel phasors are scalar loads), a lane owns the pulse pair (m, m + 1), and
+// each target's two Doppler phasors are read once per strip, not once per sample. The pair is one
+// Philox4x32-10 block (P is even, so flat indices 2q, 2q + 1 of the [C][N][P] order): the first
+// sample takes words 0-1, the second 2-3 (oracle/philox.py documents the stream). Per sample the
+// targets are summed in order (fsf:51-78), then the Box-Muller noise is added (fsf:80-88).
+#ifndef SYNTH_NS
+#define SYNTH_NS 8
+#endif
 template <class T>
-__global__ __launch_bounds__(RSP_THREADS) void k_synth(Geometry g, const double* __restrict__ tx,
-                                                     const SynthTarget* __restrict__ tg, int nt, int frame_idx,
-                                                     uint64_t seed, double nscale, cx<T>* __restrict__ cube) {
-    const size_t total = (size_t)g.P * g.N * g.C;
-    const size_t i = (size_t)blockIdx.x * RSP_THREADS + threadIdx.x;
-    if (i >= total) return;
-    const int m = (int)(i % g.P);
-    const size_t rest = i / g.P;
-    const int n = (int)(rest % g.N);
-    const int c = (int)(rest / g.N);
-    const size_t o = (size_t)c * g.cpitch + (size_t)n * g.P + m;   // pitched store offset
-    double re = 0.0, im = 0.0;
+__global__ __launch_bounds__(RSP_THREADS) void k_synth(Geometry g, const double* __restrict__ tx, SynthTargets tg,
+                                                          int nt, const d2* __restrict__ tab, int frame_idx,
+                                                          uint64_t seed, double nscale, cx<T>* __restrict__ cube) {
+    const int lane = threadIdx.x & 63;
+    const int n0 = __builtin_amdgcn_readfirstlane((int)(blockIdx.y * (RSP_THREADS / 64) + (threadIdx.x >> 6)) * SYNTH_NS);
+    if (n0 >= g.N) return;   // the whole wave
+    const int c = blockIdx.z;
+    const int m = 2 * ((int)blockIdx.x * 64 + lane);
+    const bool act = m < g.P;
+    const int per = g.P + g.C;
+    double re[SYNTH_NS][2], im[SYNTH_NS][2];
+#pragma unroll
+    for (int u = 0; u < SYNTH_NS; ++u) re[u][0] = re[u][1] = im[u][0] = im[u][1] = 0.0;
     for (int t = 0; t < nt; ++t) {
-        const int ds = tg[t].delay;
-        if (ds > 0 && ds < g.N && n >= ds) {
-            const double tr = tx[2 * (n - ds)], ti = tx[2 * (n - ds) + 1];
-            double sd, cd, sp, cp;
-            sincos(2.0 * M_PI * tg[t].fd_prt * m, &sd, &cd);       // doppler_phase_shift (fsf:58)
-            sincos((double)c * tg[t].dphi, &sp, &cp);             // channel phasor (fsf:71-72)
-            const double er = tg[t].amp * (tr * cd - ti * sd);     // amplitude * base * doppler
-            const double ei = tg[t].amp * (tr * sd + ti * cd);
-            re += er * cp - ei * sp;
-            im += er * sp + ei * cp;
+        const int ds = tg.t[t].delay;
+        if (!(ds > 0 && ds < g.N) || n0 + SYNTH_NS - 1 < ds) continue;
+        const d2 d0 = act ? tab[t * per + m] : d2{}, d1 = act ? tab[t * per + m + 1] : d2{};
+        const d2 cp = tab[t * per + g.P + c];
+        const double amp = tg.t[t].amp;
+#pragma unroll
+        for (int u = 0; u < SYNTH_NS; ++u) {
+            const int n = n0 + u;
+            if (n < g.N && n >= ds) {
+                const double tr = tx[2 * (n - ds)], ti = tx[2 * (n - ds) + 1];
+                double er = amp * (tr * d0.x - ti * d0.y);   // amplitude * base * doppler
+                double ei = amp * (tr * d0.y + ti * d0.x);
+                re[u][0] += er * cp.x - ei * cp.y;
+                im[u][0] += er * cp.y + ei * cp.x;
+                er = amp * (tr * d1.x - ti * d1.y);
+                ei = amp * (tr * d1.y + ti * d1.x);
+                re[u][1] += er * cp.x - ei * cp.y;
+                im[u][1] += er * cp.y + ei * cp.x;
+            }
         }
     }
-    // Philox noise (oracle/philox.py documents the stream)
-    const uint64_t pairi = (uint64_t)i >> 1;
-    uint32_t ctr[4] = {(uint32_t)pairi, (uint32_t)(pairi >> 32), (uint32_t)frame_idx, 0x52535020u};
-    rsp_philox10(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
-    const uint32_t xa = (i & 1) ? ctr[2] : ctr[0];
-    const uint32_t xb = (i & 1) ? ctr[3] : ctr[1];
-    const double ua = ((double)xa + 0.5) * 2.3283064365386963e-10;
-    const double ub = ((double)xb + 0.5) * 2.3283064365386963e-10;
-    const double rr = sqrt(-2.0 * log(ua));
-    double sb, cb;
-    sincos(2.0 * M_PI * ub, &sb, &cb);
-    re += rr * cb * nscale;
-    im += rr * sb * nscale;
-    cube[o] = cx<T>{(T)re, (T)im};
+    if (!act) return;
+#pragma unroll
+    for (int u = 0; u < SYNTH_NS; ++u) {
+        const int n = n0 + u;
+        if (n >= g.N) break;
+        const uint64_t q = ((uint64_t)c * g.N + n) * (uint64_t)(g.P >> 1) + (uint64_t)(m >> 1);   // flat index / 2
+        uint32_t ctr[4] = {(uint32_t)q, (uint32_t)(q >> 32), (uint32_t)frame_idx, 0x52535020u};
+        rsp_philox10(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+        cx<T>* dst = cube + (size_t)c * g.cpitch + (size_t)n * g.P + m;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t xa = h ? ctr[2] : ctr[0];
+            const uint32_t xb = h ? ctr[3] : ctr[1];
+            const double ua = ((double)xa + 0.5) * 2.3283064365386963e-10;
+            const double ub = ((double)xb + 0.5) * 2.3283064365386963e-10;
+            const double rr = sqrt(-2.0 * log(ua));
+            double sb, cb;
+            sincos(2.0 * M_PI * ub, &sb, &cb);
+            dst[h] = cx<T>{(T)(re[u][h] + rr * cb * nscale), (T)(im[u][h] + rr * sb * nscale)};
+        }
+    }
 }
 
 // ======================================================================================
@@ -2820,15 +2864,19 @@ hipError_t launch_mtd_cols(const Geometry& g, const DevConsts& k, const void* pc
     return g.prec == RSP_PREC_F64 ? launch_mtd_p<double>(g, k, pc, rdm, s) : launch_mtd_p<float>(g, k, pc, rdm, s);
 }
 
-hipError_t launch_synth(const Geometry& g, const double* tx, const SynthTarget* tg, int nt, int frame_idx,
+hipError_t launch_synth(const Geometry& g, const double* tx, const SynthTargets& tg, int nt, void* tab, int frame_idx,
                         uint64_t seed, double nscale, void* cube, hipStream_t s) {
-    const size_t total = (size_t)g.P * g.N * g.C;
-    const unsigned blocks = (unsigned)((total + RSP_THREADS - 1) / RSP_THREADS);
+    if (g.P & 1) return hipErrorInvalidValue;   // pulse pairs are Philox pairs; plans reject odd P at creation
+    if (nt > 0)
+        hipLaunchKernelGGL(k_synth_tab, dim3((nt * (g.P + g.C) + RSP_THREADS - 1) / RSP_THREADS), dim3(RSP_THREADS), 0, s,
+                           g, tg, nt, static_cast<d2*>(tab));
+    constexpr int rows = SYNTH_NS * (RSP_THREADS / 64);   // fast-time samples per workgroup
+    const dim3 grid((g.P / 2 + 63) / 64, (g.N + rows - 1) / rows, g.C);
     if (g.prec == RSP_PREC_F64)
-        hipLaunchKernelGGL(k_synth<double>, dim3(blocks), dim3(RSP_THREADS), 0, s, g, tx, tg, nt, frame_idx, seed,
-                           nscale, static_cast<d2*>(cube));
+        hipLaunchKernelGGL(k_synth<double>, grid, dim3(RSP_THREADS), 0, s, g, tx, tg, nt, static_cast<const d2*>(tab),
+                           frame_idx, seed, nscale, static_cast<d2*>(cube));
     else
-        hipLaunchKernelGGL(k_synth<float>, dim3(blocks), dim3(RSP_THREADS), 0, s, g, tx, tg, nt, frame_idx, seed,
-                           nscale, static_cast<f2*>(cube));
+        hipLaunchKernelGGL(k_synth<float>, grid, dim3(RSP_THREADS), 0, s, g, tx, tg, nt, static_cast<const d2*>(tab),
+                           frame_idx, seed, nscale, static_cast<f2*>(cube));
     return hipGetLastError();
 }

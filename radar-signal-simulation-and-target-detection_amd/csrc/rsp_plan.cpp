@@ -277,7 +277,7 @@ struct rsp_plan {
     std::vector<K2Job> jobs;
     std::vector<void*> dev_allocs;
     double* d_tx = nullptr;
-    SynthTarget* d_tg = nullptr;
+    double* d_stab = nullptr;     // S4 phasor tables: RSP_MAX_SYNTH_TARGETS x (P + C) complex
     void* d_cube = nullptr;       // staging cube for the synchronous paths
     void* d_aux = nullptr;        // second map for the stage-2 path
     void* d_smap = nullptr;       // rdm_for_cfar_all of the synchronous path (allocated on first request)
@@ -1188,7 +1188,7 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
         std::vector<double> tx(pre->tx_pulse, pre->tx_pulse + 2 * (size_t)N);
         if ((rc = p->upload(&p->d_tx, tx))) return bail(rc);
     }
-    if ((rc = p->dalloc(&p->d_tg, 64))) return bail(rc);
+    if ((rc = p->dalloc(&p->d_stab, (size_t)2 * RSP_MAX_SYNTH_TARGETS * (P + C)))) return bail(rc);
     p->z_elems = (size_t)B * g.nzc * g.NZ * P;
     p->rdm_elems = (size_t)B * P * G;
     g.Gp = (G + 3) & ~3;
@@ -1248,20 +1248,21 @@ int32_t rsp_process_cube(rsp_plan* p, const void* cube, int32_t dtype, int32_t l
 }
 
 static int synth_into(rsp_plan* p, const rsp_target_in* t, int nt, int frame_idx, uint64_t seed, double p_noise,
-                      void* d_cube, hipStream_t s) {
+                      void* d_cube, hipStream_t s, bool sync) {
     if (!p->d_tx) return fail(RSP_ERR_INVALID, "plan has no tx_pulse (synthesis path needs precomputed_data.tx_pulse)");
-    if (nt < 0 || nt > 64) return fail(RSP_ERR_INVALID, "1..64 targets supported, got %d", nt);
-    std::vector<SynthTarget> tg(nt);
+    if (nt < 0 || nt > RSP_MAX_SYNTH_TARGETS)
+        return fail(RSP_ERR_INVALID, "0..%d targets supported, got %d", RSP_MAX_SYNTH_TARGETS, nt);
+    SynthTargets tg{};
     for (int i = 0; i < nt; ++i) {   // fsf:51-72
         const double delay = 2.0 * t[i].Range / p->c;
-        tg[i].delay = (int)mround(delay / (1.0 / p->fs));
-        tg[i].fd_prt = 2.0 * t[i].Velocity / p->wavelength * p->prt;
-        tg[i].amp = std::sqrt(std::pow(10.0, t[i].SNR_dB / 10.0) * p_noise / p->p_signal_unscaled);
-        tg[i].dphi = 2.0 * M_PI * p->d * std::sin(t[i].ElevationAngle * M_PI / 180.0) / p->wavelength;
+        tg.t[i].delay = (int)mround(delay / (1.0 / p->fs));
+        tg.t[i].fd_prt = 2.0 * t[i].Velocity / p->wavelength * p->prt;
+        tg.t[i].amp = std::sqrt(std::pow(10.0, t[i].SNR_dB / 10.0) * p_noise / p->p_signal_unscaled);
+        tg.t[i].dphi = 2.0 * M_PI * p->d * std::sin(t[i].ElevationAngle * M_PI / 180.0) / p->wavelength;
     }
-    if (nt) HIPCHK(hipMemcpyAsync(p->d_tg, tg.data(), sizeof(SynthTarget) * nt, hipMemcpyHostToDevice, s));
-    HIPCHK(launch_synth(p->g, p->d_tx, p->d_tg, nt, frame_idx, seed, std::sqrt(p_noise / 2.0), d_cube, s));
-    HIPCHK(hipStreamSynchronize(s));   // targets buffer is reused by the next call
+    // the targets travel in the kernel arguments; the phasor tables are rewritten in stream order
+    HIPCHK(launch_synth(p->g, p->d_tx, tg, nt, p->d_stab, frame_idx, seed, std::sqrt(p_noise / 2.0), d_cube, s));
+    if (sync) HIPCHK(hipStreamSynchronize(s));   // the caller may read the cube from another stream
     return RSP_OK;
 }
 
@@ -1269,7 +1270,32 @@ int32_t rsp_synthesize_device(rsp_plan* p, const rsp_target_in* t, int32_t nt, i
                               double p_noise, void* d_cube) {
     if (!p || (!t && nt) || !d_cube) return fail(RSP_ERR_INVALID, "null argument");
     HIPCHK(hipSetDevice(p->device));
-    return synth_into(p, t, nt, frame_idx, seed, p_noise, d_cube, p->lanes[0].stream);
+    return synth_into(p, t, nt, frame_idx, seed, p_noise, d_cube, p->lanes[0].stream, true);
+}
+
+int32_t rsp_profile_synthesis(rsp_plan* p, const rsp_target_in* t, int32_t nt, int32_t iters, void* d_cube,
+                              float* ms_out, int64_t* bytes_out) {
+    if (!p || (!t && nt) || !d_cube || iters < 1 || !ms_out) return fail(RSP_ERR_INVALID, "bad argument");
+    HIPCHK(hipSetDevice(p->device));
+    int rc = drain_all(p);
+    if (rc) return rc;
+    hipStream_t s = p->lanes[0].stream;
+    if ((rc = synth_into(p, t, nt, 1, 20250101, 1.0, d_cube, s, false))) return rc;   // warm-up
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, s));
+    for (int i = 0; i < iters && !rc; ++i) rc = synth_into(p, t, nt, 1 + i, 20250101, 1.0, d_cube, s, false);
+    HIPCHK(hipEventRecord(e1, s));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (rc) return rc;
+    *ms_out = ms / iters;
+    if (bytes_out) *bytes_out = (int64_t)p->g.C * p->g.N * p->g.P * (int64_t)p->esz;
+    return RSP_OK;
 }
 
 int32_t rsp_process_targets(rsp_plan* p, const rsp_target_in* t, int32_t nt, int32_t frame_idx, uint64_t seed,
@@ -1278,7 +1304,8 @@ int32_t rsp_process_targets(rsp_plan* p, const rsp_target_in* t, int32_t nt, int
     HIPCHK(hipSetDevice(p->device));
     int rc = drain_all(p);
     if (rc) return rc;
-    if ((rc = synth_into(p, t, nt, frame_idx, seed, p_noise, p->d_cube, p->lanes[0].stream))) return rc;
+    // the frame runs on the same stream: no host synchronisation in between
+    if ((rc = synth_into(p, t, nt, frame_idx, seed, p_noise, p->d_cube, p->lanes[0].stream, false))) return rc;
     return run_sync_frame(p, p->d_cube, frame_idx, out);
 }
 
@@ -1379,7 +1406,8 @@ int32_t rsp_process_targets_multi(rsp_plan* const* plans, int32_t n_plans, const
             for (int j = f0; j < f1; ++j) {
                 int s;
                 if ((rc = ring_acquire(p, &s))) return rc;
-                if ((rc = synth_into(p, targets[j], n_targets[j], frame_idx[j], seed, p_noise, p->ring[s], p->up_stream)))
+                if ((rc = synth_into(p, targets[j], n_targets[j], frame_idx[j], seed, p_noise, p->ring[s], p->up_stream,
+                                  false)))   // slot_ready orders K1 after it
                     return rc;
                 if ((rc = enqueue_frame(p, p->ring[s], s, frame_idx[j]))) return rc;
             }

@@ -146,6 +146,8 @@ PROTOTYPES = {
                                          ct.c_double, ct.POINTER(FrameOut)]),
     'rsp_synthesize_device': (ct.c_int32, [_P, ct.POINTER(TargetIn), ct.c_int32, ct.c_int32, ct.c_uint64,
                                            ct.c_double, _P]),
+    'rsp_profile_synthesis': (ct.c_int32, [_P, ct.POINTER(TargetIn), ct.c_int32, ct.c_int32, _P,
+                                           ct.POINTER(ct.c_float), ct.POINTER(ct.c_int64)]),
     'rsp_enqueue_device': (ct.c_int32, [_P, _P, ct.c_int32]),
     'rsp_enqueue_device_n': (ct.c_int32, [_P, ct.POINTER(_P), ct.POINTER(ct.c_int32), ct.c_int32]),
     'rsp_enqueue_device_rdm': (ct.c_int32, [_P, _P, ct.c_int32, _P]),

@@ -232,6 +232,15 @@ class Plan:
         check(lib().rsp_synthesize_device(self.h, tin, len(targets), int(frame_idx), int(seed), float(p_noise),
                                           ct.c_void_p(ptr)))
 
+    def profile_synthesis(self, ptr, targets, iters=20):
+        """rsp_profile_synthesis: device ms of one S4 + S4.1 synthesis into ``ptr`` (HIP events
+        over ``iters`` launches) and the cube bytes it writes."""
+        tin = self._targets_in(targets)
+        ms, by = ct.c_float(), ct.c_int64()
+        check(lib().rsp_profile_synthesis(self.h, tin, len(targets), int(iters), ct.c_void_p(ptr), ct.byref(ms),
+                                          ct.byref(by)))
+        return {'stage': 'k_synth', 'ms': float(ms.value), 'bytes': int(by.value), 'frames': 1}
+
     def enqueue(self, ptr, frame_idx):
         check(lib().rsp_enqueue_device(self.h, ct.c_void_p(ptr), int(frame_idx)))
 

@@ -1,0 +1,51 @@
+"""Where a synchronous rsp_process_targets call's time goes (x2 / reference, F = 1 plan).
+usage: percall_breakdown.py CONFIG [N]"""
+import ctypes as ct
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, 'radar-signal-simulation-and-target-detection_amd'))
+from rsp import config as C, _abi  # noqa: E402
+from rsp.precompute import precompute  # noqa: E402
+from rsp.plan import Plan  # noqa: E402
+import bench  # noqa: E402
+
+name = sys.argv[1] if len(sys.argv) > 1 else 'x2'
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 100
+cfg, cfar, clus, W, ang, k = C.named_config(name)
+pre = precompute(cfg, W, ang, k, C.V8_FIR)
+plan = Plan(cfg, cfar, clus, pre, frames_per_launch=1)
+tg = bench.scene(cfg)
+tin = Plan._targets_in(tg)
+lib = _abi.lib()
+d = plan.device_alloc(plan.cube_bytes)
+o = _abi.FrameOut()
+tb = (_abi.Target * 4096)()
+o.dets, o.dets_cap, o.targets, o.targets_cap = None, 0, ct.cast(tb, ct.POINTER(_abi.Target)), 4096
+
+
+def t(fn):
+    for _ in range(5):
+        fn()
+    ts = []
+    for _ in range(n):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return 1e3 * float(np.median(ts))
+
+
+res = {
+    'synthesize_device (sync)': t(lambda: lib.rsp_synthesize_device(plan.h, tin, len(tg), 1, 20250101, 1.0, ct.c_void_p(d))),
+    'enqueue 1 frame + drain (F = 1 queue)': t(lambda: (plan.enqueue(d, 1), plan.drain(), plan.results(clear=True))),
+    'process_targets (the drop-in call)': t(lambda: lib.rsp_process_targets(plan.h, tin, len(tg), 1, 20250101, 1.0, ct.byref(o))),
+    'device_sync only': t(lambda: plan.sync()),
+}
+prof = plan.profile_stages([d], iters=20)
+res['kernels F=1 (HIP events)'] = {p['stage']: round(p['ms'], 4) for p in prof}
+print(name, res)
