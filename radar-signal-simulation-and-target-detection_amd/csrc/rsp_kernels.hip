@@ -2548,9 +2548,7 @@ __global__ __launch_bounds__(RSP_THREADS) void k_synth_tab(Geometry g, SynthTarg
 // Philox4x32-10 block (P is even, so flat indices 2q, 2q + 1 of the [C][N][P] order): the first
 // sample takes words 0-1, the second 2-3 (oracle/philox.py documents the stream). Per sample the
 // targets are summed in order (fsf:51-78), then the Box-Muller noise is added (fsf:80-88).
-#ifndef SYNTH_NS
-#define SYNTH_NS 8
-#endif
+#define SYNTH_NS 8   // 4: same time, 16: +10 % (profiles/r06q_synth_ab.txt)
 template <class T>
 __global__ __launch_bounds__(RSP_THREADS) void k_synth(Geometry g, const double* __restrict__ tx, SynthTargets tg,
                                                           int nt, const d2* __restrict__ tab, int frame_idx,
