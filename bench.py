@@ -736,9 +736,10 @@ def main():
         # quoted only while the kernel's code is the one they were collected on (pmc_traffic)
         tf = os.path.join(ROOT, 'profiles', 'pmc_traffic_%s_%s%s.json' % (a.config, a.precision,
                                                                          '_rdm' if a.want_rdm else ''))
-        # PMC files are keyed by kernel name: stage k1_dbf_mtd runs as k1p_dbf_mtd (persistent K1)
-        tr, tf_fpl, traffic_src = pmc_traffic(tf, [dom['stage']] + (['k1p_dbf_mtd'] if dom['stage'] == 'k1_dbf_mtd'
-                                                                    else []))
+        # PMC files are keyed by kernel name: stage k1_dbf_mtd runs as k1p_dbf_mtd (persistent K1,
+        # power-of-two P) or k1q_dbf_mtd (factored DFT, the reference frame's P = 332)
+        tr, tf_fpl, traffic_src = pmc_traffic(tf, [dom['stage']] + (['k1p_dbf_mtd', 'k1q_dbf_mtd']
+                                                                    if dom['stage'] == 'k1_dbf_mtd' else []))
         if tr is not None:   # scaled from the PMC passes' frames per launch to this run's
             traffic = tr * dom['frames_per_launch'] / float(tf_fpl or 4)
             dom['pmc_traffic_bytes'] = traffic

@@ -34,7 +34,7 @@ def main():
             continue
         ds = sorted(by[k])
         legs = [('queue', ds[:-iters]), ('roofline_leg', ds[-iters:])] if k.split('<')[0] in (
-            'k1_dbf_mtd', 'k1p_dbf_mtd', 'k2_pc', 'k3_cfar') and len(ds) > iters else [('all', ds)]
+            'k1_dbf_mtd', 'k1p_dbf_mtd', 'k1q_dbf_mtd', 'k2_pc', 'k3_cfar') and len(ds) > iters else [('all', ds)]
         for leg, v in legs:
             if not v:
                 continue
