@@ -568,6 +568,9 @@ def main_per_call(a):
                         'timing': '%d isolated one-frame launches per stage, HIP events on the kernel stream'
                                   % a.profile_iters, 'stages': stages,
                         'device_ms_per_frame': sum(s['ms_per_launch'] for s in stages)}}
+    if dom['stage'] == 'k_synth':
+        out['roofline']['note'] = ('k_synth is bound by its f64 VALU work (Box-Muller log/sqrt/sincos and Philox per '
+                                   'sample), not by HBM: frac is its cube store rate against the HBM peak')
     if not a.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(cfg, cfar, clus, W, ang, k, targets, nframes=a.cpu_frames, name=a.config)
     else:
