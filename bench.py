@@ -102,6 +102,10 @@ def parse(argv=None):
                     help='--config music5: every step also returns all N eigenvalues (the 3-output rsp_mex(\'music\') '
                          'and music_1d_calllib.m form, MUSIC_1D.m:29-33): the full eigensolver, never the '
                          'peaks-only fast path; a secondary line')
+    ap.add_argument('--want-spectrum', action='store_true',
+                    help='--config music5: every step also returns the pseudo-spectrum P_dB (the 2-output '
+                         'rsp_mex(\'music\') form and MUSIC_1D.m\'s plot, :37-41): the fast path only where its '
+                         'subspace bound holds P_dB to 1e-8 dB; a secondary line')
     ap.add_argument('--per-call', action='store_true',
                     help='latency mode: --steps synchronous rsp_process_targets calls, one frame each, timed one by '
                          'one like the v8 frame loop\'s tic/toc (v8:162,177,191-194); not the headline')
@@ -198,6 +202,8 @@ def validate_args(a):
         return '--want-rdm applies to the radar chain, not --config music5'
     if a.want_eig and a.config != 'music5':
         return '--want-eig applies to --config music5 only'
+    if a.want_spectrum and (a.config != 'music5' or a.want_eig):
+        return '--want-spectrum applies to --config music5 only, without --want-eig (which returns the spectrum\'s superset)'
     if a.per_call and (a.config == 'music5' or a.e2e or a.want_rdm or a.frames_total or a.gpus != 1):
         return ('--per-call times single synchronous frames of the radar chain on one GPU: it takes none of '
                 '--config music5, --e2e, --want-rdm, --frames-total, --gpus N')
@@ -400,10 +406,13 @@ def main_music(a):
     peaks = np.zeros((I, M), np.int32)
     npk = np.zeros(I, np.int32)
     eig = np.zeros((I, N), np.float64) if a.want_eig else None
+    spec = np.zeros((I, len(scan)), np.float64) if a.want_spectrum else None
 
     def step(i):
         if a.want_eig:   # all N eigenvalues back with the peaks: the full eigensolver
             plan.eig_device(ring[i % 2], I, eig, peaks, npk)
+        elif a.want_spectrum:   # P_dB back with the peaks
+            plan.spectrum_device(ring[i % 2], I, spec, peaks, npk)
         else:
             plan.peaks_device(ring[i % 2], I, peaks, npk)
 
@@ -425,7 +434,8 @@ def main_music(a):
     census = rank_census(dist, dev) if dist is not None else None
     out = None
     if rank == 0:
-        pr = plan.profile(ring[0], I, iters=a.profile_iters, what='eigenvalues' if a.want_eig else 'peaks')
+        pr = plan.profile(ring[0], I, iters=a.profile_iters,
+                          what='eigenvalues' if a.want_eig else ('spectrum' if a.want_spectrum else 'peaks'))
         n_fast = plan.fast_count()   # instances of the profiled launch on the fast path (0 with --want-eig)
         flops = 8.0 * N * (N + 1) / 2 * K * I   # Hermitian X X^H: N(N+1)/2 entries x K complex MACs
         cov_tf = flops / (pr['cov_ms'] * 1e-3) / 1e12
@@ -453,14 +463,16 @@ def main_music(a):
         mtraffic = music_traffic(a.precision, I)
         eig_tf = stages[1]['ref_eig_equiv_TFLOPs']
         out = {'metric': 'MUSIC_1D DOA instances/sec, 64ch x 1024 snapshots (BASELINE config #5)' +
-                         (', all N eigenvalues returned (full eigensolver)' if a.want_eig else ''),
+                         (', all N eigenvalues returned (full eigensolver)' if a.want_eig else
+                          (', pseudo-spectrum returned' if a.want_spectrum else '')),
                'value': I * a.steps * world / el, 'unit': 'instances/s', 'n_gpus': world, 'steps': a.steps,
                'warmup': a.warmup, 'ms_per_step': el / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
                'vs_baseline': None, 'dtype': 'fp64 (complex128)' if f64 else 'fp32 (complex64)',
                'data': 'synthetic (device Philox snapshots, MUSIC_1D.m scene: -10/-30/60 deg, 10 dB measured)',
                'config': {'workload': 'BASELINE config #5: N=64 K=1024 M=3 scan=200, %d instances per step' % I +
                                       ('; eigenvalues (N per instance) and peaks returned' if a.want_eig else
-                                       '; peak indices returned'),
+                                       ('; P_dB (200 per instance) and peaks returned' if a.want_spectrum else
+                                        '; peak indices returned')),
                           'parallelism': 'instance-sharded x%d' % world},
                'roofline': {'bound': 'mfma' if dom is stages[0] else 'valu', 'kernel': dom['stage'],
                             'achieved': dom['achieved_TFLOPs'] if dom is stages[0] else eig_tf,

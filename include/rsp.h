@@ -451,9 +451,12 @@ typedef struct rsp_music_scene {
 typedef struct rsp_music_out {
     double* spectrum_db;      /* [n_scan x I] P_MUSIC_dB (MUSIC_1D.m:41)                      */
     double* eigenvalues;      /* [N x I] descending (MUSIC_1D.m:30-31); when NULL, complex double
-                                 finds only the M signal eigenvalues the spectrum needs, and
-                                 when spectrum_db is NULL too, only the signal subspace (the
-                                 block-power fast path, rsp_music_fast_count)                  */
+                                 (M <= 4) first finds only the signal subspace (the block-power
+                                 fast path with a proven 1e-12 subspace bound,
+                                 rsp_music_fast_count); a peaks-only call keeps it whenever the
+                                 bound is proven, a call that reads spectrum_db only where the
+                                 bound also holds P_dB to 1e-8 dB; otherwise (and M > 4) the full
+                                 eigensolver finds the M signal eigenvalues the spectrum needs */
     int32_t* peak_idx;        /* [M x I] 1-based scan indices of the M largest peaks (:43-47), 0 = none */
     int32_t* n_peaks;         /* [I] number of findpeaks peaks                                 */
     double* covariance;       /* complex [N x N x I] R (MUSIC_1D.m:28), column-major           */
@@ -477,7 +480,8 @@ int32_t rsp_music_synthesize_device(rsp_music_plan* plan, const rsp_music_scene*
 int32_t rsp_music_profile(rsp_music_plan* plan, const void* d_X, int32_t n_inst, int32_t iters, float* ms_out);
 /* The same timing for the form of call `what` names: RSP_MUSIC_PEAKS (= rsp_music_profile: only
  * peak_idx / n_peaks read; the block-power fast path may stand in for the eigensolver),
- * RSP_MUSIC_SPECTRUM (spectrum_db read too: the full eigensolver, M signal eigenvalues) or
+ * RSP_MUSIC_SPECTRUM (spectrum_db read too: the fast path only where it bounds P_dB to 1e-8 dB,
+ * else the full eigensolver for the M signal eigenvalues) or
  * RSP_MUSIC_EIGENVALUES (eigenvalues read: the full eigensolver, all N eigenvalues -- the
  * 3-output rsp_mex('music') call and music_1d_calllib.m, MUSIC_1D.m:29-33). */
 #define RSP_MUSIC_PEAKS 0
@@ -486,7 +490,8 @@ int32_t rsp_music_profile(rsp_music_plan* plan, const void* d_X, int32_t n_inst,
 int32_t rsp_music_profile_ex(rsp_music_plan* plan, const void* d_X, int32_t n_inst, int32_t iters, int32_t what,
                              float* ms_out);
 /* Instances of the last call whose signal subspace came from the block-power fast path (complex
- * double, calls that read neither eigenvalues nor spectrum_db, M <= 4: the iteration converged with a proven 1e-12 subspace bound,
+ * double, calls that do not read the eigenvalues, M <= 4: the iteration converged with a proven
+ * 1e-12 subspace bound -- and, when spectrum_db is read, that bound holds P_dB to 1e-8 dB;
  * rsp_music.hip me_fast_subspace); the others ran the full tridiagonal eigensolver.  Diagnostic. */
 int32_t rsp_music_fast_count(rsp_music_plan* plan, int32_t* n_fast);
 int32_t rsp_music_device_alloc(rsp_music_plan* plan, int64_t bytes, void** d_ptr);

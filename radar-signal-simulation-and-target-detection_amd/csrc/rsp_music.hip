@@ -1036,7 +1036,8 @@ __device__ bool me_fast_subspace(const double2 (&a)[16], int n, int t, int lane,
 // FAST (peaks-only launches, neig <= 4): try me_fast_subspace first.  A separate instantiation, so
 // that the launches that read every eigenvalue run the full path without the fast path's registers.
 template <int M, bool FAST>
-__global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S, int neig, const double2* __restrict__ R,
+__global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S, int neig, double spec_tol,
+                                                          const double2* __restrict__ R,
                                                           const double2* __restrict__ S1T, int Spad,
                                                           double* __restrict__ spec_db, double* __restrict__ eig_out,
                                                           int* __restrict__ peaks_out, unsigned long long* __restrict__ trace) {
@@ -1081,6 +1082,51 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
             double2* Qb = reinterpret_cast<double2*>(lu);
             fast = me_fast_subspace<M>(a, n, t, lane, w, i, q, Qb, Qb + (M + 1) * ME_VW,
                                        reinterpret_cast<double*>(Qb + 2 * (M + 1) * ME_VW), Qs);
+        }
+    }
+    // ---- 4. den(s) = |a(s) - Q_s (Q_s^H a(s))|^2, lane = angle; returns max_s 1 / den(s)
+    auto den_pmax = [&]() -> double {
+        for (int s = t; s < S; s += ME_THREADS) {
+            double2 cf[M];
+#pragma unroll
+            for (int m = 0; m < M; ++m) cf[m] = z2;
+            for (int c = 0; c < n; ++c) {
+                const double2 av = S1T[(size_t)c * Spad + s];
+#pragma unroll
+                for (int m = 0; m < M; ++m) cf[m] = zadd(cf[m], zmc(Qs[m * 64 + c], av));
+            }
+            double r2 = 0.0;
+            for (int c = 0; c < n; ++c) {
+                double2 rr = S1T[(size_t)c * Spad + s];
+#pragma unroll
+                for (int m = 0; m < M; ++m) rr = zsub(rr, zm(Qs[m * 64 + c], cf[m]));
+                r2 += rr.x * rr.x + rr.y * rr.y;
+            }
+            den[s] = r2;
+        }
+        __syncthreads();
+        double pm = 0.0;
+        for (int s = t; s < S; s += ME_THREADS) pm = fmax(pm, 1.0 / den[s]);
+        pm = wmaxd(pm);
+        if (lane == 0) dred[w] = pm;
+        __syncthreads();
+        const double r = fmax(fmax(dred[0], dred[1]), fmax(dred[2], dred[3]));
+        __syncthreads();   // dred is reused
+        return r;
+    };
+    double pmax = 0.0;
+    bool have_den = false;
+    if constexpr (FAST) {
+        // A call that reads the spectrum (spec_tol > 0) keeps the fast subspace only if it also
+        // bounds the spectrum: sin(angle) <= 1e-12 to the signal eigenvectors moves the projector
+        // by <= 1e-12, so each den(s) by <= e0 = 1e-12 |a(s)|^2 = 1e-12 n (unit-modulus steering),
+        // and P_dB(s) = 10 log10(den_min / den(s)) by <= (20 / ln 10) e / (1 - e), e = e0 / den_min
+        // = e0 pmax.  Otherwise the full eigensolver (uniform).
+        if (fast && spec_tol > 0.0) {
+            pmax = den_pmax();
+            have_den = true;
+            const double e = 1e-12 * n * pmax;
+            if (!(e < 0.5 && 8.6858896380650366 * e / (1.0 - e) <= spec_tol)) fast = have_den = false;
         }
     }
     if (!fast) {
@@ -1429,34 +1475,9 @@ __global__ __launch_bounds__(ME_THREADS, ME_WPS) void k_music_eig64(int N, int S
     }
     }   // !fast
     ME_STAMP(4);
-    // ---- 4. den(s) = |a(s) - Q_s (Q_s^H a(s))|^2, lane = angle
-    for (int s = t; s < S; s += ME_THREADS) {
-        double2 cf[M];
-#pragma unroll
-        for (int m = 0; m < M; ++m) cf[m] = z2;
-        for (int c = 0; c < n; ++c) {
-            const double2 av = S1T[(size_t)c * Spad + s];
-#pragma unroll
-            for (int m = 0; m < M; ++m) cf[m] = zadd(cf[m], zmc(Qs[m * 64 + c], av));
-        }
-        double r2 = 0.0;
-        for (int c = 0; c < n; ++c) {
-            double2 rr = S1T[(size_t)c * Spad + s];
-#pragma unroll
-            for (int m = 0; m < M; ++m) rr = zsub(rr, zm(Qs[m * 64 + c], cf[m]));
-            r2 += rr.x * rr.x + rr.y * rr.y;
-        }
-        den[s] = r2;
-    }
-    __syncthreads();
+    if (!have_den) pmax = den_pmax();
     ME_STAMP(5);
     // ---- 5. P = 1 ./ den, P_dB = 10 log10(P / max P) (MUSIC_1D.m:37-41)
-    double pm = 0.0;
-    for (int s = t; s < S; s += ME_THREADS) pm = fmax(pm, 1.0 / den[s]);
-    pm = wmaxd(pm);
-    if (lane == 0) dred[w] = pm;
-    __syncthreads();
-    const double pmax = fmax(fmax(dred[0], dred[1]), fmax(dred[2], dred[3]));
     double* __restrict__ out = spec_db + (size_t)blockIdx.x * S;
     for (int s = t; s < S; s += ME_THREADS) {
         const double db = 10.0 * log10((1.0 / den[s]) / pmax);
@@ -1569,9 +1590,11 @@ hipError_t launch_eig64(rsp_music_plan* p, int n_inst, int want) {
     const size_t lds = me_lds_bytes(MC, p->S);
     // neig: eigenvalues the kernel finds (all N when the caller reads them, else the M signal ones)
     const int neig = want == MU_WANT_EIGS ? p->N : p->M;
-    // the fast-path instantiation only for peaks-only calls: a call that reads eigenvalues or the
-    // spectrum never takes it, whatever N and M are (an N <= 4 plan asks for neig = N <= 4 too)
-    const bool fast = want == MU_WANT_PEAKS && MC <= 4;
+    // the fast-path instantiation for peaks-only and spectrum calls: a call that reads the
+    // eigenvalues never takes it, whatever N and M are (an N <= 4 plan asks for neig = N <= 4 too)
+    const bool fast = (want == MU_WANT_PEAKS || want == MU_WANT_SPECTRUM) && MC <= 4;
+    // spectrum calls keep the fast subspace only where it bounds P_dB's error by 1e-8 dB
+    const double spec_tol = want == MU_WANT_SPECTRUM ? 1e-8 : 0.0;
     const void* kf = fast ? reinterpret_cast<const void*>(k_music_eig64<MC, true>)
                           : reinterpret_cast<const void*>(k_music_eig64<MC, false>);
     if (lds > 64 * 1024) {
@@ -1580,11 +1603,11 @@ hipError_t launch_eig64(rsp_music_plan* p, int n_inst, int want) {
     }
     if (fast)
         hipLaunchKernelGGL((k_music_eig64<MC, true>), dim3(n_inst), dim3(ME_THREADS), lds, p->stream, p->N, p->S, neig,
-                           (const double2*)p->d_R, (const double2*)p->d_S1T, p->Spad, (double*)p->d_spec,
+                           spec_tol, (const double2*)p->d_R, (const double2*)p->d_S1T, p->Spad, (double*)p->d_spec,
                            (double*)p->d_eig, p->d_peaks, p->d_trace);
     else
         hipLaunchKernelGGL((k_music_eig64<MC, false>), dim3(n_inst), dim3(ME_THREADS), lds, p->stream, p->N, p->S,
-                           neig, (const double2*)p->d_R, (const double2*)p->d_S1T, p->Spad, (double*)p->d_spec,
+                           neig, 0.0, (const double2*)p->d_R, (const double2*)p->d_S1T, p->Spad, (double*)p->d_spec,
                            (double*)p->d_eig, p->d_peaks, p->d_trace);
     return hipGetLastError();
 }

@@ -151,6 +151,14 @@ class MusicPlan:
                            n_peaks.ctypes.data_as(ct.POINTER(ct.c_int32)), None)
         _abi.check(self._lib.rsp_music_process_device(self._h, ct.c_void_p(d_X), n_inst, ct.byref(st)))
 
+    def spectrum_device(self, d_X, n_inst, spec, peaks, n_peaks):
+        """Device run returning the pseudo-spectrum P_dB ([n_inst, n_scan], MUSIC_1D.m:41) and the peak
+        indices into caller arrays, without the eigenvalues: the form of the 2-output rsp_mex('music')
+        call and of MUSIC_1D.m's plot (bench.py --want-spectrum)."""
+        st = _abi.MusicOut(spec.ctypes.data_as(_abi._dp), None, peaks.ctypes.data_as(ct.POINTER(ct.c_int32)),
+                           n_peaks.ctypes.data_as(ct.POINTER(ct.c_int32)), None)
+        _abi.check(self._lib.rsp_music_process_device(self._h, ct.c_void_p(d_X), n_inst, ct.byref(st)))
+
     def fast_count(self):
         """Instances of the last call answered by the block-power fast path (rsp_music_fast_count)."""
         n = ct.c_int32()

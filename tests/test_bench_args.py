@@ -92,6 +92,17 @@ def test_want_rdm_with_e2e_refused():
     assert r.stdout == ''
 
 
+@pytest.mark.parametrize('args,msg', [
+    (['--want-spectrum'], '--want-spectrum applies to --config music5 only'),
+    (['--config', 'music5', '--want-spectrum', '--want-eig'], '--want-spectrum applies to --config music5 only'),
+    (['--want-eig'], '--want-eig applies to --config music5 only'),
+])
+def test_music_call_forms_refused_elsewhere(args, msg):
+    r = _run(args)
+    assert r.returncode == 2 and msg in r.stderr
+    assert r.stdout == ''
+
+
 def test_visible_gpus_honours_visible_devices_env(monkeypatch):
     monkeypatch.setenv('HIP_VISIBLE_DEVICES', '')
     assert bench.visible_gpus() == 0

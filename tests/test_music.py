@@ -344,19 +344,50 @@ def test_music_small_n_full_call_returns_every_eigenvalue(N, M):
 @pytest.mark.gpu
 def test_music_spectrum_call_without_eigenvalues(music_case):
     """a call that reads spectrum_db but not the eigenvalues (rsp_mex('music')
-    with two outputs) runs the full eigensolver for the M signal eigenvalues -- never the fast path,
-    whose subspace is bounded only to 1e-12 -- so its spectrum holds the oracle tolerance."""
+    with two outputs) keeps the block-power subspace only where its proven 1e-12 subspace bound
+    also bounds P_dB's error by 1e-8 dB (<= 8.69e-12 n / den_min), else runs the full
+    eigensolver; either way its spectrum holds the oracle tolerance and its peaks are the full
+    call's.  Complex double: config #5 (den_min ~ 0.4, bound ~1.5e-9 dB) takes the fast path for
+    every instance; MUSIC_1D.m's N = 10 scene (den_min ~ 0.003, bound ~3e-8 dB) converges (the
+    peaks-only call takes the fast path) but must fall back here."""
     c = music_case
     o = c['plan'].process(c['X'][:4], want_eig=False)
     assert 'eig' not in o
-    if c['prec'] == 'c128':
+    if c['prec'] == 'c128' and c['name'] == 'config5':
+        assert c['plan'].fast_count() == 4
+    if c['prec'] == 'c128' and c['name'] == 'music_1d':
         assert c['plan'].fast_count() == 0
+        c['plan'].peaks(c['X'][:4])
+        assert c['plan'].fast_count() == 4   # so the fallback above was the spectrum bound's
     for i in range(4):
         ref = c['ref'][i]['spectrum_db']
         live = ref > -60.0
         assert np.abs(o['spectrum_db'][i][live] - ref[live]).max() <= c['tol']['db']
+        if c['prec'] == 'c128':   # against the full path (eigenvalues read) of the same instance
+            full = c['out']['spectrum_db'][i]
+            assert np.abs(o['spectrum_db'][i][live] - full[live]).max() <= 1e-8
         assert list(o['peaks'][i]) == list(c['out']['peaks'][i])
         assert o['n_peaks'][i] == c['out']['n_peaks'][i]
+
+
+@pytest.mark.gpu
+def test_music_spectrum_device_form(music_case):
+    """MusicPlan.spectrum_device (bench.py --want-spectrum's step) returns the host call's spectrum
+    and peaks for device-resident snapshots."""
+    c = music_case
+    n = 4
+    spec = np.zeros((n, len(c['scan'])), np.float64)
+    pk = np.zeros((n, c['M']), np.int32)
+    npk = np.zeros(n, np.int32)
+    d_X = c['plan'].device_alloc(n)
+    try:
+        c['plan'].synthesize_device(d_X, c['scene'], n, inst0=0, seed=SEED)
+        c['plan'].spectrum_device(d_X, n, spec, pk, npk)
+    finally:
+        c['plan'].device_free(d_X)
+    o = c['plan'].process(c['X'][:n], want_eig=False)
+    assert np.array_equal(spec, o['spectrum_db'])
+    assert np.array_equal(pk, o['peaks']) and np.array_equal(npk, o['n_peaks'])
 
 
 @pytest.mark.gpu
