@@ -20,6 +20,7 @@
 // reference's MATLAB arithmetic; the default) or float (complex64).  Complex values are
 // 2-wide ext_vector pairs (re, im) of T in registers, LDS and HBM alike.
 #include "rsp_internal.h"
+#include "rsp_noise_math.h"
 #include <math.h>
 #include <algorithm>
 
@@ -2600,9 +2601,9 @@ __global__ __launch_bounds__(RSP_THREADS) void k_synth(Geometry g, const double*
             const uint32_t xb = h ? ctr[3] : ctr[1];
             const double ua = ((double)xa + 0.5) * 2.3283064365386963e-10;
             const double ub = ((double)xb + 0.5) * 2.3283064365386963e-10;
-            const double rr = sqrt(-2.0 * log(ua));
+            const double rr = sqrt(-2.0 * rsp_nm_log(ua));
             double sb, cb;
-            sincos(2.0 * M_PI * ub, &sb, &cb);
+            rsp_nm_sincos2pi(ub, &sb, &cb);   // sincos(2 pi ub)
             dst[h] = cx<T>{(T)(re[u][h] + rr * cb * nscale), (T)(im[u][h] + rr * sb * nscale)};
         }
     }
