@@ -11,6 +11,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, 'radar-signal-simulation-and-target-detection_amd'))
 from rsp import config as C, _abi  # noqa: E402
+if os.environ.get('AB_LIB'):   # timing experiments only: an A/B variant of librsp.so
+    _abi.LIB_PATH = os.environ['AB_LIB']
 from rsp.precompute import precompute  # noqa: E402
 from rsp.plan import Plan  # noqa: E402
 import bench  # noqa: E402
