@@ -325,6 +325,7 @@ def test_music_small_n_full_call_returns_every_eigenvalue(N, M):
         o = plan.process(X)
         assert plan.fast_count() == 0
         pk, npk = plan.peaks(X)   # the peaks-only call may take the fast path; same answer
+        sp = plan.process(X, want_eig=False)   # the spectrum call: fast path only under its dB bound
     finally:
         plan.close()
     for i in range(n):
@@ -339,6 +340,8 @@ def test_music_small_n_full_call_returns_every_eigenvalue(N, M):
         assert have == [int(p) for p in ref['peaks']] == [int(p) for p in pk[i] if p > 0]
         assert list(o['peaks'][i]) == list(pk[i])
         assert o['n_peaks'][i] == ref['n_peaks'] == npk[i]
+        assert np.abs(sp['spectrum_db'][i][live] - ref['spectrum_db'][live]).max() <= 1e-7
+        assert list(sp['peaks'][i]) == list(o['peaks'][i]) and sp['n_peaks'][i] == o['n_peaks'][i]
 
 
 @pytest.mark.gpu
