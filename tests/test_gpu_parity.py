@@ -230,6 +230,34 @@ def test_synthesis_path_matches_oracle_cube(prec):
     assert np.abs(dev - ref).max() <= (1e-10 if prec == 'c128' else 1e-5) * np.abs(ref).max()
 
 
+@pytest.mark.gpu
+def test_synthesis_with_the_target_cap_matches_oracle_cube():
+    """The most targets one synthesis takes (64: they travel in the kernel arguments, 2 KiB) --
+    spread over range, velocity and angle, some outside the fast-time window -- against the oracle
+    cube; one more is refused before anything runs."""
+    s = scenario('small')
+    sc = s['cfg']['Sig_Config']
+    rng = np.random.default_rng(64)
+    rmax = sc['c'] * sc['point_PRT'] / sc['fs'] / 2 * 1.1   # a few delays past the window
+    tg = [dict(Range=float(rng.uniform(50.0, rmax)), Velocity=float(rng.uniform(-30.0, 30.0)),
+               ElevationAngle=float(rng.uniform(-40.0, 40.0)), SNR_dB=float(rng.uniform(-20.0, 20.0)))
+          for _ in range(64)]
+    import rsp
+    plan = Plan(s['cfg'], s['cfar'], s['clus'], s['pre_p'])
+    try:
+        dev = device_cube(plan, tg, frame_idx=5)
+        ptr = plan.device_alloc(plan.cube_bytes)
+        try:
+            with pytest.raises(rsp.RspError):
+                plan.synthesize_device(ptr, tg + tg[:1], frame_idx=5)
+        finally:
+            plan.device_free(ptr)
+    finally:
+        plan.close()
+    ref = noisy_cube(s, tg, frame_idx=5, dtype=np.complex128)
+    assert np.abs(dev - ref).max() <= 1e-10 * np.abs(ref).max()
+
+
 def test_process_targets_equals_cube_path():
     s = scenario('small')
     tg = targets_for('small')
