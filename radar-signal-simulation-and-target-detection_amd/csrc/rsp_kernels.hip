@@ -712,6 +712,12 @@ struct StoreZ {
 // twd = the compact pass-A table in LDS, [i][n2] = W_P^(n2 2^i) (load_tw).  Same arithmetic per
 // output as the radix-16 x radix-R1 Stockham plan, with the twiddles on the other side.
 // PTS = points per thread (nrows P <= PTS NTHR, k1_persistent_fits).
+// Which K1 slow-time FFTs run k1_fft_dif (the persistent and the tiled K1 agree, so their outputs
+// are bit-identical): P = 64, 128 always; P = 256 for plans of more than 8 channels (with 8, the
+// persistent K1's 8 sub-tiles of loads per wave and the DIF's registers spill: the Stockham passes)
+__host__ __device__ constexpr bool k1_dif(int lgp, int cp) { return lgp >= 6 && (lgp <= 7 || (lgp == 8 && cp >= 16)); }
+#define K1_DIF k1_dif(LGP, CP)
+
 template <int LGP, int PTS, int NTHR, int SH, class V, class St>
 __device__ __forceinline__ void k1_fft_dif(V* buf, int rs, int nrows, const V* twd, const St& st) {
     constexpr int P = 1 << LGP, R1 = P / 16, LGR1 = LGP - 4;
@@ -770,14 +776,17 @@ __device__ __forceinline__ void k1_fft_dif(V* buf, int rs, int nrows, const V* t
 // Slow-time FFT of every (beam, sample) column in LDS for the runtime log2(P); the last pass
 // stores through `last`.
 template <class V, class StLast>
-__device__ __forceinline__ void k1_fft(int lgp, V* Y, int Ppad, int ncols, const V* twl, const StLast& last) {
+__device__ __forceinline__ void k1_fft(int lgp, V* Y, int Ppad, int ncols, const V* twl, const StLast& last, bool dif8) {
     StoreLds<V> st{Y};
     switch (lgp) {
         case 4: fft_passes<4, 16, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
         case 5: fft_passes<5, 16, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
         case 6: k1_fft_dif<6, 16, K1_THREADS, K1_SH>(Y, Ppad, ncols, twl, last); break;   // twl = twD
         case 7: k1_fft_dif<7, 16, K1_THREADS, K1_SH>(Y, Ppad, ncols, twl, last); break;
-        case 8: fft_passes<8, 16, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
+        case 8:
+            if (dif8) k1_fft_dif<8, 16, K1_THREADS, K1_SH>(Y, Ppad, ncols, twl, last);
+            else fft_passes<8, 16, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last);
+            break;
         default: fft_passes<9, 16, K1_SH, K1_THREADS>(Y, Ppad, ncols, twl, st, last); break;
     }
 }
@@ -944,9 +953,9 @@ __global__ __launch_bounds__(K1_THREADS, 2) void k1_dbf_mtd(Geometry g, DevConst
     const bool fft = (mode & 2) && g.pow2P;
     const bool rq = RQ && (mode & 2);   // factored DFT: twl = twQ | W_P^i
     const int sh = fft ? K1_SH : 0;
-    // P = 64, 128 run the in-place k1_fft_dif (as the persistent K1: the same bits), the other
+    // P = 64 .. 256 run the in-place k1_fft_dif (as the persistent K1: the same bits), the other
     // powers of two the Stockham passes
-    const bool dif = fft && g.logP >= 6 && g.logP <= 7;
+    const bool dif = fft && k1_dif(g.logP, CP);
     const V* __restrict__ twPp = static_cast<const V*>(dif ? k.twD : k.twPp);
     const int ntw = dif ? (P >> 2) : g.twPp_elems;
     const T* __restrict__ win = static_cast<const T*>(k.win);
@@ -1068,7 +1077,7 @@ __global__ __launch_bounds__(K1_THREADS, 2) void k1_dbf_mtd(Geometry g, DevConst
         // ---- P-point FFT of every (b, nl) column (fsf:135); the last pass applies fftshift
         // and stores the [P][NT] slabs from registers
         const StoreZ<V> sz{buf_rsrc(z, (unsigned)(B * g.nzc * P * g.NZ * sizeof(V))), lgNT, g.nzc, tile, P, half, ilog2(g.NZ)};
-        k1_fft(g.logP, Y, Ppad, B * NT, twl, sz);
+        k1_fft(g.logP, Y, Ppad, B * NT, twl, sz, k1_dif(8, CP));
     } else if (RQ && rq) {
         const StoreZq<V> sz{buf_rsrc(z, (unsigned)(B * g.nzc * P * g.NZ * sizeof(V))), lgNT, g.nzc, tile, P, half, ilog2(g.NZ)};
         k1_dft_rq_r(g.rqR, Y, Ppad, B * NT, g.rqQ, twl, twl + g.twq_elems, sz);
@@ -1118,7 +1127,8 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
     const int total = nf * g.ntiles;
     int TT = blockIdx.x;
     if (TT >= total) return;
-    if constexpr (LGP <= 7) {   // k1_fft_dif's table, 4 x P/16
+    static_assert(LGP >= 6 && LGP <= 8, "the persistent K1 runs P = 64 .. 256 (k1_persistent_fits)");
+    if constexpr (K1_DIF) {   // k1_fft_dif's table, 4 x P/16
         const V* __restrict__ twD = static_cast<const V*>(k.twD);
         for (int i = threadIdx.x; i < (P >> 2); i += K1_THREADS) twl[i] = twD[i];
     } else {
@@ -1222,10 +1232,11 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
         }
     };
     const int lgNT = ilog2(NT), half = P >> 1;
-    // EARLY (P <= 128): the next tile's loads go out as soon as this wave's DBF has read xv, before
-    // the tile barrier (x2: K1 -0.6 %, bench +0.6 %); at P = 256 the xv registers live across the
-    // Stockham passes and K1 takes 36 % longer, so there they go out after the barrier
-    constexpr bool EARLY = LGP <= 7;
+    // EARLY: the next tile's loads go out as soon as this wave's DBF has read xv, before the tile
+    // barrier (x2: K1 -0.6 %, bench +0.6 %; x4, since P = 256 runs the in-place DIF FFT as well:
+    // K1 2.13 -> 2.06 ms, profiles/r06zc_k1_p256_dif_ab.txt).  Behind the Stockham passes (P = 256
+    // with 8 channels, K1_DIF) the xv registers stay live across them and it cost 36 %.
+    constexpr bool EARLY = K1_DIF;
     // EARLY2 (complex single): each sub-tile's loads of the next tile go out inside the DBF, right
     // after the sub-tile's MFMAs have read xv[u] (c64 K1 158-163 -> 151 us; in complex double
     // 226-227 -> 236-238, so double issues after the DBF)
@@ -1244,11 +1255,11 @@ __global__ __launch_bounds__(K1_THREADS, 1) void k1p_dbf_mtd(Geometry g, DevCons
         if (tile == 0 && threadIdx.x == 0 && fp.count[f]) *fp.count[f] = 0;   // K3's detection counter
         V* __restrict__ z = static_cast<V*>(fp.z[f]);
         const StoreZ<V> sz{buf_rsrc(z, (unsigned)(B * g.nzc * P * g.NZ * sizeof(V))), lgNT, g.nzc, tile, P, half, ilog2(g.NZ)};
-        // P <= 128: in place, one barrier (between its passes); P = 256 (x4): the Stockham passes
-        // (the in-place pass A's 16 twiddles spill there, +7 % K1).  No barrier after the last
-        // pass: its reads of buffer cur are ordered before the next writes of cur (the next
+        // K1_DIF: in place, one barrier between its two passes (P = 256 as 16 x 16: K1 2.23 -> 2.13
+        // ms at x4 against the Stockham passes, which 8-channel plans keep).  No barrier after the
+        // last pass: its reads of buffer cur are ordered before the next writes of cur (the next
         // tile's dbf) by the barrier below, and dbf now writes cur ^ 1
-        if constexpr (LGP <= 7)
+        if constexpr (K1_DIF)
             k1_fft_dif<LGP, k1p_pts<T>(), K1_THREADS, K1_SH>(Y + cur * bufsz, Ppad, B * NT, twl, sz);
         else
             fft_passes<LGP, k1p_pts<T>(), K1_SH, K1_THREADS, false>(Y + cur * bufsz, Ppad, B * NT, twl,

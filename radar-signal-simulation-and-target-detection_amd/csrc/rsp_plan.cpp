@@ -1093,7 +1093,7 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
     std::vector<cd> twPp, twP(P), twD;
     if (g.pow2P) build_pass_twiddles(g.logP, twPp);
     g.twPp_elems = (int)twPp.size();
-    if (g.pow2P && P >= 64 && P <= 128)   // k1_fft_dif: compact pass-A twiddles, column-major [i][n2]
+    if (g.pow2P && P >= 64 && P <= 256)   // k1_fft_dif (k1_dif: P = 64 .. 256): compact pass-A twiddles, column-major [i][n2]
         for (int i = 0; i < 4; ++i)
             for (int n2 = 0; n2 < P / 16; ++n2) twD.push_back(root_of_unity((long long)n2 << i, P));
     for (int i = 0; i < P; ++i) twP[i] = root_of_unity(i, P);
