@@ -83,7 +83,7 @@ struct Geometry {
     int rqR, rqQ, twq_elems;
     int nseg, njobs, nwg_k2;
     // complex points of LDS rows per pulse-compression workgroup: RSP_K2_POINTS, or 2560 in a
-    // complex-double plan with a 2560-point block (3 workgroups per CU: 53.5 KB of LDS each);
+    // complex-double plan with a 2560-point block (4 workgroups per CU: 40 KB of LDS each, no pads);
     // power-of-two blocks then take 2048 / M rows
     int k2_pts;
     int cfar_RT, cfar_hR, cfar_W;

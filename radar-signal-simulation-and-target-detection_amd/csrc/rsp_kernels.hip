@@ -1476,6 +1476,12 @@ __device__ __forceinline__ ZWin zrow_window(const Geometry& g, const V* z, int r
 // onto lane 12's bank), and the stride-16 stores of the two radix-16 Ns = 1 passes 2-way
 // (tools/ab/lds_conflicts64.py)
 template <class T> constexpr int k2_sh() { return 5; }
+// The 2560-point-sized workgroups (k2_pc<double, 4>): rows without pads and twiddles read from
+// L1/L2, so that a workgroup's LDS is the 2560 complex doubles of its row alone (40 KB) and 4 fit a
+// CU; SH = 30 makes every pad expression zero.  Measured against 3 per CU with pads and staged
+// twiddles: k2_pc -3 % at x2 (profiles/r06zf_k2_w4_ab.txt)
+constexpr int K2_NOPAD_SH = 30;
+template <class T, bool NOPAD> constexpr int k2_sh_np() { return NOPAD ? K2_NOPAD_SH : k2_sh<T>(); }
 // LDS complex slots of a workgroup's rows: pts points (Geometry::k2_pts) + their pads
 __host__ __device__ constexpr int k2_lds_data(int pts, int sh) { return pts + (pts >> sh); }
 
@@ -1551,12 +1557,12 @@ __device__ __forceinline__ void k2_apply_h(V (&x)[R], __amdgpu_buffer_rsrc_t hr,
 // reverse order, so that pass has the same butterflies) run in registers back to back;
 // the inverse FFT's last pass stores the kept gates to HBM.  2 (log2 M / 4) round trips
 // instead of 2 (log2 M / 4) + 3.  Twiddles are compact rows, staged in LDS.
-template <class T, int LGM, int PTS, bool EPI>
+template <class T, int LGM, int PTS, bool EPI, bool NOPAD>
 __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k, const SegDesc& sd, const K2Job& job,
                                            const cx<T>* __restrict__ z, cx<T>* __restrict__ rdm, T* __restrict__ mag,
                                            int row0, int rows_total, cx<T>* L) {
     typedef cx<T> V;
-    constexpr int SH = k2_sh<T>();
+    constexpr int SH = k2_sh_np<T, NOPAD>();
     constexpr int M = 1 << LGM;
     constexpr int rows = PTS / M > 0 ? PTS / M : 1;
     constexpr int rs = M + (M >> SH);
@@ -1639,7 +1645,7 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     constexpr int NTWF = tw_total(LGM, false, CMP, PAL);
     // twiddles staged in LDS next to the rows; a 4096-point block's (1 088 entries) do not fit the
     // 2-per-CU workgroup's LDS and are read from L1/L2 instead
-    constexpr bool TW_LDS = LGM <= 11;
+    constexpr bool TW_LDS = LGM <= 11 && !NOPAD;
     V* twL = L + k2_lds_data(g.k2_pts, SH);
     if constexpr (TW_LDS)
         for (int e = tid; e < k2_tw_lds(LGM); e += K2_THREADS) twL[e] = twl[e];   // visible after the pass-0 barrier
@@ -1718,12 +1724,12 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
 //  - 1024 = 8 x 16 x 8 in workgroups sized for 2048 points (the 3-per-CU plans): two rows, and
 //    the three Ns = 1 / fused / last passes run 2 x 128 radix-8 butterflies on all 256 threads;
 //    as 16 x 4 x 16 those passes ran 2 x 64 radix-16 butterflies on half of them.
-template <class T, int M, int R0, int R1, bool EPI>
+template <class T, int M, int R0, int R1, bool EPI, bool NOPAD>
 __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConsts& k, const SegDesc& sd, const K2Job& job,
                                                const cx<T>* __restrict__ z, cx<T>* __restrict__ rdm, T* __restrict__ mag,
                                                int row0, int rows_total, cx<T>* L) {
     typedef cx<T> V;
-    constexpr int SH = k2_sh<T>();
+    constexpr int SH = k2_sh_np<T, NOPAD>();
     static_assert(M == R0 * R1 * R0, "palindromic 3-pass plan");
     constexpr int rows = M >= 2048 ? 1 : 2048 / M;
     constexpr int rs = M + (M >> SH);
@@ -1744,7 +1750,8 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
     const V* __restrict__ H = static_cast<const V*>(k.H);
     static_assert(NB0 == 1, "one radix-R0 butterfly per thread");
     static_assert(rows == 1 || nb0 % 64 == 0, "a row per whole wave (its z window is a scalar resource)");
-    static_assert(!EPI || rows * rs + NTWF <= k2_lds_data(2560, SH) + k2_tw_lds_max(), "fits the 3-per-CU LDS");
+    static_assert(!NOPAD || rows * rs <= 2560, "the row alone fills the 4-per-CU workgroup's LDS");
+    static_assert(NOPAD || rows * rs + NTWF <= k2_lds_data(RSP_K2_POINTS, SH) + k2_tw_lds_max(), "fits the 2-per-CU LDS");
     V v0[NB0][R0];
     V hreg[EPI ? 1 : NB0][R0];   // !EPI: the fused pass's H, loaded with the samples
     // threads past the rows' butterflies (waves past them) skip the loads; a row's samples are one
@@ -1770,8 +1777,9 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
         }
     }
     V* twL = L + k2_lds_data(g.k2_pts, SH);
-    for (int e = threadIdx.x; e < NTWF; e += K2_THREADS) twL[e] = twl[e];
-    const V* twF = twL;
+    if constexpr (!NOPAD)
+        for (int e = threadIdx.x; e < NTWF; e += K2_THREADS) twL[e] = twl[e];
+    const V* twF = NOPAD ? twl : twL;
     const V* twI = twF;   // palindrome: the reversed plan's table is the forward one
     constexpr int XZ = R0 == 16 ? 1 : 0;   // Ns = 1 outputs XOR-swizzled (see sh_store)
     shg_store<R0, false, NB0, SH, K2_THREADS, M, 1, XZ>(v0, rs, rows, StoreLds<V>{L}, tid);
@@ -1817,15 +1825,18 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
     }
 }
 
-// k2_pc<T, WGS>: sized for WGS workgroups per CU.  WGS = 3 (a complex-double plan with a
-// 2560-point block, Geometry::k2_pts = 2560: 53.5 KB of LDS and <= 168 VGPRs per workgroup) runs
-// the blocks with EPI (the filter spectrum loaded after the forward DFT, the kept gates stored by
-// k2_epilogue): without them the last pass peaks at 188 VGPRs.  WGS = 2 (4096-point workgroups,
-// 76 KB of LDS) keeps H in registers from the start and stores the gates from the last pass,
-// which measured faster at that occupancy (x2 at 2 per CU: 225 vs 248 us per 8 frames).
+// k2_pc<T, WGS>: sized for WGS workgroups per CU.  WGS = 4 (a complex-double plan with a
+// 2560-point block, Geometry::k2_pts = 2560: the row's 40 KB of LDS alone -- no pads, twiddles
+// from L1/L2 (NOPAD) -- and 128 VGPRs per lane) runs the blocks with EPI (the filter spectrum loaded
+// after the forward DFT, the kept gates stored by k2_epilogue): without them the last pass peaks
+// at 188 VGPRs.  (Round 5's 3 per CU with pads and staged twiddles, 53.5 KB: 3 % slower.)
+// WGS = 2 (4096-point workgroups, 76 KB of LDS) keeps H in registers from the start and stores
+// the gates from the last pass, which measured faster at that occupancy (x2 at 2 per CU: 225 vs
+// 248 us per 8 frames).
 template <class T, int WGS>
 __global__ __launch_bounds__(K2_THREADS, WGS) void k2_pc(Geometry g, DevConsts k, FramePtrs fp, int rows_total) {
     constexpr bool EPI = WGS >= 3;
+    constexpr bool NOPAD = WGS == 4;
     typedef cx<T> V;
     V* L = reinterpret_cast<V*>(rsp_lds);   // overlap-save rows | narrow: staged rows + taps
     const int f = blockIdx.y;
@@ -1846,26 +1857,27 @@ __global__ __launch_bounds__(K2_THREADS, WGS) void k2_pc(Geometry g, DevConsts k
     K2_TAG((unsigned long long)(sd.type * 16 + sd.logM));
 
     if (sd.type == 1 && sd.logM == 0) {   // mixed-radix block
-        k2_fft_job_mix<T, 2560, 16, 10, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L);
+        k2_fft_job_mix<T, 2560, 16, 10, EPI, NOPAD>(g, k, sd, job, z, rdm, mag, row0, rows_total, L);
     } else if (sd.type == 1) {
         if constexpr (WGS >= 3) {   // workgroups sized for the 2560-point block: 2048 points of 2^k rows
+            static_assert(2048 <= 2560, "2^k rows in the 2560-point workgroup");
             switch (sd.logM) {
-                case 6: k2_fft_job<T, 6, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-                case 7: k2_fft_job<T, 7, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-                case 8: k2_fft_job<T, 8, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-                case 9: k2_fft_job<T, 9, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-                case 10: k2_fft_job<T, 10, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-                default: k2_fft_job<T, 11, 2048, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                case 6: k2_fft_job<T, 6, 2048, EPI, NOPAD>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                case 7: k2_fft_job<T, 7, 2048, EPI, NOPAD>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                case 8: k2_fft_job<T, 8, 2048, EPI, NOPAD>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                case 9: k2_fft_job<T, 9, 2048, EPI, NOPAD>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                case 10: k2_fft_job<T, 10, 2048, EPI, NOPAD>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                default: k2_fft_job<T, 11, 2048, EPI, NOPAD>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
             }
         } else {
             switch (sd.logM) {
-                case 6: k2_fft_job<T, 6, RSP_K2_POINTS, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-                case 7: k2_fft_job<T, 7, RSP_K2_POINTS, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-                case 8: k2_fft_job<T, 8, RSP_K2_POINTS, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-                case 9: k2_fft_job<T, 9, RSP_K2_POINTS, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-                case 10: k2_fft_job<T, 10, RSP_K2_POINTS, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-                case 11: k2_fft_job<T, 11, RSP_K2_POINTS, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
-                default: k2_fft_job<T, 12, RSP_K2_POINTS, EPI>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                case 6: k2_fft_job<T, 6, RSP_K2_POINTS, EPI, NOPAD>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                case 7: k2_fft_job<T, 7, RSP_K2_POINTS, EPI, NOPAD>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                case 8: k2_fft_job<T, 8, RSP_K2_POINTS, EPI, NOPAD>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                case 9: k2_fft_job<T, 9, RSP_K2_POINTS, EPI, NOPAD>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                case 10: k2_fft_job<T, 10, RSP_K2_POINTS, EPI, NOPAD>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                case 11: k2_fft_job<T, 11, RSP_K2_POINTS, EPI, NOPAD>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
+                default: k2_fft_job<T, 12, RSP_K2_POINTS, EPI, NOPAD>(g, k, sd, job, z, rdm, mag, row0, rows_total, L); break;
             }
         }
     } else {
@@ -2785,13 +2797,15 @@ hipError_t launch_k1(const Geometry& g, const DevConsts& k, const FramePtrs& fp,
 template <class T>
 static hipError_t launch_k2_p(const Geometry& g, const DevConsts& k, const FramePtrs& fp, int nf, int rows,
                               hipStream_t s) {
-    const size_t lds = (size_t)(k2_lds_data(g.k2_pts, k2_sh<T>()) + k2_tw_lds_max()) * sizeof(cx<T>);
-    const bool w3 = g.k2_pts != RSP_K2_POINTS;   // workgroups sized for the 2560-point block: 3 per CU
-    hipError_t e = w3 ? allow_lds(k2_pc<T, 3>, lds) : allow_lds(k2_pc<T, 2>, lds);
+    // workgroups sized for the 2560-point block (complex double): 4 per CU, the row's LDS alone
+    const bool w4 = g.k2_pts != RSP_K2_POINTS;
+    const size_t lds = w4 ? (size_t)g.k2_pts * sizeof(cx<T>)
+                          : (size_t)(k2_lds_data(g.k2_pts, k2_sh<T>()) + k2_tw_lds_max()) * sizeof(cx<T>);
+    hipError_t e = w4 ? allow_lds(k2_pc<T, 4>, lds) : allow_lds(k2_pc<T, 2>, lds);
     if (e != hipSuccess) return e;
     if (g.nwg_k2 > 0) {
-        if (w3)
-            hipLaunchKernelGGL((k2_pc<T, 3>), dim3(g.nwg_k2, nf), dim3(K2_THREADS), lds, s, g, k, fp, rows);
+        if (w4)
+            hipLaunchKernelGGL((k2_pc<T, 4>), dim3(g.nwg_k2, nf), dim3(K2_THREADS), lds, s, g, k, fp, rows);
         else
             hipLaunchKernelGGL((k2_pc<T, 2>), dim3(g.nwg_k2, nf), dim3(K2_THREADS), lds, s, g, k, fp, rows);
     }

@@ -932,8 +932,8 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
         p->segs.push_back(s);
     }
     // K2 workgroup size in LDS points: a complex-double plan with a 2560-point block sizes every
-    // workgroup for it (53.5 KB of LDS: 3 per CU, k2_pc's 168-VGPR budget), power-of-two blocks
-    // then holding 2048 / M rows; otherwise RSP_K2_POINTS (4096: 2 per CU in complex double)
+    // workgroup for it (40 KB of LDS, no pads: 4 per CU, k2_pc's 128-VGPR budget), power-of-two
+    // blocks then holding 2048 / M rows; otherwise RSP_K2_POINTS (4096: 2 per CU in complex double)
     g.k2_pts = RSP_K2_POINTS;
     for (auto& s : p->segs)
         if (f64 && s.type == 1 && s.M == 2560) g.k2_pts = RSP_K2_MIXPTS;
@@ -945,7 +945,7 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
     for (auto& s : p->segs)
         if (s.type == 0 && g.k2_pts != RSP_K2_POINTS) {
             const int WP = s.hi - s.lo + 1 + s.ntaps - 1;
-            if (WP + (s.ntaps + 1) / 2 > g.k2_pts + (g.k2_pts >> 5)) g.k2_pts = RSP_K2_POINTS;
+            if (WP + (s.ntaps + 1) / 2 > g.k2_pts) g.k2_pts = RSP_K2_POINTS;   // no pads at 2560
         }
     for (auto& s : p->segs) {
         if (s.seg_lo < 0 || s.seg_lo >= N) return bail(fail(RSP_ERR_INVALID, "segment start out of range"));
@@ -957,7 +957,7 @@ int32_t rsp_plan_create_ex(const rsp_sig_config* cfg, const rsp_cfar_params* cfa
             // up to 8 rows per workgroup (measured best of 1/2/4/8 at x2), within the workgroup's
             // LDS: rows * WP complex + the taps (ntaps reals = ntaps / 2 complex)
             const int WP = s.hi - s.lo + 1 + s.ntaps - 1;   // staged row: ntaps - 1 leading zeros
-            const int lds_c = g.k2_pts + (g.k2_pts >> 5);
+            const int lds_c = g.k2_pts == RSP_K2_POINTS ? g.k2_pts + (g.k2_pts >> 5) : g.k2_pts;   // k2_pc's LDS
             s.rows_per_wg = std::max(1, std::min(8, (lds_c - (s.ntaps + 1) / 2) / WP));
             if (WP * s.rows_per_wg + (s.ntaps + 1) / 2 > lds_c)
                 return bail(fail(RSP_ERR_UNSUPPORTED, "narrow segment window %d samples too long", s.hi - s.lo + 1));

@@ -1,8 +1,8 @@
 """K2's overlap-save block sizes beside the 2560-point long block.
 
 x2 is the only named configuration whose long segment takes the mixed-radix 2560-point block, and
-such a plan sizes every K2 workgroup for it (3 per CU, k2_pc<double, 3>): its power-of-two blocks
-then run the 2048-point-workgroup instantiations (2048 / M rows per workgroup).  x2's medium
+such a plan sizes every K2 workgroup for it (4 per CU, k2_pc<double, 4>: 40 KB of LDS, no pads,
+twiddles from L1/L2): its power-of-two blocks then run the 2048-point-workgroup instantiations (2048 / M rows per workgroup).  x2's medium
 segment exercises only M = 1024 there.  These configurations keep x2's long segment (28 us pulse,
 1860 gates: one 2560-point block) and shorten or lengthen the medium pulse and gate count
 (fun_process_single_frame.m:115-116 with N_fft / MF_medium_fft from
