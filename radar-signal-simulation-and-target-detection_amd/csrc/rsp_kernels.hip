@@ -85,13 +85,29 @@ __device__ __forceinline__ double cmag(d2 x) {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, unsigned bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
-template <class V> __device__ V buf_ld(__amdgpu_buffer_rsrc_t r, unsigned off);
-template <> __device__ __forceinline__ f2 buf_ld<f2>(__amdgpu_buffer_rsrc_t r, unsigned off) {
-    return __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+// AUX: cache-policy bits of the load (2 = non-temporal)
+template <class V, int AUX = 0> __device__ __forceinline__ V buf_ld(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    static_assert(sizeof(V) == 8 || sizeof(V) == 16, "one complex sample");
+    if constexpr (sizeof(V) == 8)
+        return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, AUX));
+    else
+        return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, AUX));
 }
-template <> __device__ __forceinline__ d2 buf_ld<d2>(__amdgpu_buffer_rsrc_t r, unsigned off) {
-    return __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
-}
+// A twiddle table in global memory read through a buffer resource: tw + e advances the per-lane
+// byte offset, tw[i] (i a constant after unrolling) goes to the instruction's scalar offset, so
+// the lgR loads of a butterfly share one offset VGPR instead of a 64-bit address each.
+template <class V>
+struct TwG {
+    __amdgpu_buffer_rsrc_t r;
+    unsigned off;
+    __device__ __forceinline__ TwG operator+(int e) const { return TwG{r, off + (unsigned)e * (unsigned)sizeof(V)}; }
+    __device__ __forceinline__ V operator[](int i) const {
+        if constexpr (sizeof(V) == 8)
+            return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, i * (int)sizeof(V), 0));
+        else
+            return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, i * (int)sizeof(V), 0));
+    }
+};
 // AUX: cache-policy bits of the store (2 = non-temporal)
 template <int AUX = 0>
 __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, unsigned off, f2 x) {
@@ -323,8 +339,8 @@ template <class V> struct StoresLds<StoreLds<V>> { static constexpr bool value =
 // powers formed as products of at most lgR - 1 of them.  Column-major so that the lanes of a
 // pass (consecutive k) read consecutive 16-B entries: conflict-free, where [k][i] rows of 4
 // entries put every 4th lane on the same banks (tools/ab/lds_conflicts_k2v2.py).
-template <int R, bool INV, bool CMP, int NS, class V>
-__device__ __forceinline__ void load_tw(const V* twk, V (&w)[R]) {
+template <int R, bool INV, bool CMP, int NS, class V, class TW>
+__device__ __forceinline__ void load_tw(const TW& twk, V (&w)[R]) {
     if constexpr (!CMP) {
 #pragma unroll
         for (int r = 1; r < R; ++r) {
@@ -402,8 +418,8 @@ constexpr int tw_total(int LG, bool rev = false, bool cmp = false, bool pal = fa
 // With power-of-two nb, Ns and pads every 2^SH, lidx(j + r nb) = lidx(j) + r nb + ((r nb) >> SH)
 // and lidx(idxD + r Ns) = lidx(idxD) + r Ns + ((r Ns) >> SH): every LDS address of a butterfly
 // is a per-thread base plus a compile-time offset (ds_read/ds_write immediate offsets).
-template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP = false, int XL = 0, class V>
-__device__ __forceinline__ void sh_load(const V* buf, int rs, int nrows, const V* tw, V (&v)[NB][R]) {
+template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP = false, int XL = 0, class V, class TW>
+__device__ __forceinline__ void sh_load(const V* buf, int rs, int nrows, const TW& tw, V (&v)[NB][R]) {
     constexpr int lgR = clog2(R);
     constexpr int lgnb = LGL - lgR;
     constexpr int nb = 1 << lgnb;
@@ -466,8 +482,8 @@ __device__ __forceinline__ void sh_store(V (&v)[NB][R], int rs, int nrows, const
 
 // TAIL = false: no barrier after the pass (the caller's next LDS writes go to other rows).
 template <int R, bool INV, int NB, int SH, int NTHR, int LGL, int LGNS, bool CMP, int XL = 0, bool TAIL = true, class V,
-          class St>
-__device__ __forceinline__ void sh_pass(V* buf, int rs, int nrows, const V* tw, const St& st) {
+          class TW, class St>
+__device__ __forceinline__ void sh_pass(V* buf, int rs, int nrows, const TW& tw, const St& st) {
     V v[NB][R];
     sh_load<R, INV, NB, SH, NTHR, LGL, LGNS, CMP, XL>(buf, rs, nrows, tw, v);
     if constexpr (StoresLds<St>::value) RSP_WAR_SYNC();
@@ -479,14 +495,14 @@ __device__ __forceinline__ void sh_pass(V* buf, int rs, int nrows, const V* tw, 
 // pass n_passes - 1 stores through `last`, the others through `mid`.  tw = this plan's
 // concatenated tables.  PTS = complex points per thread (nrows * L / NTHR).
 template <int LG, int Q, int QEND, int LGNS, int PTS, bool INV, bool REV, int SH, int NTHR, bool CMP, bool PAL = false,
-          int XIN = 0, bool TAIL = true, class V, class StMid, class StLast>
-__device__ __forceinline__ void fft_range(V* buf, int rs, int nrows, const V* tw, const StMid& mid, const StLast& last) {
+          int XIN = 0, bool TAIL = true, class V, class TW, class StMid, class StLast>
+__device__ __forceinline__ void fft_range(V* buf, int rs, int nrows, const TW& tw, const StMid& mid, const StLast& last) {
     constexpr int NP = n_passes(LG);
     if constexpr (Q < QEND) {
         constexpr int RB = rad_bits_p(LG, Q, REV, PAL);
         constexpr int R = 1 << RB;
         constexpr int NB = (PTS + R - 1) / R;
-        const V* twq = tw + tw_pass_off(LG, Q, REV, CMP, PAL);
+        const auto twq = tw + tw_pass_off(LG, Q, REV, CMP, PAL);
         if constexpr (Q == NP - 1)
             sh_pass<R, INV, NB, SH, NTHR, LG, LGNS, CMP, XIN, TAIL>(buf, rs, nrows, twq, last);
         else
@@ -521,8 +537,8 @@ constexpr int lidx_off(int r) {
     return r * D + (SH ? (r * D) >> SH : 0);
 }
 
-template <int R, bool INV, int NB, int SH, int NTHR, int L, int NS, bool CMP, int XL = 0, class V>
-__device__ __forceinline__ void shg_load(const V* buf, int rs, int nrows, const V* tw, V (&v)[NB][R],
+template <int R, bool INV, int NB, int SH, int NTHR, int L, int NS, bool CMP, int XL = 0, class V, class TW>
+__device__ __forceinline__ void shg_load(const V* buf, int rs, int nrows, const TW& tw, V (&v)[NB][R],
                                          int tix = threadIdx.x) {
     constexpr int nb = L / R;
     static_assert(!XL || nb % 128 == 0, "XOR-swizzled input needs r nb to keep the swizzle bits");
@@ -573,8 +589,8 @@ __device__ __forceinline__ void shg_store(V (&v)[NB][R], int rs, int nrows, cons
         }
     }
 }
-template <int R, bool INV, int NB, int SH, int NTHR, int L, int NS, bool CMP, int XL = 0, class V, class St>
-__device__ __forceinline__ void shg_pass(V* buf, int rs, int nrows, const V* tw, const St& st) {
+template <int R, bool INV, int NB, int SH, int NTHR, int L, int NS, bool CMP, int XL = 0, class V, class TW, class St>
+__device__ __forceinline__ void shg_pass(V* buf, int rs, int nrows, const TW& tw, const St& st) {
     V v[NB][R];
     shg_load<R, INV, NB, SH, NTHR, L, NS, CMP, XL>(buf, rs, nrows, tw, v);
     RSP_WAR_SYNC();
@@ -1557,6 +1573,15 @@ __device__ __forceinline__ void k2_apply_h(V (&x)[R], __amdgpu_buffer_rsrc_t hr,
 // reverse order, so that pass has the same butterflies) run in registers back to back;
 // the inverse FFT's last pass stores the kept gates to HBM.  2 (log2 M / 4) round trips
 // instead of 2 (log2 M / 4) + 3.  Twiddles are compact rows, staged in LDS.
+// The twiddle source of a K2 job: the LDS copy, or the plan's table in global memory through a
+// buffer resource (TwG; x4 k2_pc 2.355 -> 2.347 ms against 64-bit addresses, r06zg)
+template <bool LDS, class V>
+__device__ __forceinline__ auto k2_tw_src(const V* lds, const V* glob) {
+    if constexpr (LDS)
+        return lds;
+    else
+        return TwG<V>{buf_rsrc(glob, RSP_OOB), 0u};
+}
 template <class T, int LGM, int PTS, bool EPI, bool NOPAD>
 __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k, const SegDesc& sd, const K2Job& job,
                                            const cx<T>* __restrict__ z, cx<T>* __restrict__ rdm, T* __restrict__ mag,
@@ -1649,8 +1674,8 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
     V* twL = L + k2_lds_data(g.k2_pts, SH);
     if constexpr (TW_LDS)
         for (int e = tid; e < k2_tw_lds(LGM); e += K2_THREADS) twL[e] = twl[e];   // visible after the pass-0 barrier
-    const V* twF = TW_LDS ? twL : twl;
-    const V* twI = k2_tw_sym(LGM) ? twF : twF + NTWF;
+    const auto twF = k2_tw_src<TW_LDS, V>(twL, twl);
+    const auto twI = k2_tw_sym(LGM) ? twF : twF + NTWF;
     // forward pass 0 (Ns = 1, no twiddles) straight from the loaded samples
     // the Ns = 1 passes' outputs XOR-swizzled (sh_store) when a middle pass reads them (3 passes)
     constexpr int XZ = (NP == 3 && R0 == 16 && RL == 16 && 1) ? 1 : 0;
@@ -1696,7 +1721,7 @@ __device__ __forceinline__ void k2_fft_job(const Geometry& g, const DevConsts& k
                                                                                    StoreLds<V>{L});
         constexpr int LGNSL = LGM - RB0;
         static_assert(NP >= 3 || XZ == 0, "last pass input is never swizzled");
-        const V* twl_last = twI + tw_pass_off(LGM, NP - 1, true, CMP, PAL);
+        const auto twl_last = twI + tw_pass_off(LGM, NP - 1, true, CMP, PAL);
         const int rho = row0 + __builtin_amdgcn_readfirstlane(tid / nb0);
         if (rdm)
             sh_pass<R0, true, NB0, SH, K2_THREADS, LGM, LGNSL, CMP, 0, false>(
@@ -1779,8 +1804,8 @@ __device__ __forceinline__ void k2_fft_job_mix(const Geometry& g, const DevConst
     V* twL = L + k2_lds_data(g.k2_pts, SH);
     if constexpr (!NOPAD)
         for (int e = threadIdx.x; e < NTWF; e += K2_THREADS) twL[e] = twl[e];
-    const V* twF = NOPAD ? twl : twL;
-    const V* twI = twF;   // palindrome: the reversed plan's table is the forward one
+    const auto twF = k2_tw_src<!NOPAD, V>(twL, twl);
+    const auto twI = twF;   // palindrome: the reversed plan's table is the forward one
     constexpr int XZ = R0 == 16 ? 1 : 0;   // Ns = 1 outputs XOR-swizzled (see sh_store)
     shg_store<R0, false, NB0, SH, K2_THREADS, M, 1, XZ>(v0, rs, rows, StoreLds<V>{L}, tid);
     __syncthreads();
